@@ -1,0 +1,444 @@
+"""CPU ORACLE of the observation path -- TEST INFRASTRUCTURE ONLY.
+
+A restatement (numpy + the plain-C kernels in oracle_c.c) of the reference's
+Mapper.get_state / OccupancyMap.update / GridGraph path (envs.py:2010-2555,
+shortest_paths/shortest_paths.pyx) and of the third-party arithmetic it calls
+(scipy.ndimage.rotate / distance_transform_edt / binary_dilation / grey_dilation,
+skimage.draw.line, skimage.morphology.disk, numpy.linspace).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module,
+and only as the checker / the timed CPU baseline; the product (spatial-intention-maps_amd/)
+never does.  Pinned: every primitive and the whole per-agent state are checked bit-for-bit
+against tests/golden/*.npz, which tests/golden/make_goldens.py produced by running the
+reference's own code (scipy 1.7.1, scikit-image 0.18.3, Cython SPFA compiled from
+/root/reference) -- see tests/test_oracle_golden.py.
+"""
+import ctypes
+import math
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, 'spatial-intention-maps_amd'))
+from simaps import constants as K  # noqa: E402
+from simaps import synthetic  # noqa: E402
+
+PPM = K.LOCAL_MAP_PIXELS_PER_METER
+LW = K.LOCAL_MAP_PIXEL_WIDTH
+
+_lib = None
+
+
+def lib():
+    """liboracle.so (built by `make -C oracle`, or here on first use)."""
+    global _lib
+    if _lib is None:
+        so = os.path.join(HERE, 'liboracle.so')
+        src = os.path.join(HERE, 'oracle_c.c')
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            subprocess.check_call(['make', '-s', '-C', HERE, 'oracle'])
+        L = ctypes.CDLL(so)
+        u8p, i32p, f32p = (np.ctypeslib.ndpointer(t, flags='C') for t in (np.uint8, np.int32, np.float32))
+        L.oracle_spfa.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f32p, i32p]
+        L.oracle_spfa.restype = ctypes.c_int
+        L.oracle_edt_ft.argtypes = [u8p, ctypes.c_int, ctypes.c_int, i32p]
+        L.oracle_edt_ft.restype = None
+        L.oracle_sindg.argtypes = [ctypes.c_double]
+        L.oracle_sindg.restype = ctypes.c_double
+        L.oracle_cosdg.argtypes = [ctypes.c_double]
+        L.oracle_cosdg.restype = ctypes.c_double
+        L.oracle_rotate_params.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
+        L.oracle_rotate_params.restype = None
+        _lib = L
+    return _lib
+
+
+# ---------------------------------------------------------------------------------------------
+# Primitives
+# ---------------------------------------------------------------------------------------------
+def cosdg(x):
+    return lib().oracle_cosdg(float(x))
+
+
+def sindg(x):
+    return lib().oracle_sindg(float(x))
+
+
+def spfa_image(grid_u8, source):
+    """GridGraph(grid).shortest_path_image(source) (pyx:165-167): f32 (H, W), -1 unreachable."""
+    grid = np.ascontiguousarray(grid_u8, dtype=np.uint8)
+    H, W = grid.shape
+    d = np.empty(H * W, dtype=np.float32)
+    p = np.empty(H * W, dtype=np.int32)
+    rc = lib().oracle_spfa(grid.ravel(), H, W, int(source[0]), int(source[1]), d, p)
+    if rc != 0:
+        raise RuntimeError('oracle SPFA queue overflow')
+    return d.reshape(H, W)
+
+
+def edt_indices(img):
+    """scipy.ndimage.distance_transform_edt(img, return_distances=False, return_indices=True)."""
+    a = np.ascontiguousarray(img != 0, dtype=np.uint8)
+    H, W = a.shape
+    ft = np.empty((2, H, W), dtype=np.int32)
+    lib().oracle_edt_ft(a.ravel(), H, W, ft.reshape(-1))
+    return ft
+
+
+def rotate_params(n, angle):
+    """scipy.ndimage.rotate(reshape=True) geometry for an n x n input (scipy interpolation.py:909-930).
+
+    Returns (S0, S1, (c, s), offset) -- see oracle_rotate_params in oracle_c.c for the exact
+    rounding (out_center pinned to the oracle host's BLAS FMA by tests/golden/rotate.npz)."""
+    out = (ctypes.c_double * 6)()
+    lib().oracle_rotate_params(int(n), float(angle), out)
+    return int(out[0]), int(out[1]), (out[2], out[3]), (out[4], out[5])
+
+
+def rotate_index_map(n, angle):
+    """Order-0 rotate as an index map: (src_i, src_j, valid) arrays of the output shape.
+
+    Output pixel o takes input[floor(src + 0.5)] when 0 <= src <= n-1 on both axes, else cval,
+    src = (o0*M[r][0] + o1*M[r][1]) + offset[r] (scipy ni_interpolation.c geometric transform)."""
+    S0, S1, (c, s), (f0, f1) = rotate_params(n, angle)
+    o0 = np.arange(S0, dtype=np.float64)[:, None]
+    o1 = np.arange(S1, dtype=np.float64)[None, :]
+    src0 = (o0 * c + o1 * s) + f0
+    src1 = (o0 * (-s) + o1 * c) + f1
+    valid = (src0 >= 0) & (src0 <= n - 1) & (src1 >= 0) & (src1 <= n - 1)
+    i0 = np.floor(np.where(valid, src0, 0) + 0.5).astype(np.int64)
+    i1 = np.floor(np.where(valid, src1, 0) + 0.5).astype(np.int64)
+    return i0, i1, valid
+
+
+def rotate(img, angle):
+    """scipy.ndimage.rotate(img, angle, order=0) (reshape=True, cval=0) for square img."""
+    n = img.shape[0]
+    assert img.shape == (n, n)
+    i0, i1, valid = rotate_index_map(n, angle)
+    out = np.zeros(i0.shape, dtype=img.dtype)
+    out[valid] = img[i0[valid], i1[valid]]
+    return out
+
+
+def line(r0, c0, r1, c1):
+    """skimage.draw.line (Bresenham, skimage/draw/_draw.pyx _line), restated loop-for-loop."""
+    steep = 0
+    r, c = r0, c0
+    dr, dc = abs(r1 - r0), abs(c1 - c0)
+    sc = 1 if (c1 - c) > 0 else -1
+    sr = 1 if (r1 - r) > 0 else -1
+    if dr > dc:
+        steep = 1
+        c, r = r, c
+        dc, dr = dr, dc
+        sc, sr = sr, sc
+    d = (2 * dr) - dc
+    rr = np.zeros(max(dc, dr) + 1, dtype=np.intp)
+    cc = np.zeros(max(dc, dr) + 1, dtype=np.intp)
+    for i in range(dc):
+        if steep:
+            rr[i], cc[i] = c, r
+        else:
+            rr[i], cc[i] = r, c
+        while d >= 0:
+            r = r + sr
+            d = d - (2 * dc)
+        c = c + sc
+        d = d + (2 * dr)
+    rr[dc] = r1
+    cc[dc] = c1
+    return rr, cc
+
+
+def linspace(start, stop, num):
+    """numpy.linspace(start, stop, num) for python-float endpoints (numpy function_base.py):
+    y[t] = t*step + start (two fp64 roundings), y[-1] = stop; num == 1 -> [start]."""
+    div = num - 1
+    y = np.arange(0, num, dtype=np.float64)
+    delta = stop - start
+    if div > 0:
+        step = delta / div
+        if step == 0:
+            y = (y / div) * delta
+        else:
+            y = y * step
+    else:
+        y = y * delta
+    y += start
+    if num > 1:
+        y[-1] = stop
+    return y
+
+
+def disk(radius):
+    """skimage.morphology.disk (selem.py): x^2 + y^2 <= r^2 on the integer grid."""
+    L = np.arange(-radius, radius + 1)
+    X, Y = np.meshgrid(L, L)
+    return np.array((X ** 2 + Y ** 2) <= radius ** 2, dtype=np.uint8)
+
+
+def binary_dilation(img, selem):
+    """ndi.binary_dilation(img, structure=selem) for a symmetric selem, border 0."""
+    H, W = img.shape
+    r = selem.shape[0] // 2
+    src = np.zeros((H + 2 * r, W + 2 * r), dtype=bool)
+    src[r:r + H, r:r + W] = img != 0
+    out = np.zeros((H, W), dtype=bool)
+    for di, dj in np.argwhere(selem):
+        out |= src[di:di + H, dj:dj + W]
+    return out
+
+
+def grey_dilation_cross(img):
+    """skimage.morphology.dilation(img, disk(1)) = ndi.grey_dilation, 'reflect' border: the
+    out-of-image neighbour reflects to the edge pixel itself, which is already in the max."""
+    out = img.copy()
+    out[1:, :] = np.maximum(out[1:, :], img[:-1, :])
+    out[:-1, :] = np.maximum(out[:-1, :], img[1:, :])
+    out[:, 1:] = np.maximum(out[:, 1:], img[:, :-1])
+    out[:, :-1] = np.maximum(out[:, :-1], img[:, 1:])
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Mapper geometry helpers (envs.py:2383-2407)
+# ---------------------------------------------------------------------------------------------
+def position_to_pixel_indices(x, y, shape):
+    pi = int(np.floor(shape[0] / 2 - y * PPM))
+    pj = int(np.floor(shape[1] / 2 + x * PPM))
+    return min(max(pi, 0), shape[0] - 1), min(max(pj, 0), shape[1] - 1)
+
+
+def pixel_indices_to_position(i, j, shape):
+    return ((j + 0.5) - shape[1] / 2) / PPM, (shape[0] / 2 - (i + 0.5)) / PPM
+
+
+def distance(p1, p2):
+    """envs.py:2557-2558."""
+    return math.sqrt((p2[0] - p1[0]) ** 2 + (p2[1] - p1[1]) ** 2)
+
+
+def robot_mask(robot_type, show_lifted_cube=False):
+    """Mapper._create_robot_mask (envs.py:2218-2242)."""
+    g = K.ROBOT_GEOM[robot_type]
+    width = math.ceil(2 * g['RADIUS'] * PPM)
+    mask = np.zeros((LW, LW), dtype=np.float32)
+    start = math.floor(LW / 2 - width / 2)
+    cube_w = math.ceil(K.CUBE_WIDTH * PPM)
+    for i in range(start - cube_w if show_lifted_cube else start, start + width):
+        for j in range(start, start + width):
+            px, py = pixel_indices_to_position(i, j, mask.shape)
+            in_base = abs(px) <= K.HALF_WIDTH and 0 <= py - K.BACKPACK_OFFSET <= g['BASE_LENGTH']
+            in_backpack = px ** 2 + (py - K.BACKPACK_OFFSET) ** 2 <= K.HALF_WIDTH ** 2
+            if in_base or in_backpack:
+                mask[i, j] = 1
+            if show_lifted_cube:
+                in_cube = (abs(px) <= K.CUBE_WIDTH / 2 and
+                           0 <= py - (K.END_EFFECTOR_LOCATION + K.LIFTED_CUBE_OFFSET) <= K.CUBE_WIDTH)
+                if in_cube:
+                    mask[i, j] = 1
+    return mask
+
+
+def room_mask(shape, room_width, room_length):
+    i0, j0, h, w = K.room_rect(room_width, room_length)
+    m = np.zeros(shape, dtype=np.uint8)
+    m[i0:i0 + h, j0:j0 + w] = 1
+    return m
+
+
+# ---------------------------------------------------------------------------------------------
+# OccupancyMap.update (minus the point scatter) + Mapper.get_state for one agent
+# ---------------------------------------------------------------------------------------------
+class AgentOracle:
+    """One agent's observation state (the reference's per-robot Mapper + OccupancyMap)."""
+
+    def __init__(self, scene, agent):
+        self.scene = scene
+        self.a = agent
+        self.robot = scene['robots'][agent]
+        self.flags = scene['flags']
+        self.H, self.W = scene['H'], scene['W']
+        self.shape = (self.H, self.W)
+        self.occupancy = scene['occupancy'][agent]
+        self.overhead_wo = scene['overhead'][agent]
+        self.receptacle = scene['receptacle_position']
+        self._update()
+
+    # OccupancyMap.update (envs.py:2445-2460), minus the point scatter (occupancy is the input)
+    def _update(self):
+        rm = room_mask(self.shape, self.scene['room_width'], self.scene['room_length'])
+        selem = disk(K.cspace_radius_px(self.robot['type']))
+        dil = binary_dilation(self.occupancy, selem).astype(np.uint8)
+        self.cspace = (1 - np.maximum(1 - rm, dil)).astype(np.uint8)
+        self.closest = edt_indices(1 - self.cspace)
+        self._sp_cache = {}
+
+    def snap(self, pos):
+        pi, pj = position_to_pixel_indices(pos[0], pos[1], self.shape)
+        return int(self.closest[0, pi, pj]), int(self.closest[1, pi, pj])
+
+    def shortest_path_image(self, pos):
+        """OccupancyMap.shortest_path_image (envs.py:2514-2517): dist / 96 in f32."""
+        src = self.snap(pos)
+        if src not in self._sp_cache:
+            self._sp_cache[src] = spfa_image(self.cspace, src)
+        return self._sp_cache[src] / np.float32(PPM)
+
+    def _sp_global(self, pos):
+        g = self.shortest_path_image(pos)
+        g[g < 0] = g.max()
+        g *= np.float32(self.flags['shortest_path_map_scale'])
+        return g
+
+    def _local_map(self, global_map):
+        """Mapper._get_local_map (envs.py:2200-2211)."""
+        cw = K.crop_width()
+        angle = 90 - math.degrees(self.robot['heading'])
+        pi, pj = position_to_pixel_indices(self.robot['position'][0], self.robot['position'][1], global_map.shape)
+        crop = global_map[pi - cw // 2:pi + cw // 2, pj - cw // 2:pj + cw // 2]
+        rc = rotate(crop, angle)
+        return rc[rc.shape[0] // 2 - LW // 2:rc.shape[0] // 2 + LW // 2,
+                  rc.shape[1] // 2 - LW // 2:rc.shape[1] // 2 + LW // 2]
+
+    def _local_distance_map(self, global_map):
+        lm = self._local_map(global_map)
+        lm = lm - lm.min()
+        return lm
+
+    def global_robot_map(self, seg):
+        """Mapper._create_global_robot_map (envs.py:2251-2276)."""
+        gm = np.zeros(self.shape, dtype=np.float32)
+        for r in self.scene['robots']:
+            vis = robot_mask(r['type']).copy()
+            if seg:
+                vis *= np.float32(K.SEG_VALUES['robot_group_%d' % (r['group_index'] + 1)])
+            elif r['type'] == 'lifting_robot':
+                if r['lift_state'] == 'lifting':
+                    vis = robot_mask('lifting_robot', show_lifted_cube=True).copy()
+                else:
+                    vis *= np.float32(0.5)
+            rot = rotate(vis, math.degrees(r['heading']) - 90)
+            pi, pj = position_to_pixel_indices(r['position'][0], r['position'][1], self.shape)
+            si, sj = pi - rot.shape[0] // 2, pj - rot.shape[1] // 2
+            gm[si:si + rot.shape[0], sj:sj + rot.shape[1]] = np.maximum(
+                gm[si:si + rot.shape[0], sj:sj + rot.shape[1]], rot)
+        return gm
+
+    def global_overhead_map(self):
+        """Mapper._create_global_overhead_map (envs.py:2244-2249)."""
+        g = self.overhead_wo.copy()
+        seg = self.global_robot_map(seg=True)
+        g[seg > 0] = seg[seg > 0]
+        assert g.max() <= 1
+        return g
+
+    def global_intention_map(self, encoding):
+        """Mapper._create_global_intention_or_history_map (envs.py:2302-2347)."""
+        f = self.flags
+        gm = np.zeros(self.shape, dtype=np.float32)
+        for k, r in enumerate(self.scene['robots']):
+            if k == self.a or r['idle']:
+                continue
+            if encoding == 'circle':
+                ti, tj = position_to_pixel_indices(r['target_ee'][0], r['target_ee'][1], self.shape)
+                gm[ti, tj] = f['intention_map_scale']
+                continue
+            if encoding in ('ramp', 'binary', 'line'):
+                wps = synthetic.intention_path(r)
+                if encoding == 'line':
+                    wps = [wps[0], wps[-1]]
+            else:  # history
+                wps = synthetic.history_path(r)[::-1]
+            path_length = 0
+            for i in range(1, len(wps)):
+                sp, tp = wps[i - 1], wps[i]
+                seg_len = f['intention_map_scale'] * distance(sp, tp)
+                si, sj = position_to_pixel_indices(sp[0], sp[1], self.shape)
+                ti, tj = position_to_pixel_indices(tp[0], tp[1], self.shape)
+                rr, cc = line(si, sj, ti, tj)
+                if encoding in ('binary', 'line'):
+                    if i < len(wps) - 1:
+                        rr, cc = rr[:-1], cc[:-1]
+                    gm[rr, cc] = f['intention_map_scale']
+                else:
+                    vals = np.clip(linspace(1 - path_length, 1 - (path_length + seg_len), len(rr)), 0, 1)
+                    if i < len(wps) - 1:
+                        rr, cc, vals = rr[:-1], cc[:-1], vals[:-1]
+                    gm[rr, cc] = np.maximum(gm[rr, cc], vals)
+                path_length += seg_len
+        if f['intention_map_line_thickness'] > 1:
+            assert f['intention_map_line_thickness'] == 2, 'oracle restates disk(1) dilation only'
+            gm = grey_dilation_cross(gm)
+        return gm
+
+    def distance_to_receptacle_map(self):
+        """Mapper._create_global_distance_to_receptacle_map (envs.py:2278-2286)."""
+        H, W = self.shape
+        ii, jj = np.meshgrid(np.arange(H), np.arange(W), indexing='ij')
+        px = ((jj + 0.5) - W / 2) / PPM
+        py = (H / 2 - (ii + 0.5)) / PPM
+        dx = self.receptacle[0] - px
+        dy = self.receptacle[1] - py
+        g = np.sqrt(dx * dx + dy * dy).astype(np.float32)
+        g *= np.float32(self.flags['distance_to_receptacle_map_scale'])
+        return g
+
+    def intention_channels(self):
+        """Mapper._get_intention_channels (envs.py:2349-2378)."""
+        f = self.flags
+        me = self.robot
+        dists = [distance(me['position'], r['position']) for r in self.scene['robots']]
+        chans = []
+        for i in np.argsort(dists):
+            r = self.scene['robots'][i]
+            if i == self.a:
+                continue
+            if f['intention_channel_encoding'] == 'spatial':
+                gm = np.zeros(self.shape, dtype=np.float32)
+                if not r['idle']:
+                    ti, tj = position_to_pixel_indices(r['target_ee'][0], r['target_ee'][1], self.shape)
+                    gm[ti, tj] = f['intention_map_scale']
+                    gm = grey_dilation_cross(gm)
+                chans.append(self._local_map(gm))
+            else:
+                rel = (0, 0)
+                if not r['idle']:
+                    d = distance(me['position'], r['target_ee'])
+                    th = me['heading'] - math.atan2(r['target_ee'][1] - me['position'][1],
+                                                    r['target_ee'][0] - me['position'][0])
+                    rel = (d * math.sin(th), d * math.cos(th))
+                for coord in rel:
+                    chans.append(np.full((LW, LW), f['intention_channel_nonspatial_scale'] * coord,
+                                         dtype=np.float32))
+        return chans
+
+    def get_state(self):
+        """Mapper.get_state (envs.py:2068-2113, 2184-2185): (96, 96, C) float32."""
+        f = self.flags
+        ch = [self._local_map(self.global_overhead_map())]
+        if f['use_robot_map']:
+            ch.append(self._local_map(self.global_robot_map(seg=False)))
+        if f['use_distance_to_receptacle_map']:
+            ch.append(self._local_distance_map(self.distance_to_receptacle_map()))
+        if f['use_shortest_path_to_receptacle_map']:
+            ch.append(self._local_distance_map(self._sp_global(self.receptacle)))
+        if f['use_shortest_path_map']:
+            ch.append(self._local_distance_map(self._sp_global(self.robot['position'])))
+        if f['use_history_map']:
+            ch.append(self._local_map(self.global_intention_map('history')))
+        if f['use_intention_map']:
+            ch.append(self._local_map(self.global_intention_map(f['intention_map_encoding'])))
+        if f['use_intention_channels']:
+            ch.extend(self.intention_channels())
+        assert all(c.dtype == np.float32 for c in ch)
+        return np.stack(ch, axis=2)
+
+
+def agent_state(scene, agent):
+    return AgentOracle(scene, agent).get_state()

@@ -1,0 +1,244 @@
+"""Seeded synthetic scenes for the observation path.
+
+There is no PyBullet here: a scene is what the observation path reads from the simulator
+at one step -- per-robot poses / controller state, and per-agent observed global maps
+(occupancy u8 and overhead-without-robots f32).  Geometry follows the reference:
+walls / divider / room corners (envs.py:515-649), receptacle (envs.py:150-151, 469-477),
+cubes (envs.py:26, 686-692), robot spawn (envs.py:651-716), intention/history paths
+(RobotController.get_intention_path / get_history_path, envs.py:1475-1479).
+
+Pure numpy (no torch): imported by the python3.9 golden generator, by the tests and by bench.py.
+"""
+import math
+
+import numpy as np
+
+from . import constants as K
+
+# The five BASELINE.json configs (+ flag variants from config/experiments/comparisons/**,
+# used only as extra parity cases).  Flags are the reference's YAML values.
+_BASE_FLAGS = dict(K.DEFAULT_FLAGS)
+
+CONFIGS = {
+    # config/experiments/base/lifting_1-small_empty-base.yml
+    'lifting_1-small_empty': dict(env_name='small_empty', robot_config=[{'lifting_robot': 1}], flags={}),
+    # config/experiments/ours/lifting_4-small_divider-ours.yml
+    'lifting_4-small_divider': dict(env_name='small_divider', robot_config=[{'lifting_robot': 4}],
+                                    flags={'use_intention_map': True}),
+    # config/experiments/ours/pushing_4-large_empty-ours.yml
+    'pushing_4-large_empty': dict(env_name='large_empty', robot_config=[{'pushing_robot': 4}],
+                                  flags={'use_intention_map': True}),
+    # config/experiments/ours/lifting_2_throwing_2-large_empty-ours.yml
+    'lifting_2_throwing_2-large_empty': dict(env_name='large_empty',
+                                             robot_config=[{'lifting_robot': 2}, {'throwing_robot': 2}],
+                                             flags={'use_intention_map': True}),
+    # config/experiments/ours/rescue_4-small_empty-ours.yml (utils.py:177-180 drops receptacle maps)
+    'rescue_4-small_empty': dict(env_name='small_empty', robot_config=[{'rescue_robot': 4}],
+                                 flags={'use_intention_map': True, 'use_shortest_path_to_receptacle_map': False}),
+    # --- comparison variants (API completeness) ---
+    'lifting_4-small_divider-history': dict(env_name='small_divider', robot_config=[{'lifting_robot': 4}],
+                                            flags={'use_history_map': True}),
+    'lifting_4-small_divider-binary': dict(env_name='small_divider', robot_config=[{'lifting_robot': 4}],
+                                           flags={'use_intention_map': True, 'intention_map_encoding': 'binary'}),
+    'lifting_4-large_empty-line': dict(env_name='large_empty', robot_config=[{'lifting_robot': 4}],
+                                       flags={'use_intention_map': True, 'intention_map_encoding': 'line'}),
+    'lifting_4-small_empty-circle': dict(env_name='small_empty', robot_config=[{'lifting_robot': 4}],
+                                         flags={'use_intention_map': True, 'intention_map_encoding': 'circle'}),
+    'lifting_4-small_divider-spatial': dict(env_name='small_divider', robot_config=[{'lifting_robot': 4}],
+                                            flags={'use_intention_channels': True,
+                                                   'intention_channel_encoding': 'spatial'}),
+    'lifting_4-large_empty-nonspatial': dict(env_name='large_empty', robot_config=[{'lifting_robot': 4}],
+                                             flags={'use_intention_channels': True,
+                                                    'intention_channel_encoding': 'nonspatial'}),
+    # use_distance_to_receptacle_map is an API flag no shipped config turns on (envs.py:2083-2084)
+    'lifting_2_pushing_2-large_empty-all': dict(env_name='large_empty',
+                                                robot_config=[{'lifting_robot': 2}, {'pushing_robot': 2}],
+                                                flags={'use_distance_to_receptacle_map': True,
+                                                       'use_history_map': True, 'use_intention_map': True,
+                                                       'use_intention_channels': True}),
+}
+
+BASELINE_CONFIGS = ('lifting_1-small_empty', 'lifting_4-small_divider', 'pushing_4-large_empty',
+                    'lifting_2_throwing_2-large_empty', 'rescue_4-small_empty')
+
+
+def config_flags(name):
+    cfg = CONFIGS[name]
+    flags = dict(_BASE_FLAGS)
+    flags.update(cfg['flags'])
+    if any('rescue_robot' in g for g in cfg['robot_config']):  # utils.py:177-180
+        flags['use_distance_to_receptacle_map'] = False
+        flags['use_shortest_path_to_receptacle_map'] = False
+    return flags
+
+
+def num_channels(flags, num_robots):
+    """Channel count of Mapper.get_state (envs.py:2068-2113)."""
+    c = 1
+    c += bool(flags['use_robot_map'])
+    c += bool(flags['use_distance_to_receptacle_map'])
+    c += bool(flags['use_shortest_path_to_receptacle_map'])
+    c += bool(flags['use_shortest_path_map'])
+    c += bool(flags['use_history_map'])
+    c += bool(flags['use_intention_map'])
+    if flags['use_intention_channels']:
+        per = 1 if flags['intention_channel_encoding'] == 'spatial' else 2
+        c += per * (num_robots - 1)
+    return c
+
+
+def pixel_center_positions(H, W):
+    """Mapper.pixel_indices_to_position over the whole grid (envs.py:2399-2403), fp64."""
+    ii, jj = np.meshgrid(np.arange(H), np.arange(W), indexing='ij')
+    x = ((jj + 0.5) - W / 2) / K.LOCAL_MAP_PIXELS_PER_METER
+    y = (H / 2 - (ii + 0.5)) / K.LOCAL_MAP_PIXELS_PER_METER
+    return x, y
+
+
+def _obstacles(env_name, room_length, room_width, rs):
+    """Boxes of VectorEnv._get_obstacles (envs.py:515-571) + robot spawn bounds.
+
+    Only the env names of the BASELINE configs (empty / divider) are generated."""
+    wall_thickness = 1.4
+    boxes = []
+    for x, y, length, width in [
+            (-room_length / 2 - wall_thickness / 2, 0, wall_thickness, room_width),
+            (room_length / 2 + wall_thickness / 2, 0, wall_thickness, room_width),
+            (0, -room_width / 2 - wall_thickness / 2, room_length + 2 * wall_thickness, wall_thickness),
+            (0, room_width / 2 + wall_thickness / 2, room_length + 2 * wall_thickness, wall_thickness)]:
+        boxes.append((x, y, length, width))
+    spawn_bounds = None
+    if env_name in ('small_divider', 'small_divider_norand'):
+        x_offset = rs.uniform(-0.1, 0.1) if env_name == 'small_divider' else 0.0
+        divider_width, opening_width = 0.05, 0.16
+        boxes.append((x_offset, 0.0, divider_width, room_width - 2 * opening_width))
+        spawn_bounds = (x_offset + divider_width / 2, None, None, None)
+    elif env_name not in ('small_empty', 'large_empty'):
+        raise ValueError('synthetic scenes support small_empty/small_divider/large_empty, not %r' % env_name)
+    return boxes, spawn_bounds
+
+
+def _random_position(rs, room_length, room_width, padding, bounds=None):
+    """VectorEnv._get_random_position (envs.py:700-716)."""
+    low_x, high_x = -room_length / 2 + padding, room_length / 2 - padding
+    low_y, high_y = -room_width / 2 + padding, room_width / 2 - padding
+    if bounds is not None:
+        x_min, x_max, y_min, y_max = bounds
+        if x_min is not None:
+            low_x = x_min + padding
+        if x_max is not None:
+            high_x = x_max - padding
+        if y_min is not None:
+            low_y = y_min + padding
+        if y_max is not None:
+            high_y = y_max - padding
+    px, py = rs.uniform((low_x, low_y), (high_x, high_y))
+    return float(px), float(py)
+
+
+def make_scene(config_name, env_idx, seed_base=1234, observe_all=False):
+    """One env's observation-path inputs.
+
+    Returns a dict:
+      env_name, room_length, room_width, flags, robot_config, H, W,
+      receptacle_position (x, y, 0) or None,
+      robots: list of dicts {type, cls, group_index, position (x,y,0), heading, lift_state, idle,
+                             waypoint_positions [(x,y,0)...], waypoint_index, target_ee (x,y,0)},
+      occupancy: u8 [A, H, W]  (per agent, OccupancyMap.occupancy_map after update)
+      overhead: f32 [A, H, W]  (per agent, Mapper.global_overhead_map_without_robots)
+      obstacle_mask: bool [H, W] (ground truth, for the point cloud of the golden generator)
+    """
+    cfg = CONFIGS[config_name]
+    rs = np.random.RandomState(seed_base + env_idx)
+    room_length, room_width, num_cubes = K.room_dims(cfg['env_name'])
+    flags = config_flags(config_name)
+    H, W = K.padded_room_shape(room_width, room_length)
+    is_rescue = any('rescue_robot' in g for g in cfg['robot_config'])
+    receptacle = None if is_rescue else (room_length / 2 - K.RECEPTACLE_WIDTH / 2,
+                                         room_width / 2 - K.RECEPTACLE_WIDTH / 2, 0)  # envs.py:150-151
+
+    boxes, spawn_bounds = _obstacles(cfg['env_name'], room_length, room_width, rs)
+    X, Y = pixel_center_positions(H, W)
+    obstacle = np.zeros((H, W), dtype=bool)
+    for (bx, by, bl, bw) in boxes:
+        obstacle |= (np.abs(X - bx) <= bl / 2) & (np.abs(Y - by) <= bw / 2)
+    # Rounded room corners (envs.py:573-587): a w x w square minus a quarter disk.
+    w = 0.1006834873
+    for (cx, cy) in [(-room_length / 2, room_width / 2), (room_length / 2, room_width / 2),
+                     (room_length / 2, -room_width / 2), (-room_length / 2, -room_width / 2)]:
+        if receptacle is not None and math.hypot(cx - receptacle[0], cy - receptacle[1]) <= \
+                (1 + 1e-6) * (K.RECEPTACLE_WIDTH / 2) * math.sqrt(2):
+            continue
+        sx, sy = -math.copysign(1, cx), -math.copysign(1, cy)
+        in_sq = (np.abs(X - cx) <= w) & (np.abs(Y - cy) <= w) & ((X - cx) * sx >= 0) & ((Y - cy) * sy >= 0)
+        ox, oy = cx + sx * w, cy + sy * w
+        obstacle |= in_sq & ((X - ox) ** 2 + (Y - oy) ** 2 > w * w)
+
+    in_room = (np.abs(X) <= room_length / 2) & (np.abs(Y) <= room_width / 2)
+    seg = np.where(in_room, K.SEG_VALUES['floor'], K.SEG_VALUES['obstacle']).astype(np.float32)
+    seg[obstacle] = K.SEG_VALUES['obstacle']
+    if receptacle is not None:
+        rec = (np.abs(X - receptacle[0]) <= K.RECEPTACLE_WIDTH / 2) & (np.abs(Y - receptacle[1]) <= K.RECEPTACLE_WIDTH / 2)
+        seg[rec & in_room & ~obstacle] = K.SEG_VALUES['receptacle']
+    for _ in range(num_cubes):
+        px, py = _random_position(rs, room_length, room_width, K.CUBE_WIDTH / 2)
+        cube = (np.abs(X - px) <= K.CUBE_WIDTH / 2) & (np.abs(Y - py) <= K.CUBE_WIDTH / 2)
+        seg[cube & in_room & ~obstacle] = K.SEG_VALUES['cube']
+
+    robots = []
+    for group_index, g in enumerate(cfg['robot_config']):
+        rtype, count = next(iter(g.items()))
+        geom = K.ROBOT_GEOM[rtype]
+        for _ in range(count):
+            px, py = _random_position(rs, room_length, room_width, geom['RADIUS'], spawn_bounds)
+            heading = float(rs.uniform(-math.pi, math.pi))
+            n_wp = int(rs.randint(2, 6))
+            wps = [(px, py, 0)]
+            for _ in range(n_wp - 1):
+                wx, wy = _random_position(rs, room_length, room_width, geom['RADIUS'])
+                wps.append((wx, wy, 0))
+            tx, ty = _random_position(rs, room_length, room_width, 0.0)
+            robots.append({
+                'type': rtype, 'cls': K.ROBOT_TYPES.index(rtype), 'group_index': group_index,
+                'position': (px, py, 0), 'heading': heading,
+                'lift_state': 'lifting' if (rtype == 'lifting_robot' and rs.rand() < 0.5) else 'ready',
+                'idle': bool(len(robots) == 0 or rs.rand() < 0.15),
+                'waypoint_positions': wps,
+                'waypoint_index': int(rs.randint(1, n_wp)),
+                'target_ee': (tx, ty, 0),
+            })
+
+    # Per-agent observed maps (partial observation: a disk around the agent plus a random
+    # earlier viewpoint), values as Mapper.update writes them (envs.py:2057-2066).
+    A = len(robots)
+    occupancy = np.zeros((A, H, W), dtype=np.uint8)
+    overhead = np.zeros((A, H, W), dtype=np.float32)
+    for a, r in enumerate(robots):
+        if observe_all:
+            seen = np.ones((H, W), dtype=bool)
+        else:
+            seen = np.zeros((H, W), dtype=bool)
+            for (vx, vy) in [r['position'][:2], _random_position(rs, room_length, room_width, 0.0)]:
+                rad = rs.uniform(0.35, 1.2)
+                seen |= (X - vx) ** 2 + (Y - vy) ** 2 <= rad * rad
+        overhead[a][seen] = seg[seen]
+        occupancy[a][seen & (seg == K.SEG_VALUES['obstacle'])] = 1
+
+    return {
+        'config': config_name, 'env_name': cfg['env_name'], 'room_length': room_length,
+        'room_width': room_width, 'flags': flags, 'robot_config': cfg['robot_config'], 'H': H, 'W': W,
+        'receptacle_position': receptacle, 'robots': robots,
+        'occupancy': occupancy, 'overhead': overhead, 'seg_truth': seg,
+    }
+
+
+def intention_path(robot):
+    """RobotController.get_intention_path (envs.py:1475-1476)."""
+    idx = robot['waypoint_index']
+    return [robot['position']] + list(robot['waypoint_positions'][idx:-1]) + [robot['target_ee']]
+
+
+def history_path(robot):
+    """RobotController.get_history_path (envs.py:1478-1479)."""
+    idx = robot['waypoint_index']
+    return list(robot['waypoint_positions'][:idx]) + [robot['position']]

@@ -1,0 +1,127 @@
+"""CPU: the oracle (oracle/) reproduces the reference's outputs bit for bit.
+
+The goldens were produced by running the reference's own code (tests/golden/make_goldens.py).
+These tests pin the oracle; the GPU tests then check the HIP path against the oracle.
+"""
+import hashlib
+import math
+
+import numpy as np
+import pytest
+
+import goldens as G
+import oracle as O
+from simaps import constants as K
+
+
+def test_trig_cosdg_sindg_bitwise():
+    g = G.load('trig.npz')
+    c = np.array([O.cosdg(a) for a in g['angle']])
+    s = np.array([O.sindg(a) for a in g['angle']])
+    assert np.array_equal(c.view(np.int64), g['cosdg'].view(np.int64))
+    assert np.array_equal(s.view(np.int64), g['sindg'].view(np.int64))
+
+
+@pytest.mark.parametrize('n', [96, 136])
+def test_rotate_index_maps(n):
+    g = G.load('rotate.npz')
+    for k, a in enumerate(g['angle']):
+        i0, i1, v = O.rotate_index_map(n, float(a))
+        m = np.where(v, i0 * n + i1, -1).astype(np.int32)
+        assert m.shape == tuple(g['shape_%d' % n][k]), a
+        assert hashlib.sha256(m.tobytes()).digest() == g['sha_%d' % n][k].tobytes(), a
+    for q in range(6):
+        i0, i1, v = O.rotate_index_map(n, float(g['angle'][q * 97]))
+        assert np.array_equal(np.where(v, i0 * n + i1, -1), g['full_%d_%d' % (n, q)])
+
+
+def test_edt_feature_transform():
+    g = G.load('edt.npz')
+    for q in range(24):
+        assert np.array_equal(O.edt_indices(g['in_%d' % q]), g['ft_%d' % q]), q
+
+
+def test_bresenham_line():
+    g = G.load('line.npz')
+    off = g['off']
+    for k, (r0, c0, r1, c1) in enumerate(g['ends']):
+        rr, cc = O.line(int(r0), int(c0), int(r1), int(c1))
+        assert np.array_equal(rr, g['rr'][off[k]:off[k + 1]]) and np.array_equal(cc, g['cc'][off[k]:off[k + 1]])
+
+
+def test_linspace_ramp():
+    g = G.load('linspace.npz')
+    off = g['off']
+    for k, (a, b, n) in enumerate(zip(g['start'], g['seg'], g['n'])):
+        v = np.clip(O.linspace(1 - a, 1 - (a + b), int(n)), 0, 1)
+        assert np.array_equal(v.view(np.int64), g['vals'][off[k]:off[k + 1]].view(np.int64))
+
+
+def test_selems_and_grey_dilation():
+    g = G.load('selem.npz')
+    for r in range(9):
+        assert np.array_equal(O.disk(r), g['disk_%d' % r])
+    assert np.array_equal(O.grey_dilation_cross(g['grey_in']), g['grey_out'])
+
+
+def test_robot_masks():
+    g = G.load('masks.npz')
+    for t in K.ROBOT_TYPES:
+        assert np.array_equal(O.robot_mask(t), g[t])
+    assert np.array_equal(O.robot_mask('lifting_robot', show_lifted_cube=True), g['lifting_robot_with_cube'])
+
+
+def test_spfa_demo_known_answer():
+    """shortest_paths/demo.py:33-52 sample: distance 136.46806, image, 12 more sources."""
+    g = G.load('sssp.npz')
+    img = O.spfa_image(g['demo_cspace'], (75, 156))
+    assert np.array_equal(img.view(np.int32), g['demo_image'].view(np.int32))
+    assert img[131, 112] == g['demo_distance']
+    assert abs(float(g['demo_distance']) - 136.46806) < 1e-4
+    assert (img >= 0).sum() == 5489
+    for (i, j), sha in zip(g['demo_sources'], g['demo_sha']):
+        im = O.spfa_image(g['demo_cspace'], (int(i), int(j)))
+        assert hashlib.sha256(im.tobytes()).digest() == sha.tobytes()
+
+
+def test_spfa_random_grids():
+    g = G.load('sssp.npz')
+    for q in range(10):
+        im = O.spfa_image(g['rand_grid_%d' % q], tuple(int(x) for x in g['rand_src_%d' % q]))
+        assert np.array_equal(im.view(np.int32), g['rand_img_%d' % q].view(np.int32)), q
+
+
+CASES = list(G.scene_cases())
+
+
+@pytest.mark.parametrize('case', CASES, ids=['%s-e%d-a%d' % c[:3] for c in CASES])
+def test_agent_state_matches_reference(case):
+    cfg, e, a, scene, pre, z = case
+    ao = O.AgentOracle(scene, a)
+    i0, j0, h, w = K.room_rect(scene['room_width'], scene['room_length'])
+    assert np.array_equal(ao.cspace[i0:i0 + h, j0:j0 + w], z[pre + 'cspace_rect'])
+    assert ao.cspace.sum() == z[pre + 'cspace_rect'].sum()
+    assert np.array_equal(ao.closest, z[pre + 'closest'])
+    srcs = []
+    if scene['flags']['use_shortest_path_to_receptacle_map']:
+        srcs.append(('receptacle', scene['receptacle_position']))
+    if scene['flags']['use_shortest_path_map']:
+        srcs.append(('robot', scene['robots'][a]['position']))
+    for name, pos in srcs:
+        ref = z[pre + 'src_%s' % name]
+        assert O.position_to_pixel_indices(pos[0], pos[1], ao.shape) == (ref[0], ref[1])
+        assert ao.snap(pos) == (ref[2], ref[3])
+        img = O.spfa_image(ao.cspace, (ref[2], ref[3]))
+        assert np.array_equal(img[i0:i0 + h, j0:j0 + w].view(np.int32), z[pre + 'sp_%s_rect' % name].view(np.int32))
+    assert np.array_equal(ao.global_overhead_map(), z[pre + 'global_overhead'])
+    assert np.array_equal(ao.global_robot_map(seg=False), z[pre + 'global_robot'])
+    if scene['flags']['use_intention_map']:
+        gi = ao.global_intention_map(scene['flags']['intention_map_encoding'])
+        assert np.array_equal(gi.view(np.int32), z[pre + 'global_intention'].view(np.int32))
+    if scene['flags']['use_history_map']:
+        gh = ao.global_intention_map('history')
+        assert np.array_equal(gh.view(np.int32), z[pre + 'global_history'].view(np.int32))
+    st = ao.get_state()
+    ref = z[pre + 'state']
+    assert st.shape == ref.shape and st.dtype == np.float32
+    assert np.array_equal(st.view(np.int32), ref.view(np.int32))
