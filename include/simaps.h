@@ -1,0 +1,152 @@
+/* simaps.h -- C ABI of libsimaps.so, the MI355X-native observation-map pipeline of
+ * Spatial Intention Maps (reference: mushroonhead/spatial-intention-maps, envs.py + shortest_paths/).
+ *
+ * Plain C: pointers, sizes, POD structs; no torch/HIP types in any signature.  Device pointers
+ * are HIP device allocations (e.g. torch CUDA/ROCm tensors' data_ptr()).  `stream` is a
+ * hipStream_t passed as void* (NULL = default stream); every compute call is asynchronous on it.
+ * Return value: 0 = ok, negative = error (see SIMAPS_E*; simaps_last_error() has the text).
+ * No exceptions cross the ABI.  Thread-safe: no global mutable state besides the last-error
+ * string (thread-local).
+ *
+ * Reference interfaces replaced (file:line relative to the reference repo root):
+ *   simaps_get_state    <- Mapper.get_state (envs.py:2068-2185) for a batch of agents, including
+ *                          the OccupancyMap.update work it needs (envs.py:2445-2460: cspace,
+ *                          EDT snap, GridGraph) minus the camera-point scatter; what
+ *                          VectorEnv.get_state(all_robots=True) (envs.py:322-323) returns.
+ *   simaps_sssp_grid    <- GridGraph(grid).shortest_path_image(source)
+ *                          (shortest_paths/shortest_paths.pyx:24-67, 69-119, 165-167), batched.
+ *   simaps_robot_mask   <- Mapper._create_robot_mask (envs.py:2218-2242) (host helper).
+ *   simaps_num_channels <- the channel list of Mapper.get_state (envs.py:2071-2113).
+ */
+#ifndef SIMAPS_H
+#define SIMAPS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIMAPS_ABI_VERSION 1
+
+/* error codes */
+#define SIMAPS_OK 0
+#define SIMAPS_EINVAL -1      /* bad argument / shape / flag combination */
+#define SIMAPS_EUNSUPPORTED -2 /* valid for the reference but outside this build's limits */
+#define SIMAPS_EHIP -3        /* HIP runtime error (launch / memory) */
+
+/* robot classes (envs.py: LiftingRobot 1169, PushingRobot 1059, ThrowingRobot 1279, RescueRobot 1346) */
+#define SIMAPS_LIFTING 0
+#define SIMAPS_PUSHING 1
+#define SIMAPS_THROWING 2
+#define SIMAPS_RESCUE 3
+
+/* intention_map_encoding (envs.py:2308-2340) */
+#define SIMAPS_ENC_RAMP 0
+#define SIMAPS_ENC_BINARY 1
+#define SIMAPS_ENC_LINE 2
+#define SIMAPS_ENC_CIRCLE 3
+
+/* limits of this build */
+#define SIMAPS_MAX_ROBOTS 8      /* robots per env */
+#define SIMAPS_MAX_PATH 16       /* points per intention / history path */
+#define SIMAPS_MAX_ROOM_CELLS 8836 /* (room_h + 2) * (room_w + 2) */
+#define SIMAPS_MAX_ROOM_W 120
+
+/* One robot of an env, as the observation path reads it (Robot / RobotController state). */
+typedef struct simaps_robot {
+    double x, y;            /* robot.get_position()[:2]                         (envs.py:942)  */
+    double heading;         /* robot.get_heading()                              (envs.py:950)  */
+    double target_x;        /* robot.target_end_effector_position[:2]           (envs.py:870)  */
+    double target_y;
+    int32_t type;           /* SIMAPS_LIFTING ... SIMAPS_RESCUE                                */
+    int32_t group_index;    /* robot.group_index (seg value (g+5)/8, envs.py:2257)             */
+    int32_t lifting;        /* LiftingRobot.lift_state == 'lifting' (envs.py:2260)             */
+    int32_t idle;           /* robot.is_idle() (envs.py:937)                                   */
+    int32_t intention_off;  /* RobotController.get_intention_path() (envs.py:1475) in paths[]  */
+    int32_t intention_len;
+    int32_t history_off;    /* get_history_path()[::-1] (envs.py:1478, 2318), ALREADY reversed */
+    int32_t history_len;
+} simaps_robot;
+
+/* One env (VectorEnv) of the batch. */
+typedef struct simaps_env {
+    double receptacle_x, receptacle_y; /* VectorEnv.receptacle_position (envs.py:150-151) */
+    int32_t has_receptacle;
+    int32_t robot_off;                 /* first robot of this env in robots[] */
+    int32_t num_robots;
+    int32_t reserved;
+} simaps_env;
+
+/* One agent-state stack to render: robot `robot` of env `env`. */
+typedef struct simaps_agent {
+    int32_t env;
+    int32_t robot;
+} simaps_agent;
+
+/* Batch-wide configuration: VectorEnv state-representation flags (envs.py:39-45) + grid. */
+typedef struct simaps_config {
+    int32_t H, W;                   /* Mapper.create_padded_room_zeros shape (envs.py:2384-2389) */
+    int32_t room_i0, room_j0;       /* OccupancyMap._create_room_mask rect (envs.py:2468-2476)   */
+    int32_t room_h, room_w;
+    int32_t use_robot_map;
+    int32_t use_distance_to_receptacle_map;
+    int32_t use_shortest_path_to_receptacle_map;
+    int32_t use_shortest_path_map;
+    int32_t use_intention_map;
+    int32_t intention_map_encoding; /* SIMAPS_ENC_* */
+    int32_t intention_map_line_thickness;
+    int32_t use_history_map;
+    int32_t use_intention_channels;
+    int32_t intention_channel_spatial; /* 1 = 'spatial', 0 = 'nonspatial' */
+    int32_t layout_chw;             /* 0: state is [N,96,96,C] (reference HWC), 1: [N,C,96,96] */
+    int32_t reserved;
+    double distance_to_receptacle_map_scale;
+    double shortest_path_map_scale;
+    double intention_map_scale;
+    double intention_channel_nonspatial_scale;
+} simaps_config;
+
+/* Optional per-agent intermediates (device pointers, any may be NULL), for parity tests. */
+typedef struct simaps_debug {
+    uint8_t *cspace;   /* [N, room_h, room_w] OccupancyMap.configuration_space inside the room rect */
+    int32_t *sources;  /* [N, 2, 4]: (pi, pj, snapped_i, snapped_j) for receptacle / robot sources */
+    float *dist;       /* [N, 2, room_h, room_w] raw GridGraph.shortest_path_image (-1 unreachable) */
+    int32_t *status;   /* [N] bit0: no free cell (sp channels undefined in the reference); bit1: SSSP
+                        round cap hit (bug guard); bits 8+: SSSP rounds to convergence */
+} simaps_debug;
+
+int simaps_abi_version(void);
+const char *simaps_last_error(void);
+
+/* Number of channels C of the stack for an env with `num_robots` robots (envs.py:2071-2113). */
+int simaps_num_channels(const simaps_config *cfg, int num_robots);
+
+/* Host helper: Mapper._create_robot_mask(cls, show_lifted_cube) into out[96*96] (float32, host). */
+int simaps_robot_mask(int type, int with_cube, float *out);
+
+/* Batched Mapper.get_state (+ the OccupancyMap.update work it needs).
+ *   agents[N], envs[E], robots[R], paths[P][2] (fp64 x, y), all DEVICE pointers;
+ *   occupancy [N, H, W] uint8 and overhead [N, H, W] float32: the per-agent global maps
+ *   (OccupancyMap.occupancy_map, Mapper.global_overhead_map_without_robots), DEVICE;
+ *   state: [N, 96, 96, C] (or [N, C, 96, 96] if cfg->layout_chw) float32, DEVICE, C =
+ *   simaps_num_channels(cfg, num_robots) -- every env of one call must have the same robot count
+ *   when intention channels are on.  `num_robots_per_env` is that count (or 0 if unused).
+ *   dbg may be NULL. */
+int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                     const simaps_robot *robots, const double *paths, const uint8_t *occupancy,
+                     const float *overhead, float *state, int num_robots_per_env, const simaps_debug *dbg,
+                     void *stream);
+
+/* Batched GridGraph(grid).shortest_path_image(source):
+ *   grids [B, H, W] uint8 (nonzero = free), sources [B, 2] int32 (row, col), out dists [B, H, W]
+ *   float32 (-1 unreachable, like pyx:110-112), all DEVICE.  All free cells of every grid must lie
+ *   in the window rows [wi0, wi0+wh) x cols [wj0, wj0+ww) with (wh+2)*(ww+2) <= SIMAPS_MAX_ROOM_CELLS
+ *   and ww <= SIMAPS_MAX_ROOM_W (cells outside the window are treated as blocked). */
+int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *sources, float *dists,
+                     int wi0, int wj0, int wh, int ww, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIMAPS_H */

@@ -1,0 +1,945 @@
+// simaps.hip -- MI355X (gfx950) kernels of the Spatial Intention Maps observation path.
+//
+// One workgroup (1024 threads = 16 waves) renders one agent-state stack end to end with every
+// intermediate resident in LDS (~151 KiB, one workgroup per CU):
+//
+//   1. cspace    OccupancyMap.update (envs.py:2453-2454): 1 - max(1 - room_mask,
+//                binary_dilation(occ, disk(r))) inside the room rect; occupancy rows turned into
+//                bit rows by wave ballots, disk dilation as OR of shifted bit rows.
+//   2. snap      OccupancyMap._closest_valid_cspace_indices (envs.py:2523-2524) =
+//                scipy distance_transform_edt(return_indices) evaluated at the <= 2 query pixels
+//                with scipy's own separable Voronoi tie-breaking (column pass, then one lane).
+//   3. SSSP      GridGraph._spfa (pyx:69-114) from the <= 2 snapped sources: pull-style
+//                Bellman-Ford over the LDS-resident room rect, frontier kept as bit rows
+//                (only 8-neighbours of last round's changed cells are re-evaluated).  The float32
+//                fixpoint is unique (dist[v] = min over paths of the left-fold f32 sum), so any
+//                schedule that runs to convergence is bit-identical to the reference's SPFA.
+//   4. render    Mapper.get_state (envs.py:2068-2113): 96x96 output pixels x C channels; the
+//                scipy order-0 rotate is evaluated as a gather (same fp64 index rule), robot
+//                stamps / masks are evaluated analytically per pixel, intention / history lines
+//                are rasterised into an LDS tile (closed-form Bresenham, fp64 linspace ramp,
+//                atomicMax) and grey-dilated at sample time.
+//
+// HBM traffic per stack: the occupancy window (room rect + r halo, bytes), the overhead window
+// gathered through L2 (<= 136^2 f32 footprint), the state write (96*96*C f32).  No intermediate
+// map ever leaves the CU.
+//
+// Compiled with -ffp-contract=off: every fp32/fp64 operation rounds exactly like the reference
+// (see geom.h for the one explicit fma).
+#include <hip/hip_runtime.h>
+
+#include "geom.h"
+#include "simaps.h"
+
+using namespace simaps;
+
+namespace {
+
+constexpr int NT = 1024;
+constexpr int MAX_SEG = 128;     // intention / history segments per agent
+constexpr int SEG_PER_ROBOT = SIMAPS_MAX_PATH - 1;
+constexpr int MAX_ROWS = 112;    // room rect rows (bit-row arrays)
+constexpr int WIN_WORDS = 3;     // occupancy window row: up to 192 bits
+constexpr int MAX_WIN_ROWS = MAX_ROWS + 16;
+constexpr unsigned INF_BITS = 0x7f800000u;
+constexpr float SQRT2F = 1.41421354f;  // float(np.sqrt(2)) (pyx:31-32)
+
+struct B128 {
+    uint64_t lo, hi;
+};
+__device__ __forceinline__ B128 b_or(B128 a, B128 b) { return {a.lo | b.lo, a.hi | b.hi}; }
+__device__ __forceinline__ B128 b_and(B128 a, B128 b) { return {a.lo & b.lo, a.hi & b.hi}; }
+__device__ __forceinline__ B128 b_shl1(B128 a) { return {a.lo << 1, (a.hi << 1) | (a.lo >> 63)}; }
+__device__ __forceinline__ B128 b_shr1(B128 a) { return {(a.lo >> 1) | (a.hi << 63), a.hi >> 1}; }
+__device__ __forceinline__ bool b_test(const B128 &a, int c)
+{
+    return c < 64 ? (a.lo >> c) & 1 : (a.hi >> (c - 64)) & 1;
+}
+__device__ __forceinline__ B128 b_mask(int w)
+{
+    B128 m;
+    m.lo = w >= 64 ? ~0ull : ((1ull << w) - 1);
+    m.hi = w >= 128 ? ~0ull : (w > 64 ? ((1ull << (w - 64)) - 1) : 0ull);
+    return m;
+}
+// bits [o, o + 128) of a 3-word row, 0 <= o < 64
+__device__ __forceinline__ B128 win_get(const uint64_t *row, int o)
+{
+    B128 r;
+    if (o == 0) {
+        r.lo = row[0];
+        r.hi = row[1];
+    } else {
+        r.lo = (row[0] >> o) | (row[1] << (64 - o));
+        r.hi = (row[1] >> o) | (row[2] << (64 - o));
+    }
+    return r;
+}
+__device__ __forceinline__ void b_atomic_or(B128 *dst, B128 v)
+{
+    unsigned *w = reinterpret_cast<unsigned *>(dst);
+    if ((unsigned)v.lo) atomicOr(w + 0, (unsigned)v.lo);
+    if ((unsigned)(v.lo >> 32)) atomicOr(w + 1, (unsigned)(v.lo >> 32));
+    if ((unsigned)v.hi) atomicOr(w + 2, (unsigned)v.hi);
+    if ((unsigned)(v.hi >> 32)) atomicOr(w + 3, (unsigned)(v.hi >> 32));
+}
+
+// ------------------------------------------------------------------------------------------------
+// LDS layout
+// ------------------------------------------------------------------------------------------------
+struct RobotP {
+    double c, s, f0, f1;  // stamp rotation (angle = degrees(h) - 90, envs.py:2266)
+    double x, y, tx, ty;
+    int S0, S1, st_i, st_j;  // stamp shape, placement (pixel - S // 2, envs.py:2272)
+    int type, lifting, idle, group;
+    int tpi, tpj;            // target end-effector pixel
+    float seg_val, pad;
+};
+
+struct Seg {
+    double start, step, stop;
+    int si, sj, ti, tj;
+    int n, last, dr, dc;
+};
+
+struct Shared {
+    Rot rot;             // local map rotation (angle = 90 - degrees(h), envs.py:2203)
+    int pi, pj;          // agent pixel
+    int nr, me, env, has_rec;
+    int h, w, i0, j0, r;
+    int nsrc;
+    int src_q[2][2], src_s[2][2], src_ok[2];
+    int sp_slot[2];      // which dist buffer each sp channel uses (-1 = off)
+    float dmax[2];
+    int flag[2];
+    int rounds;          // SSSP rounds to convergence (-1: cap hit)
+    int nseg;
+    int seg_robot_cnt[SIMAPS_MAX_ROBOTS];
+    int order[SIMAPS_MAX_ROBOTS];
+    float red[2][16];
+    float nonsp[2 * SIMAPS_MAX_ROBOTS];
+    RobotP rob[SIMAPS_MAX_ROBOTS];
+    int colbest[2][SIMAPS_MAX_ROOM_W];
+    int envg[2][SIMAPS_MAX_ROOM_W];  // Voronoi envelope (rect columns) per source
+    Seg seg[MAX_SEG];
+};
+
+// SSSP scratch (aliases the raster tile, which is only used after the SSSP phase)
+struct SsspScratch {
+    uint64_t win[MAX_WIN_ROWS][WIN_WORDS];
+    B128 blocked[MAX_ROWS];
+    B128 freeb[MAX_ROWS];
+    B128 bits[2][3][MAX_ROWS];  // [source][prev/cand/next][row]
+};
+
+constexpr int align16(int x) { return (x + 15) & ~15; }
+constexpr int OFF_DIST = align16((int)sizeof(Shared));
+constexpr int DIST_FLOATS = SIMAPS_MAX_ROOM_CELLS;
+constexpr int OFF_UNION = OFF_DIST + align16(2 * DIST_FLOATS * 4);
+constexpr int TILE_BYTES = TILE * TILE * 4;
+constexpr int UNION_BYTES = align16((int)sizeof(SsspScratch) > TILE_BYTES ? (int)sizeof(SsspScratch) : TILE_BYTES);
+constexpr int LDS_BYTES = OFF_UNION + UNION_BYTES;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+
+// ------------------------------------------------------------------------------------------------
+// Block reductions (16 waves)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_min(float v)
+{
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v)
+{
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase: occupancy window -> free-cell bit rows (cspace inside the room rect)
+// ------------------------------------------------------------------------------------------------
+// occ: the agent's occupancy map [H, W] (nonzero = obstacle).  r = disk radius.
+__device__ void build_cspace(SsspScratch &S, const uint8_t *__restrict__ occ, int H, int W, int i0, int j0,
+                             int h, int w, int r)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wh = h + 2 * r, ww = w + 2 * r;
+    const int nwords = (ww + 63) >> 6;
+    // (a) window rows -> bits: one wave-ballot per 64 columns
+    for (int item = wave; item < wh * WIN_WORDS; item += NT / 64) {
+        const int wr = item / WIN_WORDS, wd = item % WIN_WORDS;
+        const int gi = i0 - r + wr, x = wd * 64 + lane, gj = j0 - r + x;
+        bool ob = false;
+        if (wd < nwords && x < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ob = occ[(size_t)gi * W + gj] != 0;
+        const uint64_t m = __ballot(ob);
+        if (lane == 0) S.win[wr][wd] = m;
+    }
+    for (int rr = tid; rr < h; rr += NT) S.blocked[rr] = {0, 0};
+    __syncthreads();
+    // (b) blocked[row] = OR over disk offsets (dy, |dx| <= hw(dy)) of the window bits
+    const int span = 2 * r + 1;
+    for (int item = tid; item < h * span; item += NT) {
+        const int row = item / span, dy = item % span - r;
+        int hw = 0;
+        while ((hw + 1) * (hw + 1) + dy * dy <= r * r) hw++;
+        const uint64_t *wrow = S.win[row + r + dy];
+        B128 acc = {0, 0};
+        for (int k = -hw; k <= hw; k++) acc = b_or(acc, win_get(wrow, r + k));
+        b_atomic_or(&S.blocked[row], acc);
+    }
+    __syncthreads();
+    const B128 m = b_mask(w);
+    for (int rr = tid; rr < h; rr += NT) {
+        const B128 b = S.blocked[rr];
+        S.freeb[rr] = {~b.lo & m.lo, ~b.hi & m.hi};
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase: snap the query pixels to the closest free cell (scipy EDT feature transform at q)
+// ------------------------------------------------------------------------------------------------
+__device__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc)
+{
+    const int tid = threadIdx.x;
+    const int h = sh.h, w = sh.w, i0 = sh.i0, j0 = sh.j0;
+    // pass 1 (scipy: per column along axis 0): nearest free row of each rect column, ties low
+    for (int item = tid; item < nsrc * w; item += NT) {
+        const int s = item / w, c = item % w;
+        const int qi = sh.src_q[s][0];
+        int best = -1, bestd = 1 << 30;
+        for (int rr = 0; rr < h; rr++) {
+            if (b_test(S.freeb[rr], c)) {
+                const int d = abs(i0 + rr - qi);
+                if (d < bestd) { bestd = d; best = i0 + rr; }
+            }
+        }
+        sh.colbest[s][c] = best;
+    }
+    __syncthreads();
+    // pass 2 (scipy _VoronoiFT along axis 1), one lane per source
+    if ((tid & 63) == 0 && (tid >> 6) < nsrc) {
+        const int s = tid >> 6;
+        const int qi = sh.src_q[s][0], qj = sh.src_q[s][1];
+        const int qr = qi - i0, qc = qj - j0;
+        sh.src_ok[s] = 0;
+        if (qr >= 0 && qr < h && qc >= 0 && qc < w && b_test(S.freeb[qr], qc)) {
+            sh.src_s[s][0] = qi;
+            sh.src_s[s][1] = qj;
+            sh.src_ok[s] = 1;
+        } else {
+            int *g = sh.envg[s];  // envelope (indices into rect columns)
+            int l = -1;
+            for (int c = 0; c < w; c++) {
+                const int f0 = sh.colbest[s][c];
+                if (f0 < 0) continue;
+                const long long fd = j0 + c;
+                const long long tw = (long long)f0 - qi;
+                const long long wR = tw * tw;
+                while (l >= 1) {
+                    const int c1 = g[l], c2 = g[l - 1];
+                    const long long f1d = j0 + c1;
+                    const long long a = f1d - (j0 + c2);
+                    const long long b = fd - f1d;
+                    const long long tu = (long long)sh.colbest[s][c2] - qi, tv = (long long)sh.colbest[s][c1] - qi;
+                    const long long uR = tu * tu, vR = tv * tv;
+                    const long long cc = a + b;
+                    if (cc * vR - b * uR - a * wR - a * b * cc <= 0) break;
+                    --l;
+                }
+                ++l;
+                g[l] = c;
+            }
+            if (l >= 0) {
+                const int maxl = l;
+                l = 0;
+                for (int ii = 0; ii <= qj; ii++) {
+                    long long t0 = (long long)sh.colbest[s][g[l]] - qi, t1 = (long long)(j0 + g[l]) - ii;
+                    long long d1 = t0 * t0 + t1 * t1;
+                    while (l < maxl) {
+                        t0 = (long long)sh.colbest[s][g[l + 1]] - qi;
+                        t1 = (long long)(j0 + g[l + 1]) - ii;
+                        const long long d2 = t0 * t0 + t1 * t1;
+                        if (d1 <= d2) break;
+                        d1 = d2;
+                        ++l;
+                    }
+                }
+                sh.src_s[s][0] = sh.colbest[s][g[l]];
+                sh.src_s[s][1] = j0 + g[l];
+                sh.src_ok[s] = 1;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase: single-source shortest paths for nsrc sources over the free cells of the rect
+// ------------------------------------------------------------------------------------------------
+// dist[s]: (h + 2) x (w + 2) float32, padded with +inf.  Result: exact float32 SPFA distances,
+// +inf where unreachable / not free.  sh.dmax[s] = max reachable distance.
+__device__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
+{
+    const int tid = threadIdx.x;
+    const int h = sh.h, w = sh.w, pw = w + 2;
+    const int cells = (h + 2) * pw;
+    unsigned *du = reinterpret_cast<unsigned *>(dist);
+    for (int k = tid; k < nsrc * DIST_FLOATS; k += NT) du[k] = INF_BITS;
+    for (int k = tid; k < nsrc * 3 * MAX_ROWS; k += NT) (&S.bits[0][0][0])[k] = {0, 0};
+    if (tid < 2) sh.flag[tid] = 0;
+    __syncthreads();
+    if (tid < nsrc && sh.src_ok[tid]) {
+        const int r = sh.src_s[tid][0] - sh.i0, c = sh.src_s[tid][1] - sh.j0;
+        dist[tid * DIST_FLOATS + (r + 1) * pw + (c + 1)] = 0.0f;
+        B128 b = {0, 0};
+        if (c < 64) b.lo = 1ull << c; else b.hi = 1ull << (c - 64);
+        S.bits[tid][0][r] = b;
+    }
+    __syncthreads();
+    const int CH = (w + 7) >> 3;
+    // Bellman-Ford needs at most (#cells) rounds; the cap only guards against a bug hanging the GPU.
+    const int max_rounds = h * w + 16;
+    int prev = 0, next = 2;
+    sh.rounds = 0;
+    for (int round = 0;; round++) {
+        // (a) candidates = 8-dilation of last round's changed cells, restricted to free cells
+        for (int u = tid; u < nsrc * h; u += NT) {
+            const int s = u / h, rr = u % h;
+            B128 x = S.bits[s][prev][rr];
+            if (rr > 0) x = b_or(x, S.bits[s][prev][rr - 1]);
+            if (rr < h - 1) x = b_or(x, S.bits[s][prev][rr + 1]);
+            x = b_or(x, b_or(b_shl1(x), b_shr1(x)));
+            S.bits[s][1][rr] = b_and(x, S.freeb[rr]);
+            S.bits[s][next][rr] = {0, 0};
+        }
+        __syncthreads();
+        if (tid == 0) sh.flag[(round + 1) & 1] = 0;
+        // (b) pull-relax every candidate cell (in place; any interleaving is a valid relaxation)
+        for (int u = tid; u < nsrc * h * CH; u += NT) {
+            const int s = u / (h * CH), rem = u % (h * CH), rr = rem / CH, ch = rem % CH;
+            const B128 cb = S.bits[s][1][rr];
+            unsigned bits = (unsigned)((ch < 8 ? (cb.lo >> (8 * ch)) : (cb.hi >> (8 * (ch - 8)))) & 0xffu);
+            if (!bits) continue;
+            float *D = dist + s * DIST_FLOATS;
+            unsigned changed = 0;
+            while (bits) {
+                const int b = __builtin_ctz(bits);
+                bits &= bits - 1;
+                const int v = (rr + 1) * pw + (ch * 8 + b + 1);
+                const float dv = D[v];
+                float best = dv, t;
+                t = D[v - 1] + 1.0f;       best = t < best ? t : best;
+                t = D[v + 1] + 1.0f;       best = t < best ? t : best;
+                t = D[v - pw] + 1.0f;      best = t < best ? t : best;
+                t = D[v + pw] + 1.0f;      best = t < best ? t : best;
+                t = D[v - pw - 1] + SQRT2F; best = t < best ? t : best;
+                t = D[v - pw + 1] + SQRT2F; best = t < best ? t : best;
+                t = D[v + pw - 1] + SQRT2F; best = t < best ? t : best;
+                t = D[v + pw + 1] + SQRT2F; best = t < best ? t : best;
+                if (best < dv) {
+                    D[v] = best;
+                    changed |= 1u << b;
+                }
+            }
+            if (changed) {
+                unsigned *nw = reinterpret_cast<unsigned *>(&S.bits[s][next][rr]);
+                atomicOr(nw + (ch >> 2), changed << (8 * (ch & 3)));
+                sh.flag[round & 1] = 1;
+            }
+        }
+        __syncthreads();
+        if (sh.flag[round & 1] == 0 || round >= max_rounds) {
+            if (tid == 0) sh.rounds = round >= max_rounds ? -1 : round + 1;
+            break;
+        }
+        const int t = prev;
+        prev = next;
+        next = t;
+    }
+    // max reachable distance per source
+    for (int s = 0; s < nsrc; s++) {
+        float m = -1.0f;
+        for (int k = tid; k < cells; k += NT) {
+            const float d = dist[s * DIST_FLOATS + k];
+            if (d != __int_as_float(INF_BITS)) m = fmaxf(m, d);
+        }
+        m = wave_max(m);
+        if ((tid & 63) == 0) sh.red[0][tid >> 6] = m;
+        __syncthreads();
+        if (tid == 0) {
+            float mm = sh.red[0][0];
+            for (int k = 1; k < NT / 64; k++) mm = fmaxf(mm, sh.red[0][k]);
+            sh.dmax[s] = mm;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Intention / history raster (Mapper._create_global_intention_or_history_map, envs.py:2302-2347)
+// ------------------------------------------------------------------------------------------------
+// enc: SIMAPS_ENC_* or 4 = history (ramp over the reversed history path)
+__device__ void raster_lines(Shared &sh, float *tile, const simaps_config &cfg, const simaps_robot *rb,
+                             const double *__restrict__ paths, int enc)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    unsigned *tu = reinterpret_cast<unsigned *>(tile);
+    for (int k = tid; k < TILE * TILE; k += NT) tu[k] = 0u;
+    const double scale = cfg.intention_map_scale;
+    const float scale_f = (float)scale;
+    // per-robot segment tables (one lane per robot; path_length accumulates sequentially)
+    if (tid < sh.nr) {
+        const int k = tid;
+        int cnt = 0;
+        const RobotP &R = sh.rob[k];
+        if (k != sh.me && !R.idle && enc != SIMAPS_ENC_CIRCLE) {
+            const simaps_robot &r = rb[k];
+            const int off = enc == 4 ? r.history_off : r.intention_off;
+            const int full = enc == 4 ? r.history_len : r.intention_len;
+            const bool as_line = enc == SIMAPS_ENC_LINE && full >= 2;  // [path[0], path[-1]] (envs.py:2315-2316)
+            const int len = as_line ? 2 : full;
+            double L = 0.0;
+            for (int i = 1; i < len && cnt < SEG_PER_ROBOT; i++) {
+                const int ia = i - 1, ib = as_line ? full - 1 : i;
+                const double sx = paths[2 * (off + ia)], sy = paths[2 * (off + ia) + 1];
+                const double tx = paths[2 * (off + ib)], ty = paths[2 * (off + ib) + 1];
+                const double dx = tx - sx, dy = ty - sy;
+                const double seg_len = scale * sqrt(dx * dx + dy * dy);  // envs.py:2324, 2557-2558
+                Seg &G = sh.seg[k * SEG_PER_ROBOT + cnt];
+                pos_to_pix(sx, sy, cfg.H, cfg.W, G.si, G.sj);
+                pos_to_pix(tx, ty, cfg.H, cfg.W, G.ti, G.tj);
+                G.dr = abs(G.ti - G.si);
+                G.dc = abs(G.tj - G.sj);
+                G.n = (G.dr > G.dc ? G.dr : G.dc) + 1;
+                G.last = (i == len - 1);
+                // np.clip(np.linspace(1 - L, 1 - (L + seg), n), 0, 1) (envs.py:2335)
+                G.start = 1 - L;
+                G.stop = 1 - (L + seg_len);
+                G.step = G.n > 1 ? (G.stop - G.start) / (G.n - 1) : 0.0;
+                L += seg_len;
+                cnt++;
+            }
+        }
+        sh.seg_robot_cnt[k] = cnt;
+    }
+    __syncthreads();
+    const int ti0 = sh.pi - TILE_HALF, tj0 = sh.pj - TILE_HALF;
+    if (enc == SIMAPS_ENC_CIRCLE) {
+        if (tid < sh.nr && tid != sh.me && !sh.rob[tid].idle) {
+            const int a = sh.rob[tid].tpi - ti0, b = sh.rob[tid].tpj - tj0;
+            if (a >= 0 && a < TILE && b >= 0 && b < TILE) atomicMax(&tu[a * TILE + b], __float_as_uint(scale_f));
+        }
+    } else {
+        // one wave per segment, lanes stride over its pixels
+        const int total = sh.nr * SEG_PER_ROBOT;
+        for (int q = wave; q < total; q += NT / 64) {
+            const int k = q / SEG_PER_ROBOT, j = q % SEG_PER_ROBOT;
+            if (j >= sh.seg_robot_cnt[k]) continue;
+            const Seg &G = sh.seg[q];
+            const int npix = G.last ? G.n : G.n - 1;  // non-final segments drop their last pixel
+            const bool steep = G.dr > G.dc;
+            const int major = steep ? G.dr : G.dc, minor = steep ? G.dc : G.dr;
+            const int smaj = steep ? (G.ti - G.si > 0 ? 1 : -1) : (G.tj - G.sj > 0 ? 1 : -1);
+            const int smin = steep ? (G.tj - G.sj > 0 ? 1 : -1) : (G.ti - G.si > 0 ? 1 : -1);
+            for (int t = lane; t < npix; t += 64) {
+                int pr, pc;
+                if (t == G.n - 1) {  // skimage: rr[dc] = r1, cc[dc] = c1
+                    pr = G.ti;
+                    pc = G.tj;
+                } else {  // closed-form Bresenham: minor steps k_t = floor((2*minor*t + major) / (2*major))
+                    const int kt = (2 * minor * t + major) / (2 * major);
+                    if (steep) { pr = G.si + smaj * t; pc = G.sj + smin * kt; }
+                    else { pc = G.sj + smaj * t; pr = G.si + smin * kt; }
+                }
+                float v;
+                if (enc == SIMAPS_ENC_BINARY || enc == SIMAPS_ENC_LINE) {
+                    v = scale_f;
+                } else {
+                    double y = (t == G.n - 1 && G.n > 1) ? G.stop : (G.n > 1 ? (double)t * G.step + G.start : G.start);
+                    y = y < 0.0 ? 0.0 : (y > 1.0 ? 1.0 : y);
+                    v = (float)y;
+                }
+                const int a = pr - ti0, b = pc - tj0;
+                if (v > 0.0f && a >= 0 && a < TILE && b >= 0 && b < TILE) atomicMax(&tu[a * TILE + b], __float_as_uint(v));
+            }
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ float tile_sample(const float *tile, int thick, int gi, int gj, int pi, int pj)
+{
+    const int a = gi - pi + TILE_HALF, b = gj - pj + TILE_HALF;
+    float v = tile[a * TILE + b];
+    if (thick > 1) {
+        v = fmaxf(v, tile[(a - 1) * TILE + b]);
+        v = fmaxf(v, tile[(a + 1) * TILE + b]);
+        v = fmaxf(v, tile[a * TILE + b - 1]);
+        v = fmaxf(v, tile[a * TILE + b + 1]);
+    }
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// The fused per-agent kernel
+// ------------------------------------------------------------------------------------------------
+constexpr int PPT = (LW * LW) / NT;  // 9 output pixels per thread
+static_assert(PPT * NT == LW * LW, "pixel split");
+
+__global__ void __launch_bounds__(NT) get_state_kernel(
+    simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents, const simaps_env *__restrict__ envs,
+    const simaps_robot *__restrict__ robots, const double *__restrict__ paths, const uint8_t *__restrict__ occupancy,
+    const float *__restrict__ overhead, float *__restrict__ state, int C, simaps_debug dbg)
+{
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    Shared &sh = *reinterpret_cast<Shared *>(smem);
+    float *dist = reinterpret_cast<float *>(smem + OFF_DIST);
+    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
+    float *tile = reinterpret_cast<float *>(smem + OFF_UNION);
+
+    const int n = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int H = cfg.H, W = cfg.W;
+    const simaps_agent ag = agents[n];
+    const simaps_env ev = envs[ag.env];
+    const simaps_robot *rb = robots + ev.robot_off;
+
+    // ---- parameters (one lane per robot; the agent's own local rotation on another wave)
+    if (tid == 0) {
+        sh.nr = ev.num_robots;
+        sh.me = ag.robot;
+        sh.env = ag.env;
+        sh.has_rec = ev.has_receptacle;
+        sh.h = cfg.room_h;
+        sh.w = cfg.room_w;
+        sh.i0 = cfg.room_i0;
+        sh.j0 = cfg.room_j0;
+        sh.r = geo.cspace_r[rb[ag.robot].type];
+        int ns = 0;
+        sh.sp_slot[0] = sh.sp_slot[1] = -1;
+        if (cfg.use_shortest_path_to_receptacle_map) {
+            pos_to_pix(ev.receptacle_x, ev.receptacle_y, H, W, sh.src_q[ns][0], sh.src_q[ns][1]);
+            sh.sp_slot[0] = ns++;
+        }
+        if (cfg.use_shortest_path_map) {
+            pos_to_pix(rb[ag.robot].x, rb[ag.robot].y, H, W, sh.src_q[ns][0], sh.src_q[ns][1]);
+            sh.sp_slot[1] = ns++;
+        }
+        sh.nsrc = ns;
+    }
+    if (tid == 64) {
+        const simaps_robot &me = rb[ag.robot];
+        sh.rot = rot_params(CROP, 90.0 - me.heading * RAD_TO_DEG);
+        pos_to_pix(me.x, me.y, H, W, sh.pi, sh.pj);
+    }
+    if (tid >= 128 && tid < 128 + ev.num_robots) {
+        const int k = tid - 128;
+        const simaps_robot &r = rb[k];
+        RobotP &P = sh.rob[k];
+        const Rot R = rot_params(LW, r.heading * RAD_TO_DEG - 90.0);
+        P.c = R.c; P.s = R.s; P.f0 = R.f0; P.f1 = R.f1; P.S0 = R.S0; P.S1 = R.S1;
+        int pi, pj;
+        pos_to_pix(r.x, r.y, H, W, pi, pj);
+        P.st_i = pi - R.S0 / 2;
+        P.st_j = pj - R.S1 / 2;
+        P.type = r.type; P.lifting = r.lifting; P.idle = r.idle; P.group = r.group_index;
+        P.x = r.x; P.y = r.y; P.tx = r.target_x; P.ty = r.target_y;
+        pos_to_pix(r.target_x, r.target_y, H, W, P.tpi, P.tpj);
+        P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
+    }
+    __syncthreads();
+
+    // ---- cspace + snap + SSSP
+    const int nsrc = sh.nsrc;
+    if (nsrc > 0 || dbg.cspace) {
+        build_cspace(S, occupancy + (size_t)n * H * W, H, W, sh.i0, sh.j0, sh.h, sh.w, sh.r);
+        if (dbg.cspace) {
+            for (int k = tid; k < sh.h * sh.w; k += NT)
+                dbg.cspace[(size_t)n * sh.h * sh.w + k] = b_test(S.freeb[k / sh.w], k % sh.w) ? 1 : 0;
+        }
+    }
+    if (nsrc > 0) {
+        snap_sources(sh, S, nsrc);
+        sssp(sh, S, dist, nsrc);
+        if (dbg.sources && tid < 2) {
+            int32_t *o = dbg.sources + ((size_t)n * 2 + tid) * 4;
+            const int s = sh.sp_slot[tid];
+            if (s >= 0) { o[0] = sh.src_q[s][0]; o[1] = sh.src_q[s][1]; o[2] = sh.src_s[s][0]; o[3] = sh.src_s[s][1]; }
+            else { o[0] = o[1] = o[2] = o[3] = -1; }
+        }
+        if (dbg.dist) {
+            for (int k = tid; k < 2 * sh.h * sh.w; k += NT) {
+                const int which = k / (sh.h * sh.w), rem = k % (sh.h * sh.w);
+                const int s = sh.sp_slot[which];
+                float v = -1.0f;
+                if (s >= 0) {
+                    v = dist[s * DIST_FLOATS + (rem / sh.w + 1) * (sh.w + 2) + rem % sh.w + 1];
+                    if (v == __int_as_float(INF_BITS)) v = -1.0f;
+                }
+                dbg.dist[(size_t)n * 2 * sh.h * sh.w + k] = v;
+            }
+        }
+    }
+    if (dbg.status && tid == 0) {
+        int st = 0;
+        for (int s = 0; s < nsrc; s++) st |= sh.src_ok[s] ? 0 : 1;
+        if (nsrc > 0 && sh.rounds < 0) st |= 2;
+        dbg.status[n] = st | ((nsrc > 0 ? sh.rounds : 0) << 8);
+    }
+
+    // ---- render: each thread owns output pixels p = tid + k * NT
+    int gpix[PPT];  // packed (gi << 16 | gj), -1 = rotate fell outside the crop (cval 0)
+    {
+        const Rot R = sh.rot;
+        const int b0 = R.S0 / 2 - LW / 2, b1 = R.S1 / 2 - LW / 2;
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const int p = tid + k * NT, a = p / LW, b = p % LW;
+            int k0, k1;
+            if (rot_src(R, CROP, a + b0, b + b1, k0, k1)) {
+                const int gi = sh.pi - HALF_CROP + k0, gj = sh.pj - HALF_CROP + k1;
+                gpix[k] = (gi >= 0 && gi < H && gj >= 0 && gj < W) ? (gi << 16) | gj : -1;
+            } else {
+                gpix[k] = -1;
+            }
+        }
+    }
+    float *out = state + (size_t)n * LW * LW * C;
+    auto put = [&](int ch, int p, float v) {
+        if (cfg.layout_chw) out[(size_t)ch * LW * LW + p] = v;
+        else out[(size_t)p * C + ch] = v;
+    };
+    const int nr = sh.nr;
+    int ch = 0;
+
+    // channels 0 (overhead) and 1 (robot map): robot stamps evaluated per global pixel
+    {
+        const float *ovh = overhead + (size_t)n * H * W;
+#pragma unroll 1
+        for (int k = 0; k < PPT; k++) {
+            const int p = tid + k * NT;
+            float vseg = 0.0f, vrob = 0.0f, vov = 0.0f;
+            if (gpix[k] >= 0) {
+                const int gi = gpix[k] >> 16, gj = gpix[k] & 0xffff;
+                for (int q = 0; q < nr; q++) {
+                    const RobotP &P = sh.rob[q];
+                    const int o0 = gi - P.st_i, o1 = gj - P.st_j;
+                    if (o0 < 0 || o0 >= P.S0 || o1 < 0 || o1 >= P.S1) continue;
+                    const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
+                    int m0, m1;
+                    if (!rot_src(R, LW, o0, o1, m0, m1)) continue;
+                    if (mask_bit(geo, P.type, false, m0, m1)) {
+                        vseg = fmaxf(vseg, P.seg_val);
+                        if (P.type != SIMAPS_LIFTING || !P.lifting) vrob = fmaxf(vrob, (P.type == SIMAPS_LIFTING) ? 0.5f : 1.0f);
+                    }
+                    if (P.type == SIMAPS_LIFTING && P.lifting && mask_bit(geo, SIMAPS_LIFTING, true, m0, m1)) vrob = fmaxf(vrob, 1.0f);
+                }
+                vov = vseg > 0.0f ? vseg : ovh[(size_t)gi * W + gj];
+            }
+            put(0, p, vov);
+            if (cfg.use_robot_map) put(1, p, vrob);
+        }
+        ch = cfg.use_robot_map ? 2 : 1;
+    }
+
+    // distance channels (local -= local.min(), envs.py:2213-2216): up to 3, kept in registers
+    {
+        const int has_eu = cfg.use_distance_to_receptacle_map ? 1 : 0;
+        const int nd = has_eu + nsrc;
+        if (nd > 0) {
+            float vals[3][PPT];
+            float mins[3];
+            const float sps = (float)cfg.shortest_path_map_scale;
+            const float eus = (float)cfg.distance_to_receptacle_map_scale;
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                mins[q] = INFINITY;
+                if (q >= nd) continue;
+                const bool eu = q < has_eu;  // Euclidean map first (envs.py:2083-2084)
+                const int s = q - has_eu;
+                const float *D = dist + (eu ? 0 : s) * DIST_FLOATS;
+                const float unreach = eu ? 0.0f : (sh.dmax[eu ? 0 : s] / 96.0f) * sps;
+#pragma unroll
+                for (int k = 0; k < PPT; k++) {
+                    float v = 0.0f;
+                    if (gpix[k] >= 0) {
+                        const int gi = gpix[k] >> 16, gj = gpix[k] & 0xffff;
+                        if (eu) {  // envs.py:2278-2286
+                            const double px = ((gj + 0.5) - (double)W / 2) / PPM, py = ((double)H / 2 - (gi + 0.5)) / PPM;
+                            const double dx = ev.receptacle_x - px, dy = ev.receptacle_y - py;
+                            v = (float)sqrt(dx * dx + dy * dy) * eus;
+                        } else {  // envs.py:2288-2300, 2514-2517
+                            const int r = gi - sh.i0, c = gj - sh.j0;
+                            float dd = __int_as_float(INF_BITS);
+                            if (r >= 0 && r < sh.h && c >= 0 && c < sh.w) dd = D[(r + 1) * (sh.w + 2) + c + 1];
+                            v = dd != __int_as_float(INF_BITS) ? (dd / 96.0f) * sps : unreach;
+                        }
+                    }
+                    vals[q][k] = v;
+                    mins[q] = fminf(mins[q], v);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                if (q >= nd) continue;
+                const float m = wave_min(mins[q]);
+                if ((tid & 63) == 0) sh.red[q & 1][tid >> 6] = m;
+                __syncthreads();
+                float mm = sh.red[q & 1][0];
+                for (int k = 1; k < NT / 64; k++) mm = fminf(mm, sh.red[q & 1][k]);
+                mins[q] = mm;
+            }
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                if (q >= nd) continue;
+#pragma unroll
+                for (int k = 0; k < PPT; k++) put(ch + q, tid + k * NT, vals[q][k] - mins[q]);
+            }
+            ch += nd;
+            __syncthreads();
+        }
+    }
+
+    // history / intention maps (rasterised into the LDS tile, which reuses the SSSP scratch)
+    const int thick = cfg.intention_map_line_thickness;
+    for (int pass = 0; pass < 2; pass++) {
+        const bool on = pass == 0 ? cfg.use_history_map : cfg.use_intention_map;
+        if (!on) continue;
+        raster_lines(sh, tile, cfg, rb, paths, pass == 0 ? 4 : cfg.intention_map_encoding);
+        for (int k = 0; k < PPT; k++) {
+            float v = 0.0f;
+            if (gpix[k] >= 0) v = tile_sample(tile, thick, gpix[k] >> 16, gpix[k] & 0xffff, sh.pi, sh.pj);
+            put(ch, tid + k * NT, v);
+        }
+        ch++;
+        __syncthreads();
+    }
+
+    // baseline intention channels (Mapper._get_intention_channels, envs.py:2349-2378)
+    if (cfg.use_intention_channels) {
+        if (tid == 0) {
+            // np.argsort of distances (insertion sort for n <= 16 -> stable)
+            double dd[SIMAPS_MAX_ROBOTS];
+            const RobotP &M = sh.rob[sh.me];
+            for (int q = 0; q < nr; q++) {
+                const double dx = sh.rob[q].x - M.x, dy = sh.rob[q].y - M.y;
+                dd[q] = sqrt(dx * dx + dy * dy);
+                int j = q;
+                while (j > 0 && dd[sh.order[j - 1]] > dd[q]) { sh.order[j] = sh.order[j - 1]; j--; }
+                sh.order[j] = q;
+            }
+            if (!cfg.intention_channel_spatial) {
+                int c2 = 0;
+                for (int q = 0; q < nr; q++) {
+                    const int k = sh.order[q];
+                    if (k == sh.me) continue;
+                    const RobotP &R = sh.rob[k];
+                    double rel0 = 0.0, rel1 = 0.0;
+                    if (!R.idle) {
+                        const double dx = R.tx - M.x, dy = R.ty - M.y;
+                        const double dist_t = sqrt(dx * dx + dy * dy);
+                        const double th = rb[sh.me].heading - atan2(R.ty - M.y, R.tx - M.x);
+                        rel0 = dist_t * sin(th);
+                        rel1 = dist_t * cos(th);
+                    }
+                    sh.nonsp[c2++] = (float)(cfg.intention_channel_nonspatial_scale * rel0);
+                    sh.nonsp[c2++] = (float)(cfg.intention_channel_nonspatial_scale * rel1);
+                }
+            }
+        }
+        __syncthreads();
+        int c2 = 0;
+        const float scale_f = (float)cfg.intention_map_scale;
+        for (int q = 0; q < nr; q++) {
+            const int kq = sh.order[q];
+            if (kq == sh.me) continue;
+            if (cfg.intention_channel_spatial) {
+                const RobotP &R = sh.rob[kq];
+                for (int k = 0; k < PPT; k++) {
+                    float v = 0.0f;
+                    if (gpix[k] >= 0 && !R.idle) {
+                        const int di = abs((gpix[k] >> 16) - R.tpi), dj = abs((gpix[k] & 0xffff) - R.tpj);
+                        const bool hit = thick > 1 ? (di + dj <= 1) : (di == 0 && dj == 0);
+                        v = hit ? scale_f : 0.0f;
+                    }
+                    put(ch, tid + k * NT, v);
+                }
+                ch++;
+            } else {
+                for (int e = 0; e < 2; e++, ch++, c2++)
+                    for (int k = 0; k < PPT; k++) put(ch, tid + k * NT, sh.nonsp[c2]);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// GridGraph.shortest_path_image for arbitrary grids (one workgroup per grid)
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(NT) sssp_grid_kernel(int H, int W, const uint8_t *__restrict__ grids,
+                                                      const int32_t *__restrict__ sources, float *__restrict__ out,
+                                                      int wi0, int wj0, int wh, int ww)
+{
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    Shared &sh = *reinterpret_cast<Shared *>(smem);
+    float *dist = reinterpret_cast<float *>(smem + OFF_DIST);
+    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint8_t *grid = grids + (size_t)b * H * W;
+    if (tid == 0) {
+        sh.h = wh; sh.w = ww; sh.i0 = wi0; sh.j0 = wj0;
+        const int si = sources[2 * b], sj = sources[2 * b + 1];
+        const bool ok = si >= wi0 && si < wi0 + wh && sj >= wj0 && sj < wj0 + ww && grid[(size_t)si * W + sj] != 0;
+        sh.src_s[0][0] = si; sh.src_s[0][1] = sj; sh.src_ok[0] = ok;
+    }
+    const int nwords = (ww + 63) >> 6;
+    for (int item = wave; item < wh * 2; item += NT / 64) {
+        const int rr = item >> 1, wd = item & 1, c = wd * 64 + lane;
+        const bool f = wd < nwords && c < ww && grid[(size_t)(wi0 + rr) * W + wj0 + c] != 0;
+        const uint64_t m = __ballot(f);
+        if (lane == 0) { if (wd == 0) S.freeb[rr].lo = m; else S.freeb[rr].hi = m; }
+    }
+    __syncthreads();
+    sssp(sh, S, dist, 1);
+    for (int k = tid; k < H * W; k += NT) {
+        const int i = k / W - wi0, j = k % W - wj0;
+        float v = -1.0f;
+        if (i >= 0 && i < wh && j >= 0 && j < ww) {
+            const float d = dist[(i + 1) * (ww + 2) + j + 1];
+            if (d != __int_as_float(INF_BITS)) v = d;
+        }
+        out[(size_t)b * H * W + k] = v;
+    }
+}
+
+}  // namespace
+
+// =================================================================================================
+// C ABI
+// =================================================================================================
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+namespace {
+thread_local char g_err[512] = "";
+
+int fail(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+// Robot geometry with the reference's own expressions (envs.py:802-810, 1060, 1280, 2218-2242, 2421).
+Geometry make_geometry()
+{
+    Geometry g;
+    const double HALF_WIDTH = 0.03, BACKPACK_OFFSET = -0.0135, BASE_LENGTH = 0.065, CUBE_WIDTH = 0.044;
+    const double bl[4] = {BASE_LENGTH, BASE_LENGTH + 0.005, BASE_LENGTH + 0.006, BASE_LENGTH};
+    for (int t = 0; t < 4; t++) {
+        const double ee = BACKPACK_OFFSET + bl[t];
+        const double radius = std::sqrt(HALF_WIDTH * HALF_WIDTH + ee * ee);
+        g.base_length[t] = bl[t];
+        g.cspace_r[t] = (int)std::floor(radius * 96.0);
+        g.mask_width[t] = (int)std::ceil(2 * radius * 96.0);
+        g.mask_start[t] = (int)std::floor(96 / 2.0 - g.mask_width[t] / 2.0);
+    }
+    g.cube_w = (int)std::ceil(CUBE_WIDTH * 96.0);
+    g.pad = 0;
+    g.half_width = HALF_WIDTH;
+    g.half_width_sq = HALF_WIDTH * HALF_WIDTH;
+    g.backpack_offset = BACKPACK_OFFSET;
+    g.cube_half = CUBE_WIDTH / 2;
+    g.cube_width = CUBE_WIDTH;
+    g.cube_base = (BACKPACK_OFFSET + BASE_LENGTH) + (-0.007);  // LiftingRobot END_EFFECTOR + LIFTED_CUBE_OFFSET
+    return g;
+}
+
+int check_cfg(const simaps_config *c)
+{
+    if (!c) return fail(SIMAPS_EINVAL, "cfg is NULL");
+    if (c->H <= 0 || c->W <= 0 || c->H > 32767 || c->W > 32767) return fail(SIMAPS_EINVAL, "bad grid %dx%d", c->H, c->W);
+    if (c->room_h <= 0 || c->room_w <= 0 || c->room_i0 < 0 || c->room_j0 < 0 || c->room_i0 + c->room_h > c->H ||
+        c->room_j0 + c->room_w > c->W)
+        return fail(SIMAPS_EINVAL, "room rect outside the grid");
+    if (c->room_w > SIMAPS_MAX_ROOM_W || c->room_h > MAX_ROWS || (c->room_h + 2) * (c->room_w + 2) > SIMAPS_MAX_ROOM_CELLS)
+        return fail(SIMAPS_EUNSUPPORTED, "room rect %dx%d exceeds the LDS-resident limit", c->room_h, c->room_w);
+    if (c->intention_map_encoding < 0 || c->intention_map_encoding > 3) return fail(SIMAPS_EINVAL, "bad intention encoding");
+    if (c->intention_map_line_thickness < 1 || c->intention_map_line_thickness > 2)
+        return fail(SIMAPS_EUNSUPPORTED, "intention_map_line_thickness must be 1 or 2");
+    if (c->intention_map_scale < 0) return fail(SIMAPS_EUNSUPPORTED, "negative intention_map_scale");
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int simaps_abi_version(void) { return SIMAPS_ABI_VERSION; }
+
+const char *simaps_last_error(void) { return g_err; }
+
+int simaps_num_channels(const simaps_config *c, int num_robots)
+{
+    if (!c) return fail(SIMAPS_EINVAL, "cfg is NULL");
+    int n = 1 + !!c->use_robot_map + !!c->use_distance_to_receptacle_map + !!c->use_shortest_path_to_receptacle_map +
+            !!c->use_shortest_path_map + !!c->use_history_map + !!c->use_intention_map;
+    if (c->use_intention_channels) n += (c->intention_channel_spatial ? 1 : 2) * (num_robots - 1);
+    return n;
+}
+
+int simaps_robot_mask(int type, int with_cube, float *out)
+{
+    if (type < 0 || type > 3 || !out) return fail(SIMAPS_EINVAL, "bad robot type / output");
+    if (with_cube && type != SIMAPS_LIFTING) return fail(SIMAPS_EINVAL, "lifted cube mask is LiftingRobot only");
+    const Geometry g = make_geometry();
+    for (int i = 0; i < LW; i++)
+        for (int j = 0; j < LW; j++) out[i * LW + j] = mask_bit(g, type, with_cube != 0, i, j) ? 1.0f : 0.0f;
+    return 0;
+}
+
+int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                     const simaps_robot *robots, const double *paths, const uint8_t *occupancy, const float *overhead,
+                     float *state, int num_robots_per_env, const simaps_debug *dbg, void *stream)
+{
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (N < 0) return fail(SIMAPS_EINVAL, "N < 0");
+    if (N == 0) return 0;
+    if (!agents || !envs || !robots || !occupancy || !overhead || !state) return fail(SIMAPS_EINVAL, "NULL buffer");
+    if ((cfg->use_intention_map || cfg->use_history_map) && !paths) return fail(SIMAPS_EINVAL, "paths is NULL");
+    if (cfg->use_intention_channels && (num_robots_per_env < 1 || num_robots_per_env > SIMAPS_MAX_ROBOTS))
+        return fail(SIMAPS_EINVAL, "intention channels need num_robots_per_env in [1, %d]", SIMAPS_MAX_ROBOTS);
+    const int C = simaps_num_channels(cfg, num_robots_per_env > 0 ? num_robots_per_env : 1);
+    simaps_debug d;
+    memset(&d, 0, sizeof(d));
+    if (dbg) d = *dbg;
+    hipLaunchKernelGGL(get_state_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, make_geometry(), agents, envs,
+                       robots, paths, occupancy, overhead, state, C, d);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "get_state launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *sources, float *dists, int wi0, int wj0,
+                     int wh, int ww, void *stream)
+{
+    if (B < 0 || H <= 0 || W <= 0) return fail(SIMAPS_EINVAL, "bad batch / grid shape");
+    if (B == 0) return 0;
+    if (!grids || !sources || !dists) return fail(SIMAPS_EINVAL, "NULL buffer");
+    if (wh <= 0 || ww <= 0 || wi0 < 0 || wj0 < 0 || wi0 + wh > H || wj0 + ww > W)
+        return fail(SIMAPS_EINVAL, "window outside the grid");
+    if (ww > SIMAPS_MAX_ROOM_W || wh > MAX_ROWS || (wh + 2) * (ww + 2) > SIMAPS_MAX_ROOM_CELLS)
+        return fail(SIMAPS_EUNSUPPORTED, "window %dx%d exceeds the LDS-resident limit", wh, ww);
+    hipLaunchKernelGGL(sssp_grid_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, H, W, grids, sources, dists, wi0,
+                       wj0, wh, ww);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "sssp_grid launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
+}  // extern "C"

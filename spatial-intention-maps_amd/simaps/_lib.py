@@ -1,0 +1,98 @@
+"""ctypes binding of libsimaps.so (the C ABI declared in include/simaps.h).
+
+torch is imported FIRST so that libsimaps.so binds to the HIP runtime torch already loaded
+(both resolve SONAME libamdhip64.so.7): one runtime instance, so torch device pointers and
+streams are valid in our launches.  There is no CPU fallback: if the library is missing this
+module raises at import.
+"""
+import ctypes
+import os
+
+import numpy as np
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('SIMAPS_LIB', os.path.join(HERE, 'libsimaps.so'))
+
+LIFTING, PUSHING, THROWING, RESCUE = 0, 1, 2, 3
+TYPE_IDS = {'lifting_robot': LIFTING, 'pushing_robot': PUSHING, 'throwing_robot': THROWING, 'rescue_robot': RESCUE}
+ENC_IDS = {'ramp': 0, 'binary': 1, 'line': 2, 'circle': 3}
+MAX_ROBOTS = 8
+MAX_PATH = 16
+
+# numpy mirrors of the device structs (include/simaps.h), packed C layout
+ROBOT_DTYPE = np.dtype([('x', '<f8'), ('y', '<f8'), ('heading', '<f8'), ('target_x', '<f8'), ('target_y', '<f8'),
+                        ('type', '<i4'), ('group_index', '<i4'), ('lifting', '<i4'), ('idle', '<i4'),
+                        ('intention_off', '<i4'), ('intention_len', '<i4'), ('history_off', '<i4'),
+                        ('history_len', '<i4')], align=True)
+ENV_DTYPE = np.dtype([('receptacle_x', '<f8'), ('receptacle_y', '<f8'), ('has_receptacle', '<i4'),
+                      ('robot_off', '<i4'), ('num_robots', '<i4'), ('reserved', '<i4')], align=True)
+AGENT_DTYPE = np.dtype([('env', '<i4'), ('robot', '<i4')], align=True)
+assert ROBOT_DTYPE.itemsize == 72 and ENV_DTYPE.itemsize == 32 and AGENT_DTYPE.itemsize == 8
+
+
+class Config(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        'H', 'W', 'room_i0', 'room_j0', 'room_h', 'room_w', 'use_robot_map', 'use_distance_to_receptacle_map',
+        'use_shortest_path_to_receptacle_map', 'use_shortest_path_map', 'use_intention_map',
+        'intention_map_encoding', 'intention_map_line_thickness', 'use_history_map', 'use_intention_channels',
+        'intention_channel_spatial', 'layout_chw', 'reserved')] + \
+        [(n, ctypes.c_double) for n in ('distance_to_receptacle_map_scale', 'shortest_path_map_scale',
+                                         'intention_map_scale', 'intention_channel_nonspatial_scale')]
+
+
+class Debug(ctypes.Structure):
+    _fields_ = [('cspace', ctypes.c_void_p), ('sources', ctypes.c_void_p), ('dist', ctypes.c_void_p),
+                ('status', ctypes.c_void_p)]
+
+
+class SimapsError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError('libsimaps.so not found at %s -- build it with `make -C spatial-intention-maps_amd/csrc` '
+                          '(or __graft_entry__.build()); there is no CPU fallback' % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32 = ctypes.c_void_p, ctypes.c_int
+    L.simaps_abi_version.restype = i32
+    L.simaps_last_error.restype = ctypes.c_char_p
+    L.simaps_num_channels.argtypes = [ctypes.POINTER(Config), i32]
+    L.simaps_num_channels.restype = i32
+    L.simaps_robot_mask.argtypes = [i32, i32, vp]
+    L.simaps_robot_mask.restype = i32
+    L.simaps_get_state.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, vp, i32,
+                                   ctypes.POINTER(Debug), vp]
+    L.simaps_get_state.restype = i32
+    L.simaps_sssp_grid.argtypes = [i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp]
+    L.simaps_sssp_grid.restype = i32
+    if L.simaps_abi_version() != 1:
+        raise ImportError('libsimaps ABI version mismatch')
+    return L
+
+
+lib = _load()
+
+EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_num_channels', 'simaps_robot_mask',
+            'simaps_get_state', 'simaps_sssp_grid')
+
+
+def check(rc):
+    if rc != 0:
+        raise SimapsError('libsimaps error %d: %s' % (rc, lib.simaps_last_error().decode()))
+
+
+def stream_handle(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def robot_mask(robot_type, with_cube=False):
+    out = np.zeros((96, 96), dtype=np.float32)
+    check(lib.simaps_robot_mask(TYPE_IDS.get(robot_type, robot_type), int(with_cube), out.ctypes.data))
+    return out

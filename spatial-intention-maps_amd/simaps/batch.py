@@ -1,0 +1,176 @@
+"""Device-resident batches of agent-state stacks and the fused get_state launch.
+
+A StateBatch packs E envs x (their agents) of ONE configuration (same grid / flags) into HBM:
+  occupancy  u8  [N, H, W]   per-agent OccupancyMap.occupancy_map      (envs.py:2417, 2447-2450)
+  overhead   f32 [N, H, W]   per-agent global_overhead_map_without_robots (envs.py:2026, 2057-2062)
+  robots / envs / agents / paths: the per-step scene descriptor (poses, controller state, paths)
+and renders every agent's (96, 96, C) float32 stack in one kernel launch.  The per-agent maps are
+meant to stay resident across steps (the reference keeps them in each robot's Mapper); only the
+descriptor (~100 B per robot) changes per step.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from . import constants as K
+
+
+def make_config(flags, room_width, room_length, layout='hwc'):
+    H, W = K.padded_room_shape(room_width, room_length)
+    i0, j0, h, w = K.room_rect(room_width, room_length)
+    c = _lib.Config()
+    c.H, c.W, c.room_i0, c.room_j0, c.room_h, c.room_w = H, W, i0, j0, h, w
+    c.use_robot_map = int(bool(flags['use_robot_map']))
+    c.use_distance_to_receptacle_map = int(bool(flags['use_distance_to_receptacle_map']))
+    c.use_shortest_path_to_receptacle_map = int(bool(flags['use_shortest_path_to_receptacle_map']))
+    c.use_shortest_path_map = int(bool(flags['use_shortest_path_map']))
+    c.use_intention_map = int(bool(flags['use_intention_map']))
+    c.intention_map_encoding = _lib.ENC_IDS[flags['intention_map_encoding']]
+    c.intention_map_line_thickness = int(flags['intention_map_line_thickness'])
+    c.use_history_map = int(bool(flags['use_history_map']))
+    c.use_intention_channels = int(bool(flags['use_intention_channels']))
+    c.intention_channel_spatial = int(flags['intention_channel_encoding'] == 'spatial')
+    c.layout_chw = 1 if layout == 'chw' else 0
+    c.distance_to_receptacle_map_scale = float(flags['distance_to_receptacle_map_scale'])
+    c.shortest_path_map_scale = float(flags['shortest_path_map_scale'])
+    c.intention_map_scale = float(flags['intention_map_scale'])
+    c.intention_channel_nonspatial_scale = float(flags['intention_channel_nonspatial_scale'])
+    return c
+
+
+def _intention_path(r):
+    """RobotController.get_intention_path (envs.py:1475-1476)."""
+    idx = r['waypoint_index']
+    return [r['position']] + list(r['waypoint_positions'][idx:-1]) + [r['target_ee']]
+
+
+def _history_path_reversed(r):
+    """RobotController.get_history_path()[::-1] (envs.py:1478-1479, 2318)."""
+    idx = r['waypoint_index']
+    return (list(r['waypoint_positions'][:idx]) + [r['position']])[::-1]
+
+
+def pack_descriptors(scenes, agents):
+    """Host-side packing of the per-step scene descriptor into the C structs.
+
+    scenes: list of scene dicts (simaps.synthetic format); agents: list of (env_idx, robot_idx)."""
+    n_rob = sum(len(s['robots']) for s in scenes)
+    robots = np.zeros(n_rob, dtype=_lib.ROBOT_DTYPE)
+    envs = np.zeros(len(scenes), dtype=_lib.ENV_DTYPE)
+    paths = []
+    k = 0
+    for e, s in enumerate(scenes):
+        if len(s['robots']) > _lib.MAX_ROBOTS:
+            raise ValueError('at most %d robots per env' % _lib.MAX_ROBOTS)
+        envs[e]['robot_off'] = k
+        envs[e]['num_robots'] = len(s['robots'])
+        rec = s['receptacle_position']
+        envs[e]['has_receptacle'] = rec is not None
+        if rec is not None:
+            envs[e]['receptacle_x'], envs[e]['receptacle_y'] = rec[0], rec[1]
+        for r in s['robots']:
+            R = robots[k]
+            R['x'], R['y'] = r['position'][0], r['position'][1]
+            R['heading'] = r['heading']
+            R['target_x'], R['target_y'] = r['target_ee'][0], r['target_ee'][1]
+            R['type'] = _lib.TYPE_IDS[r['type']]
+            R['group_index'] = r['group_index']
+            R['lifting'] = int(r.get('lift_state') == 'lifting')
+            R['idle'] = int(bool(r['idle']))
+            for name, pts in (('intention', _intention_path(r)), ('history', _history_path_reversed(r))):
+                if len(pts) > _lib.MAX_PATH:
+                    raise ValueError('path longer than %d points' % _lib.MAX_PATH)
+                R[name + '_off'] = len(paths)
+                R[name + '_len'] = len(pts)
+                paths.extend((float(p[0]), float(p[1])) for p in pts)
+            k += 1
+    ag = np.zeros(len(agents), dtype=_lib.AGENT_DTYPE)
+    for n, (e, a) in enumerate(agents):
+        ag[n]['env'], ag[n]['robot'] = e, a
+    paths = np.array(paths if paths else [(0.0, 0.0)], dtype=np.float64).reshape(-1, 2)
+    return robots, envs, ag, paths
+
+
+def _to_dev(a, device):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(device)
+
+
+class StateBatch:
+    """One configuration's batch of agent-state stacks, resident on `device`."""
+
+    def __init__(self, scenes, agents=None, device='cuda', layout='hwc'):
+        s0 = scenes[0]
+        for s in scenes:
+            if (s['H'], s['W'], s['room_width'], s['room_length']) != (s0['H'], s0['W'], s0['room_width'], s0['room_length']) \
+                    or s['flags'] != s0['flags']:
+                raise ValueError('one StateBatch holds one configuration (grid + flags)')
+        if agents is None:
+            agents = [(e, a) for e, s in enumerate(scenes) for a in range(len(s['robots']))]
+        self.scenes, self.agents, self.device = scenes, list(agents), torch.device(device)
+        self.flags = s0['flags']
+        self.H, self.W = s0['H'], s0['W']
+        self.cfg = make_config(self.flags, s0['room_width'], s0['room_length'], layout)
+        self.num_robots = len(s0['robots'])
+        if self.flags['use_intention_channels'] and any(len(s['robots']) != self.num_robots for s in scenes):
+            raise ValueError('intention channels need the same robot count in every env of a batch')
+        self.C = _lib.lib.simaps_num_channels(self.cfg, self.num_robots)
+        self.N = len(self.agents)
+        occ = np.stack([scenes[e]['occupancy'][a] for e, a in self.agents]).astype(np.uint8)
+        ovh = np.stack([scenes[e]['overhead'][a] for e, a in self.agents]).astype(np.float32)
+        self.occupancy = torch.from_numpy(occ).to(self.device)
+        self.overhead = torch.from_numpy(ovh).to(self.device)
+        self.set_descriptors(scenes)
+        self.layout = layout
+
+    def set_descriptors(self, scenes):
+        """Upload a new per-step scene descriptor (poses, controller state, paths)."""
+        robots, envs, ag, paths = pack_descriptors(scenes, self.agents)
+        self.robots_d = _to_dev(robots, self.device)
+        self.envs_d = _to_dev(envs, self.device)
+        self.agents_d = _to_dev(ag, self.device)
+        self.paths_d = torch.from_numpy(paths).to(self.device)
+
+    def out_shape(self):
+        if self.cfg.layout_chw:
+            return (self.N, self.C, K.LOCAL_MAP_PIXEL_WIDTH, K.LOCAL_MAP_PIXEL_WIDTH)
+        return (self.N, K.LOCAL_MAP_PIXEL_WIDTH, K.LOCAL_MAP_PIXEL_WIDTH, self.C)
+
+    def alloc_state(self):
+        return torch.empty(self.out_shape(), dtype=torch.float32, device=self.device)
+
+    def alloc_debug(self):
+        h, w = self.cfg.room_h, self.cfg.room_w
+        z = lambda *s, dt: torch.empty(s, dtype=dt, device=self.device)  # noqa: E731
+        return {'cspace': z(self.N, h, w, dt=torch.uint8), 'sources': z(self.N, 2, 4, dt=torch.int32),
+                'dist': z(self.N, 2, h, w, dt=torch.float32), 'status': z(self.N, dt=torch.int32)}
+
+    def render(self, out=None, debug=None, stream=None):
+        """Launch the fused kernel: every agent's stack into `out` (allocated if None)."""
+        if out is None:
+            out = self.alloc_state()
+        assert out.is_contiguous() and tuple(out.shape) == self.out_shape() and out.dtype == torch.float32
+        dbg = None
+        if debug is not None:
+            dbg = _lib.Debug(*(debug[k].data_ptr() if debug.get(k) is not None else None
+                               for k in ('cspace', 'sources', 'dist', 'status')))
+        _lib.check(_lib.lib.simaps_get_state(
+            self.cfg, self.N, _lib.ptr(self.agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d),
+            _lib.ptr(self.paths_d), _lib.ptr(self.occupancy), _lib.ptr(self.overhead), _lib.ptr(out),
+            self.num_robots if self.flags['use_intention_channels'] else 0,
+            None if dbg is None else dbg, _lib.stream_handle(stream)))
+        return out
+
+
+def sssp_grid(grids, sources, window=None, stream=None):
+    """Batched GridGraph(grid).shortest_path_image(source) on device.
+
+    grids: uint8 tensor [B, H, W] (device), sources: int32 [B, 2].  window = (i0, j0, h, w) that
+    contains every free cell (defaults to the whole grid, which must then fit the LDS limit)."""
+    B, H, W = grids.shape
+    if window is None:
+        window = (0, 0, H, W)
+    out = torch.empty((B, H, W), dtype=torch.float32, device=grids.device)
+    src = sources.to(device=grids.device, dtype=torch.int32).contiguous()
+    _lib.check(_lib.lib.simaps_sssp_grid(B, H, W, _lib.ptr(grids.contiguous()), _lib.ptr(src), _lib.ptr(out),
+                                         *[int(x) for x in window], _lib.stream_handle(stream)))
+    return out

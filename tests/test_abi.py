@@ -1,0 +1,72 @@
+"""CPU: libsimaps.so loads, exports every symbol include/simaps.h declares, host helpers work.
+
+No kernel is launched here (no GPU in the CPU tier)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'simaps.h')
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r'\b(simaps_[a-z_0-9]+)\s*\(', txt)))
+
+
+def test_header_declares_the_abi():
+    assert declared_symbols() == sorted(['simaps_abi_version', 'simaps_last_error', 'simaps_num_channels',
+                                         'simaps_robot_mask', 'simaps_get_state', 'simaps_sssp_grid'])
+
+
+def test_library_exports_every_declared_symbol():
+    from simaps import _lib
+    for name in declared_symbols():
+        assert hasattr(_lib.lib, name), name
+        assert isinstance(getattr(_lib.lib, name), ctypes._CFuncPtr)
+    assert set(_lib.EXPORTED) == set(declared_symbols())
+    assert _lib.lib.simaps_abi_version() == 1
+
+
+def test_struct_layouts_match_header():
+    from simaps import _lib
+    assert _lib.ROBOT_DTYPE.itemsize == 72
+    assert _lib.ENV_DTYPE.itemsize == 32
+    assert _lib.AGENT_DTYPE.itemsize == 8
+    assert ctypes.sizeof(_lib.Config) == 18 * 4 + 4 * 8
+    assert ctypes.sizeof(_lib.Debug) == 4 * 8
+
+
+def test_host_robot_masks_match_reference():
+    """simaps_robot_mask (host C++) == Mapper._create_robot_mask goldens (envs.py:2218-2242)."""
+    from simaps import _lib
+    import goldens as G
+    g = G.load('masks.npz')
+    for t in ('lifting_robot', 'pushing_robot', 'throwing_robot', 'rescue_robot'):
+        assert np.array_equal(_lib.robot_mask(t), g[t]), t
+    assert np.array_equal(_lib.robot_mask('lifting_robot', True), g['lifting_robot_with_cube'])
+
+
+@pytest.mark.parametrize('cfg_name', ['lifting_1-small_empty', 'lifting_4-small_divider', 'rescue_4-small_empty',
+                                      'lifting_4-large_empty-nonspatial', 'lifting_2_pushing_2-large_empty-all'])
+def test_num_channels(cfg_name):
+    from simaps import _lib, batch, synthetic
+    flags = synthetic.config_flags(cfg_name)
+    cfg = synthetic.CONFIGS[cfg_name]
+    nr = sum(sum(g.values()) for g in cfg['robot_config'])
+    c = batch.make_config(flags, 0.5 if cfg['env_name'].startswith('small') else 1.0, 1.0)
+    assert _lib.lib.simaps_num_channels(c, nr) == synthetic.num_channels(flags, nr)
+
+
+def test_error_paths_do_not_launch():
+    from simaps import _lib, batch, synthetic
+    flags = synthetic.config_flags('lifting_4-small_divider')
+    c = batch.make_config(flags, 0.5, 1.0)
+    assert _lib.lib.simaps_get_state(c, 0, None, None, None, None, None, None, None, 0, None, None) == 0
+    c.intention_map_line_thickness = 5
+    rc = _lib.lib.simaps_get_state(c, 1, None, None, None, None, None, None, None, 0, None, None)
+    assert rc == -2 and b'thickness' in _lib.lib.simaps_last_error()
+    assert _lib.lib.simaps_sssp_grid(1, 300, 300, None, None, None, 0, 0, 300, 300, None) == -1

@@ -1,0 +1,165 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference goldens and the oracle.
+
+Bar (BASELINE.json north_star): bit-exact for the integer channels / intermediates (cspace,
+snapped sources), and within 1e-5 for float channels -- we assert BIT-EXACT everywhere except
+the nonspatial intention channels, whose fp64 sin/cos/atan2 come from the device libm (OCML)
+instead of glibc and may differ in the last f32 bit (tolerance 1e-7 absolute there).
+"""
+import numpy as np
+import pytest
+import torch
+
+import goldens as G
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def S():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a GPU (run with -m gpu on an MI355X)')
+    from simaps import batch, constants, synthetic
+    return batch, constants, synthetic
+
+
+def _bitwise(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and np.array_equal(a.view(np.int32), b.view(np.int32))
+
+
+def _nonspatial_slice(flags, nr):
+    if not (flags['use_intention_channels'] and flags['intention_channel_encoding'] == 'nonspatial'):
+        return None
+    c0 = 1 + sum(bool(flags[k]) for k in ('use_robot_map', 'use_distance_to_receptacle_map',
+                                          'use_shortest_path_to_receptacle_map', 'use_shortest_path_map',
+                                          'use_history_map', 'use_intention_map'))
+    return slice(c0, c0 + 2 * (nr - 1))
+
+
+def _check_state(got, ref, flags, nr):
+    ns = _nonspatial_slice(flags, nr)
+    if ns is None:
+        assert _bitwise(got, ref), 'max abs diff %g' % np.abs(got - ref).max()
+    else:
+        mask = np.ones(got.shape[-1], bool)
+        mask[ns] = False
+        assert _bitwise(np.ascontiguousarray(got[..., mask]), np.ascontiguousarray(ref[..., mask]))
+        assert np.abs(got[..., ns] - ref[..., ns]).max() <= 1e-7
+
+
+GOLD = list(G.scene_cases())
+
+
+@pytest.mark.parametrize('case', GOLD, ids=['%s-e%d-a%d' % c[:3] for c in GOLD])
+def test_golden_scene_state_and_intermediates(S, case):
+    batch, K, synthetic = S
+    cfg, e, a, scene, pre, z = case
+    b = batch.StateBatch([scene], agents=[(0, a)])
+    dbg = b.alloc_debug()
+    st = b.render(debug=dbg)
+    torch.cuda.synchronize()
+    flags = scene['flags']
+    assert int(dbg['status'][0]) & 0xff == 0
+    assert np.array_equal(dbg['cspace'][0].cpu().numpy(), z[pre + 'cspace_rect'])
+    src = dbg['sources'][0].cpu().numpy()
+    dist = dbg['dist'][0].cpu().numpy()
+    if flags['use_shortest_path_to_receptacle_map']:
+        assert np.array_equal(src[0], z[pre + 'src_receptacle'])
+        assert _bitwise(dist[0], z[pre + 'sp_receptacle_rect'])
+    if flags['use_shortest_path_map']:
+        assert np.array_equal(src[1], z[pre + 'src_robot'])
+        assert _bitwise(dist[1], z[pre + 'sp_robot_rect'])
+    _check_state(st[0].cpu().numpy(), z[pre + 'state'], flags, len(scene['robots']))
+
+
+def test_layout_chw_matches_hwc(S):
+    batch, K, synthetic = S
+    scenes = [synthetic.make_scene('lifting_2_pushing_2-large_empty-all', e) for e in range(3)]
+    hwc = batch.StateBatch(scenes).render().cpu().numpy()
+    chw = batch.StateBatch(scenes, layout='chw').render().cpu().numpy()
+    assert _bitwise(np.transpose(chw, (0, 2, 3, 1)), hwc)
+
+
+@pytest.mark.parametrize('cfg', ['lifting_1-small_empty', 'lifting_4-small_divider', 'pushing_4-large_empty',
+                                 'lifting_2_throwing_2-large_empty', 'rescue_4-small_empty',
+                                 'lifting_4-small_divider-history', 'lifting_4-large_empty-line',
+                                 'lifting_4-small_empty-circle', 'lifting_4-small_divider-spatial',
+                                 'lifting_4-large_empty-nonspatial', 'lifting_2_pushing_2-large_empty-all'])
+def test_oracle_parity_fresh_seeds(S, cfg):
+    """Seeds never used for the goldens: every agent of 6 envs vs the (golden-pinned) oracle."""
+    batch, K, synthetic = S
+    scenes = [synthetic.make_scene(cfg, 100 + e) for e in range(6)]
+    b = batch.StateBatch(scenes)
+    st = b.render().cpu().numpy()
+    for n, (e, a) in enumerate(b.agents):
+        _check_state(st[n], O.agent_state(scenes[e], a), scenes[e]['flags'], len(scenes[e]['robots']))
+
+
+def test_full_size_lifting_4_small_divider_properties(S):
+    """BASELINE configs[1] size (64 envs x 4 agents): determinism, channel invariants, and a
+    seeded sample of agents against the oracle."""
+    batch, K, synthetic = S
+    scenes = [synthetic.make_scene('lifting_4-small_divider', e) for e in range(64)]
+    b = batch.StateBatch(scenes)
+    s1 = b.render().cpu().numpy()
+    s2 = b.render().cpu().numpy()
+    assert _bitwise(s1, s2)                       # idempotent / deterministic
+    assert s1.shape == (256, 96, 96, 5)
+    assert np.all(s1[..., 0] <= 1) and np.all(s1 >= 0)
+    assert np.all(s1[..., 2].reshape(256, -1).min(1) == 0) and np.all(s1[..., 3].reshape(256, -1).min(1) == 0)
+    assert set(np.unique(s1[..., 1])) <= {0.0, 0.5, 1.0}
+    assert set(np.unique(s1[..., 0])) <= {k / 8 for k in range(9)}
+    rs = np.random.RandomState(7)
+    for n in rs.choice(256, 12, replace=False):
+        e, a = b.agents[n]
+        assert _bitwise(s1[n], O.agent_state(scenes[e], a))
+
+
+def test_snap_slow_path_and_idle(S):
+    """Agents pressed against walls / divider (query pixel not free -> EDT snap), all robots idle."""
+    batch, K, synthetic = S
+    scenes = []
+    for e in range(8):
+        s = synthetic.make_scene('lifting_4-small_divider', 300 + e, observe_all=True)
+        for k, r in enumerate(s['robots']):
+            x = (-0.5 + 0.03) if k % 2 == 0 else (0.5 - 0.02 - 0.01 * e)
+            y = (0.25 - 0.02) if k < 2 else (-0.25 + 0.04)
+            r['position'] = (x, y, 0)
+            r['waypoint_positions'][0] = r['position']
+            r['idle'] = e % 2 == 0
+        scenes.append(s)
+    b = batch.StateBatch(scenes)
+    dbg = b.alloc_debug()
+    st = b.render(debug=dbg).cpu().numpy()
+    src = dbg['sources'].cpu().numpy()
+    assert (src[:, 1, :2] != src[:, 1, 2:]).any(), 'expected at least one snapped robot source'
+    for n, (e, a) in enumerate(b.agents):
+        assert _bitwise(st[n], O.agent_state(scenes[e], a))
+
+
+def test_sssp_grid_demo_known_answer(S):
+    """shortest_paths/demo.py sample: distance 136.46806 and the full image, + 12 more sources."""
+    batch, K, synthetic = S
+    g = G.load('sssp.npz')
+    grid = g['demo_cspace']
+    fr = np.argwhere(grid > 0)
+    (i0, j0), (i1, j1) = fr.min(0), fr.max(0)
+    win = (int(i0), int(j0), int(i1 - i0 + 1), int(j1 - j0 + 1))
+    srcs = [(75, 156)] + [tuple(int(x) for x in p) for p in g['demo_sources']]
+    grids = torch.from_numpy(np.repeat(grid[None], len(srcs), 0)).cuda()
+    out = batch.sssp_grid(grids, torch.tensor(srcs, dtype=torch.int32), window=win).cpu().numpy()
+    assert _bitwise(out[0], g['demo_image'])
+    assert out[0][131, 112] == g['demo_distance']
+    for q, (i, j) in enumerate(srcs[1:]):
+        assert _bitwise(out[q + 1], O.spfa_image(grid, (i, j)))
+
+
+def test_sssp_grid_random(S):
+    batch, K, synthetic = S
+    g = G.load('sssp.npz')
+    for q in range(10):
+        grid = g['rand_grid_%d' % q]
+        src = torch.tensor([tuple(int(x) for x in g['rand_src_%d' % q])], dtype=torch.int32)
+        out = batch.sssp_grid(torch.from_numpy(grid[None].copy()).cuda(), src).cpu().numpy()
+        assert _bitwise(out[0], g['rand_img_%d' % q]), q
