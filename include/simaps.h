@@ -50,7 +50,7 @@ extern "C" {
 /* limits of this build */
 #define SIMAPS_MAX_ROBOTS 8      /* robots per env */
 #define SIMAPS_MAX_PATH 16       /* points per intention / history path */
-#define SIMAPS_MAX_ROOM_CELLS 8836 /* (room_h + 2) * (room_w + 2) */
+#define SIMAPS_MAX_ROOM_CELLS 9024 /* (room_h + 2) * ((room_w + 2) | 1) */
 #define SIMAPS_MAX_ROOM_W 120
 
 /* One robot of an env, as the observation path reads it (Robot / RobotController state). */
@@ -141,7 +141,7 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
 /* Batched GridGraph(grid).shortest_path_image(source):
  *   grids [B, H, W] uint8 (nonzero = free), sources [B, 2] int32 (row, col), out dists [B, H, W]
  *   float32 (-1 unreachable, like pyx:110-112), all DEVICE.  All free cells of every grid must lie
- *   in the window rows [wi0, wi0+wh) x cols [wj0, wj0+ww) with (wh+2)*(ww+2) <= SIMAPS_MAX_ROOM_CELLS
+ *   in the window rows [wi0, wi0+wh) x cols [wj0, wj0+ww) with (wh+2)*((ww+2)|1) <= SIMAPS_MAX_ROOM_CELLS
  *   and ww <= SIMAPS_MAX_ROOM_W (cells outside the window are treated as blocked). */
 int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *sources, float *dists,
                      int wi0, int wj0, int wh, int ww, void *stream);

@@ -36,6 +36,20 @@ using namespace simaps;
 namespace {
 
 constexpr int NT = 1024;
+#ifdef SIMAPS_PHASE_STAMPS
+// Diagnostic build only (libsimaps_prof.so): per-workgroup s_memrealtime (100 MHz) stamps.
+constexpr int MAX_STAMP_WG = 8192, NSTAMP = 16;
+__device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
+#define STAMP(k)                                                                                 \
+    do {                                                                                         \
+        if (threadIdx.x == 0 && blockIdx.x < MAX_STAMP_WG)                                       \
+            g_stamps[blockIdx.x * NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime();              \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
 constexpr int MAX_SEG = 128;     // intention / history segments per agent
 constexpr int SEG_PER_ROBOT = SIMAPS_MAX_PATH - 1;
 constexpr int MAX_ROWS = 112;    // room rect rows (bit-row arrays)
@@ -93,6 +107,7 @@ struct RobotP {
     int S0, S1, st_i, st_j;  // stamp shape, placement (pixel - S // 2, envs.py:2272)
     int type, lifting, idle, group;
     int tpi, tpj;            // target end-effector pixel
+    int bi0, bi1, bj0, bj1;  // global-pixel box outside which the rotated mask is surely 0
     float seg_val, pad;
 };
 
@@ -129,12 +144,12 @@ struct SsspScratch {
     uint64_t win[MAX_WIN_ROWS][WIN_WORDS];
     B128 blocked[MAX_ROWS];
     B128 freeb[MAX_ROWS];
-    B128 bits[2][3][MAX_ROWS];  // [source][prev/cand/next][row]
+    int changed[3];  // rotating per-round "some sweep improved a cell" flags
 };
 
 constexpr int align16(int x) { return (x + 15) & ~15; }
 constexpr int OFF_DIST = align16((int)sizeof(Shared));
-constexpr int DIST_FLOATS = SIMAPS_MAX_ROOM_CELLS;
+constexpr int DIST_FLOATS = SIMAPS_MAX_ROOM_CELLS;  // (h + 2) * pitch, pitch = (w + 2) | 1
 constexpr int OFF_UNION = OFF_DIST + align16(2 * DIST_FLOATS * 4);
 constexpr int TILE_BYTES = TILE * TILE * 4;
 constexpr int UNION_BYTES = align16((int)sizeof(SsspScratch) > TILE_BYTES ? (int)sizeof(SsspScratch) : TILE_BYTES);
@@ -277,92 +292,127 @@ __device__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc)
 // ------------------------------------------------------------------------------------------------
 // Phase: single-source shortest paths for nsrc sources over the free cells of the rect
 // ------------------------------------------------------------------------------------------------
-// dist[s]: (h + 2) x (w + 2) float32, padded with +inf.  Result: exact float32 SPFA distances,
-// +inf where unreachable / not free.  sh.dmax[s] = max reachable distance.
+// Directional sweeps.  Per source, four waves sweep the LDS-resident distance array concurrently:
+// down / up (row by row, lanes own 2 columns each) and right / left (column by column, lanes own 2
+// rows each).  A sweep step relaxes every cell of a line from the 3 cells of the previous line
+// (straight + 2 diagonals); the previous line's new values stay in registers and reach the
+// neighbouring lanes by DPP wave shifts, so a path that is monotone in the sweep direction is
+// settled in ONE pass.  Rounds of 4 concurrent sweeps repeat until a round changes nothing.
+// Every write is min(current, fl(d_u + w)) for a real edge, i.e. a valid relaxation (plain stores:
+// a racing sweep can only lose an improvement, which re-triggers a round), so the result is the
+// unique float32 fixpoint = the reference SPFA's distances, bit for bit.
+// Layout: dist[s] = (h + 2) x pitch float32, +inf border, pitch = (w + 2) | 1 (odd: column-wise
+// sweeps hit at most 2-way LDS bank conflicts).  Blocked cells stay +inf.
+
+__device__ __forceinline__ float from_prev_lane(float v)  // lane i <- lane i-1 (lane 0 <- +inf)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp((int)INF_BITS, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float from_next_lane(float v)  // lane i <- lane i+1 (lane 63 <- +inf)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp((int)INF_BITS, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ int sssp_pitch(int w) { return (w + 2) | 1; }
+
+// One sweep of one wave.  dir: 0 down, 1 up, 2 right, 3 left.  Returns true if it improved a cell.
+// Blocked and padding cells hold a quiet NaN: every comparison with NaN is false, so a blocked cell
+// is never written and its NaN never wins a min (v_min3 drops NaN operands) -- no free-bit tests.
+constexpr unsigned QNAN_BITS = 0x7fc00000u;
+
+__device__ bool sweep(float *D, float *dummy, int h, int w, int pw, int dir_in)
+{
+    const int lane = threadIdx.x & 63;
+    const int dir = __builtin_amdgcn_readfirstlane(dir_in);
+    const bool vert = dir < 2;
+    const int len = vert ? h : w, span = vert ? w : h;
+    const int sl = vert ? pw : 1, sa = vert ? 1 : pw;  // address strides along / across the line
+    const int a0 = 1 + 2 * lane;
+    const bool v0 = a0 <= span, v1 = a0 + 1 <= span;
+    const bool fwd = (dir & 1) == 0;
+    const int dl = fwd ? sl : -sl;
+    // lanes past the span read / never write: point them at a padding cell (NaN)
+    int ad0 = v0 ? (fwd ? 1 : len) * sl + a0 * sa : 0;
+    int ad1 = v1 ? ad0 + sa : 0;
+    const int st0 = v0 ? dl : 0, st1 = v1 ? dl : 0;
+    const float QN = __int_as_float(QNAN_BITS);
+    float p0 = QN, p1 = QN;
+    bool changed = false;
+    // Two register pairs (A: even lines, B: odd lines), each refilled with the line two ahead
+    // right after its old value is consumed: no register rotation at the back-edge, so each
+    // load has a whole step to land.  Padding rows beyond the last line are NaN (never used).
+    float A0 = D[ad0], A1 = D[ad1];
+    float B0 = D[ad0 + st0], B1 = D[ad1 + st1];
+    auto step = [&](float &R0, float &R1, int) {
+        const float pm = from_prev_lane(p1);  // previous line, across index a0 - 1
+        const float pp = from_next_lane(p0);  // previous line, across index a0 + 2
+        const float m0 = fminf(fminf(p0 + 1.0f, pm + SQRT2F), p1 + SQRT2F);
+        const float m1 = fminf(fminf(p1 + 1.0f, p0 + SQRT2F), pp + SQRT2F);
+        const bool u0 = m0 < R0, u1 = m1 < R1;  // false for NaN (blocked) d or NaN m
+        const float c0 = u0 ? m0 : R0, c1 = u1 ? m1 : R1;
+        // exactly 2 stores + 2 loads per step (non-improving lanes store into a private dummy slot),
+        // so the compiler's LDS counter waits stay partial and the loads overlap the next step.
+        // The final two prefetches read past the line range: still inside this kernel's LDS block.
+        *(u0 ? &D[ad0] : &dummy[2 * lane]) = c0;
+        *(u1 ? &D[ad1] : &dummy[2 * lane + 1]) = c1;
+        changed |= u0 | u1;
+        p0 = c0;
+        p1 = c1;
+        R0 = D[ad0 + 2 * st0];
+        R1 = D[ad1 + 2 * st1];
+        ad0 += st0;
+        ad1 += st1;
+    };
+    // even trip count: an odd line count ends with one extra step on the NaN padding line (no writes)
+    for (int t = 0; t < len; t += 2) {
+        step(A0, A1, t);
+        step(B0, B1, t + 1);
+    }
+    return __ballot(changed) != 0;
+}
+
 __device__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
 {
-    const int tid = threadIdx.x;
-    const int h = sh.h, w = sh.w, pw = w + 2;
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
     const int cells = (h + 2) * pw;
-    unsigned *du = reinterpret_cast<unsigned *>(dist);
-    for (int k = tid; k < nsrc * DIST_FLOATS; k += NT) du[k] = INF_BITS;
-    for (int k = tid; k < nsrc * 3 * MAX_ROWS; k += NT) (&S.bits[0][0][0])[k] = {0, 0};
-    if (tid < 2) sh.flag[tid] = 0;
-    __syncthreads();
-    if (tid < nsrc && sh.src_ok[tid]) {
-        const int r = sh.src_s[tid][0] - sh.i0, c = sh.src_s[tid][1] - sh.j0;
-        dist[tid * DIST_FLOATS + (r + 1) * pw + (c + 1)] = 0.0f;
-        B128 b = {0, 0};
-        if (c < 64) b.lo = 1ull << c; else b.hi = 1ull << (c - 64);
-        S.bits[tid][0][r] = b;
+    const float QN = __int_as_float(QNAN_BITS);
+    // free cells +inf, blocked / padding NaN
+    for (int k = tid; k < nsrc * DIST_FLOATS; k += NT) {
+        const int q = k % DIST_FLOATS, r = q / pw - 1, c = q % pw - 1;
+        const bool fr = q < cells && r >= 0 && r < h && c >= 0 && c < w && b_test(S.freeb[r], c);
+        dist[k] = fr ? INFINITY : QN;
     }
+    if (tid < 3) S.changed[tid] = 0;
     __syncthreads();
-    const int CH = (w + 7) >> 3;
-    // Bellman-Ford needs at most (#cells) rounds; the cap only guards against a bug hanging the GPU.
+    for (int s = tid; s < nsrc; s += NT)
+        if (sh.src_ok[s]) dist[s * DIST_FLOATS + (sh.src_s[s][0] - sh.i0 + 1) * pw + (sh.src_s[s][1] - sh.j0 + 1)] = 0.0f;
+    __syncthreads();
+    // a converged round changes nothing; the cap only guards against a bug hanging the GPU
     const int max_rounds = h * w + 16;
-    int prev = 0, next = 2;
     sh.rounds = 0;
     for (int round = 0;; round++) {
-        // (a) candidates = 8-dilation of last round's changed cells, restricted to free cells
-        for (int u = tid; u < nsrc * h; u += NT) {
-            const int s = u / h, rr = u % h;
-            B128 x = S.bits[s][prev][rr];
-            if (rr > 0) x = b_or(x, S.bits[s][prev][rr - 1]);
-            if (rr < h - 1) x = b_or(x, S.bits[s][prev][rr + 1]);
-            x = b_or(x, b_or(b_shl1(x), b_shr1(x)));
-            S.bits[s][1][rr] = b_and(x, S.freeb[rr]);
-            S.bits[s][next][rr] = {0, 0};
+        if (tid == 0) S.changed[(round + 1) % 3] = 0;
+        if (wave < 4 * nsrc) {
+            const int s = wave >> 2;
+            float *dummy = reinterpret_cast<float *>(&S.win[0][0]) + 128 * wave;  // dead after build_cspace
+            if (sh.src_ok[s] && sweep(dist + s * DIST_FLOATS, dummy, h, w, pw, wave & 3) && (tid & 63) == 0)
+                S.changed[round % 3] = 1;
         }
         __syncthreads();
-        if (tid == 0) sh.flag[(round + 1) & 1] = 0;
-        // (b) pull-relax every candidate cell (in place; any interleaving is a valid relaxation)
-        for (int u = tid; u < nsrc * h * CH; u += NT) {
-            const int s = u / (h * CH), rem = u % (h * CH), rr = rem / CH, ch = rem % CH;
-            const B128 cb = S.bits[s][1][rr];
-            unsigned bits = (unsigned)((ch < 8 ? (cb.lo >> (8 * ch)) : (cb.hi >> (8 * (ch - 8)))) & 0xffu);
-            if (!bits) continue;
-            float *D = dist + s * DIST_FLOATS;
-            unsigned changed = 0;
-            while (bits) {
-                const int b = __builtin_ctz(bits);
-                bits &= bits - 1;
-                const int v = (rr + 1) * pw + (ch * 8 + b + 1);
-                const float dv = D[v];
-                float best = dv, t;
-                t = D[v - 1] + 1.0f;       best = t < best ? t : best;
-                t = D[v + 1] + 1.0f;       best = t < best ? t : best;
-                t = D[v - pw] + 1.0f;      best = t < best ? t : best;
-                t = D[v + pw] + 1.0f;      best = t < best ? t : best;
-                t = D[v - pw - 1] + SQRT2F; best = t < best ? t : best;
-                t = D[v - pw + 1] + SQRT2F; best = t < best ? t : best;
-                t = D[v + pw - 1] + SQRT2F; best = t < best ? t : best;
-                t = D[v + pw + 1] + SQRT2F; best = t < best ? t : best;
-                if (best < dv) {
-                    D[v] = best;
-                    changed |= 1u << b;
-                }
-            }
-            if (changed) {
-                unsigned *nw = reinterpret_cast<unsigned *>(&S.bits[s][next][rr]);
-                atomicOr(nw + (ch >> 2), changed << (8 * (ch & 3)));
-                sh.flag[round & 1] = 1;
-            }
-        }
-        __syncthreads();
-        if (sh.flag[round & 1] == 0 || round >= max_rounds) {
+        if (!S.changed[round % 3] || round >= max_rounds) {
             if (tid == 0) sh.rounds = round >= max_rounds ? -1 : round + 1;
             break;
         }
-        const int t = prev;
-        prev = next;
-        next = t;
     }
-    // max reachable distance per source
+    __syncthreads();
+    // NaN (blocked) -> +inf; max reachable distance per source
     for (int s = 0; s < nsrc; s++) {
         float m = -1.0f;
-        for (int k = tid; k < cells; k += NT) {
-            const float d = dist[s * DIST_FLOATS + k];
-            if (d != __int_as_float(INF_BITS)) m = fmaxf(m, d);
+        for (int q = tid; q < cells; q += NT) {
+            float &d = dist[s * DIST_FLOATS + q];
+            if (d != d) d = INFINITY;
+            else if (d != INFINITY) m = fmaxf(m, d);
         }
         m = wave_max(m);
         if ((tid & 63) == 0) sh.red[0][tid >> 6] = m;
@@ -504,6 +554,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const simaps_agent ag = agents[n];
     const simaps_env ev = envs[ag.env];
     const simaps_robot *rb = robots + ev.robot_off;
+    STAMP(0);
 
     // ---- parameters (one lane per robot; the agent's own local rotation on another wave)
     if (tid == 0) {
@@ -546,11 +597,27 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         P.type = r.type; P.lifting = r.lifting; P.idle = r.idle; P.group = r.group_index;
         P.x = r.x; P.y = r.y; P.tx = r.target_x; P.ty = r.target_y;
         pos_to_pix(r.target_x, r.target_y, H, W, P.tpi, P.tpj);
+        {   // conservative prefilter box: inverse-rotate the mask's nonzero window (+-2 px)
+            const int st = geo.mask_start[r.type], wd = geo.mask_width[r.type];
+            const double lo0 = st - (r.type == SIMAPS_LIFTING ? geo.cube_w : 0) - 1.0, hi0 = st + wd + 1.0;
+            const double lo1 = st - 1.0, hi1 = st + wd + 1.0;
+            double mn0 = 1e30, mx0 = -1e30, mn1 = 1e30, mx1 = -1e30;
+            for (int q = 0; q < 4; q++) {
+                const double a = ((q & 1) ? hi0 : lo0) - R.f0, b = ((q & 2) ? hi1 : lo1) - R.f1;
+                const double o0 = R.c * a - R.s * b, o1 = R.s * a + R.c * b;
+                mn0 = fmin(mn0, o0); mx0 = fmax(mx0, o0); mn1 = fmin(mn1, o1); mx1 = fmax(mx1, o1);
+            }
+            P.bi0 = max(P.st_i, P.st_i + (int)floor(mn0) - 2);
+            P.bi1 = min(P.st_i + R.S0 - 1, P.st_i + (int)ceil(mx0) + 2);
+            P.bj0 = max(P.st_j, P.st_j + (int)floor(mn1) - 2);
+            P.bj1 = min(P.st_j + R.S1 - 1, P.st_j + (int)ceil(mx1) + 2);
+        }
         P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
     }
     __syncthreads();
 
     // ---- cspace + snap + SSSP
+    STAMP(1);
     const int nsrc = sh.nsrc;
     if (nsrc > 0 || dbg.cspace) {
         build_cspace(S, occupancy + (size_t)n * H * W, H, W, sh.i0, sh.j0, sh.h, sh.w, sh.r);
@@ -559,9 +626,12 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
                 dbg.cspace[(size_t)n * sh.h * sh.w + k] = b_test(S.freeb[k / sh.w], k % sh.w) ? 1 : 0;
         }
     }
+    STAMP(2);
     if (nsrc > 0) {
         snap_sources(sh, S, nsrc);
+        STAMP(3);
         sssp(sh, S, dist, nsrc);
+        STAMP(4);
         if (dbg.sources && tid < 2) {
             int32_t *o = dbg.sources + ((size_t)n * 2 + tid) * 4;
             const int s = sh.sp_slot[tid];
@@ -574,7 +644,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
                 const int s = sh.sp_slot[which];
                 float v = -1.0f;
                 if (s >= 0) {
-                    v = dist[s * DIST_FLOATS + (rem / sh.w + 1) * (sh.w + 2) + rem % sh.w + 1];
+                    v = dist[s * DIST_FLOATS + (rem / sh.w + 1) * sssp_pitch(sh.w) + rem % sh.w + 1];
                     if (v == __int_as_float(INF_BITS)) v = -1.0f;
                 }
                 dbg.dist[(size_t)n * 2 * sh.h * sh.w + k] = v;
@@ -589,6 +659,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     }
 
     // ---- render: each thread owns output pixels p = tid + k * NT
+    STAMP(5);
     int gpix[PPT];  // packed (gi << 16 | gj), -1 = rotate fell outside the crop (cval 0)
     {
         const Rot R = sh.rot;
@@ -616,6 +687,10 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     // channels 0 (overhead) and 1 (robot map): robot stamps evaluated per global pixel
     {
         const float *ovh = overhead + (size_t)n * H * W;
+        float ovv[PPT];
+#pragma unroll
+        for (int k = 0; k < PPT; k++)  // issue every HBM gather before any use
+            ovv[k] = gpix[k] >= 0 ? ovh[(size_t)(gpix[k] >> 16) * W + (gpix[k] & 0xffff)] : 0.0f;
 #pragma unroll 1
         for (int k = 0; k < PPT; k++) {
             const int p = tid + k * NT;
@@ -624,18 +699,17 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
                 const int gi = gpix[k] >> 16, gj = gpix[k] & 0xffff;
                 for (int q = 0; q < nr; q++) {
                     const RobotP &P = sh.rob[q];
-                    const int o0 = gi - P.st_i, o1 = gj - P.st_j;
-                    if (o0 < 0 || o0 >= P.S0 || o1 < 0 || o1 >= P.S1) continue;
+                    if (gi < P.bi0 || gi > P.bi1 || gj < P.bj0 || gj > P.bj1) continue;
                     const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
                     int m0, m1;
-                    if (!rot_src(R, LW, o0, o1, m0, m1)) continue;
+                    if (!rot_src(R, LW, gi - P.st_i, gj - P.st_j, m0, m1)) continue;
                     if (mask_bit(geo, P.type, false, m0, m1)) {
                         vseg = fmaxf(vseg, P.seg_val);
                         if (P.type != SIMAPS_LIFTING || !P.lifting) vrob = fmaxf(vrob, (P.type == SIMAPS_LIFTING) ? 0.5f : 1.0f);
                     }
                     if (P.type == SIMAPS_LIFTING && P.lifting && mask_bit(geo, SIMAPS_LIFTING, true, m0, m1)) vrob = fmaxf(vrob, 1.0f);
                 }
-                vov = vseg > 0.0f ? vseg : ovh[(size_t)gi * W + gj];
+                vov = vseg > 0.0f ? vseg : ovv[k];
             }
             put(0, p, vov);
             if (cfg.use_robot_map) put(1, p, vrob);
@@ -644,6 +718,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     }
 
     // distance channels (local -= local.min(), envs.py:2213-2216): up to 3, kept in registers
+    STAMP(6);
     {
         const int has_eu = cfg.use_distance_to_receptacle_map ? 1 : 0;
         const int nd = has_eu + nsrc;
@@ -672,7 +747,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
                         } else {  // envs.py:2288-2300, 2514-2517
                             const int r = gi - sh.i0, c = gj - sh.j0;
                             float dd = __int_as_float(INF_BITS);
-                            if (r >= 0 && r < sh.h && c >= 0 && c < sh.w) dd = D[(r + 1) * (sh.w + 2) + c + 1];
+                            if (r >= 0 && r < sh.h && c >= 0 && c < sh.w) dd = D[(r + 1) * sssp_pitch(sh.w) + c + 1];
                             v = dd != __int_as_float(INF_BITS) ? (dd / 96.0f) * sps : unreach;
                         }
                     }
@@ -702,6 +777,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     }
 
     // history / intention maps (rasterised into the LDS tile, which reuses the SSSP scratch)
+    STAMP(7);
     const int thick = cfg.intention_map_line_thickness;
     for (int pass = 0; pass < 2; pass++) {
         const bool on = pass == 0 ? cfg.use_history_map : cfg.use_intention_map;
@@ -717,6 +793,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     }
 
     // baseline intention channels (Mapper._get_intention_channels, envs.py:2349-2378)
+    STAMP(8);
     if (cfg.use_intention_channels) {
         if (tid == 0) {
             // np.argsort of distances (insertion sort for n <= 16 -> stable)
@@ -772,6 +849,10 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             }
         }
     }
+    STAMP(9);
+#ifdef SIMAPS_PHASE_STAMPS
+    if (tid == 0 && blockIdx.x < MAX_STAMP_WG) g_stamps[blockIdx.x * NSTAMP + 10] = (unsigned long long)sh.rounds;
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -806,7 +887,7 @@ __global__ void __launch_bounds__(NT) sssp_grid_kernel(int H, int W, const uint8
         const int i = k / W - wi0, j = k % W - wj0;
         float v = -1.0f;
         if (i >= 0 && i < wh && j >= 0 && j < ww) {
-            const float d = dist[(i + 1) * (ww + 2) + j + 1];
+            const float d = dist[(i + 1) * sssp_pitch(ww) + j + 1];
             if (d != __int_as_float(INF_BITS)) v = d;
         }
         out[(size_t)b * H * W + k] = v;
@@ -867,7 +948,7 @@ int check_cfg(const simaps_config *c)
     if (c->room_h <= 0 || c->room_w <= 0 || c->room_i0 < 0 || c->room_j0 < 0 || c->room_i0 + c->room_h > c->H ||
         c->room_j0 + c->room_w > c->W)
         return fail(SIMAPS_EINVAL, "room rect outside the grid");
-    if (c->room_w > SIMAPS_MAX_ROOM_W || c->room_h > MAX_ROWS || (c->room_h + 2) * (c->room_w + 2) > SIMAPS_MAX_ROOM_CELLS)
+    if (c->room_w > SIMAPS_MAX_ROOM_W || c->room_h > MAX_ROWS || (c->room_h + 2) * ((c->room_w + 2) | 1) > SIMAPS_MAX_ROOM_CELLS)
         return fail(SIMAPS_EUNSUPPORTED, "room rect %dx%d exceeds the LDS-resident limit", c->room_h, c->room_w);
     if (c->intention_map_encoding < 0 || c->intention_map_encoding > 3) return fail(SIMAPS_EINVAL, "bad intention encoding");
     if (c->intention_map_line_thickness < 1 || c->intention_map_line_thickness > 2)
@@ -880,6 +961,14 @@ int check_cfg(const simaps_config *c)
 extern "C" {
 
 int simaps_abi_version(void) { return SIMAPS_ABI_VERSION; }
+
+#ifdef SIMAPS_PHASE_STAMPS
+// Diagnostic build only: copy the stamp table (uint64 [8192][16]) to host memory.
+int simaps_debug_read_stamps(unsigned long long *host_out)
+{
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : SIMAPS_EHIP;
+}
+#endif
 
 const char *simaps_last_error(void) { return g_err; }
 
@@ -933,7 +1022,7 @@ int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *s
     if (!grids || !sources || !dists) return fail(SIMAPS_EINVAL, "NULL buffer");
     if (wh <= 0 || ww <= 0 || wi0 < 0 || wj0 < 0 || wi0 + wh > H || wj0 + ww > W)
         return fail(SIMAPS_EINVAL, "window outside the grid");
-    if (ww > SIMAPS_MAX_ROOM_W || wh > MAX_ROWS || (wh + 2) * (ww + 2) > SIMAPS_MAX_ROOM_CELLS)
+    if (ww > SIMAPS_MAX_ROOM_W || wh > MAX_ROWS || (wh + 2) * ((ww + 2) | 1) > SIMAPS_MAX_ROOM_CELLS)
         return fail(SIMAPS_EUNSUPPORTED, "window %dx%d exceeds the LDS-resident limit", wh, ww);
     hipLaunchKernelGGL(sssp_grid_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, H, W, grids, sources, dists, wi0,
                        wj0, wh, ww);

@@ -1,0 +1,53 @@
+"""Per-phase timing of get_state_kernel from the diagnostic build (libsimaps_prof.so).
+
+Loads the stamp build through SIMAPS_LIB, renders one batch (after a warm-up), and prints per-phase
+wall time (median / max over workgroups, us) plus SSSP rounds.  Diagnostic only: the stamps
+serialize nothing but add a few instructions; quote shares, not absolute kernel time."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ['SIMAPS_LIB'] = os.path.join(ROOT, 'spatial-intention-maps_amd', 'simaps', 'libsimaps_prof.so')
+sys.path.insert(0, os.path.join(ROOT, 'spatial-intention-maps_amd'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from simaps import _lib, batch, synthetic  # noqa: E402
+
+PHASES = ['params', 'cspace', 'snap', 'sssp', 'dbg/status', 'render ch0-1', 'dist ch', 'raster ch', 'intent ch']
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', default='lifting_4-small_divider')
+    ap.add_argument('--envs', type=int, default=64)
+    args = ap.parse_args()
+    L = _lib.lib
+    L.simaps_debug_read_stamps.argtypes = [ctypes.c_void_p]
+    scenes = [synthetic.make_scene(args.config, e) for e in range(args.envs)]
+    b = batch.StateBatch(scenes)
+    out = b.alloc_state()
+    for _ in range(3):
+        b.render(out)
+    torch.cuda.synchronize()
+    st = np.zeros((8192, 16), dtype=np.uint64)
+    b.render(out)
+    torch.cuda.synchronize()
+    assert L.simaps_debug_read_stamps(st.ctypes.data) == 0
+    st = st[:b.N].astype(np.int64)
+    t = st[:, :10]
+    d = np.diff(t, axis=1) / 100.0  # 100 MHz -> us
+    res = {'config': args.config, 'N': b.N, 'total_us_median': float(np.median((t[:, 9] - t[:, 0]) / 100.0)),
+           'span_us': float((t[:, 9].max() - t[:, 0].min()) / 100.0),
+           'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())},
+           'phases_us': {p: {'median': float(np.median(d[:, i])), 'max': float(d[:, i].max())}
+                         for i, p in enumerate(PHASES)}}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == '__main__':
+    main()
