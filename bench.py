@@ -55,7 +55,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--config', default='lifting_4-small_divider')
     ap.add_argument('--envs', type=int, default=64, help='envs per GPU (BASELINE configs[1]: 64)')
-    ap.add_argument('--layout', default='hwc', choices=['hwc', 'chw'])
+    ap.add_argument('--layout', default='chw', choices=['hwc', 'chw'])
     ap.add_argument('--cpu-budget', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()

@@ -21,7 +21,7 @@ constexpr double PPM = 96.0;     // Mapper.LOCAL_MAP_PIXELS_PER_METER
 constexpr double RAD_TO_DEG = 180.0 / 3.141592653589793;  // CPython math.degrees: x * (180 / pi)
 
 // Per-class robot geometry (envs.py:802-810, 1059-1062, 1279-1282), computed on the host with
-// the reference's own expressions (see simaps_host.cpp: make_geometry).
+// the reference's own expressions (see make_geometry in simaps.hip).
 struct Geometry {
     double base_length[4];
     int cspace_r[4];    // floor(RADIUS * 96)                  (envs.py:2421)
@@ -31,6 +31,10 @@ struct Geometry {
     int pad;
     double half_width, half_width_sq, backpack_offset;
     double cube_half, cube_width, cube_base;  // CUBE_WIDTH/2, CUBE_WIDTH, EE + LIFTED_CUBE_OFFSET
+    // The 5 robot masks (types 0..3, 4 = lifting with lifted cube) as bit windows, filled on the
+    // host from mask_bit(): mbits[m][r] bit c = mask[mrow0[m] + r][mcol0[m] + c].
+    int mrow0[5], mcol0[5], mnrows[5], mncols[5];
+    uint32_t mbits[5][24];
 };
 
 // ---- scipy.special.cosdg / sindg (cephes sindg.c) -----------------------------------------

@@ -40,14 +40,24 @@ constexpr int NT = 1024;
 // Diagnostic build only (libsimaps_prof.so): per-workgroup s_memrealtime (100 MHz) stamps.
 constexpr int MAX_STAMP_WG = 8192, NSTAMP = 16;
 __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
+// (a barrier first, so a stamp marks the moment the SLOWEST wave finished the previous phase)
 #define STAMP(k)                                                                                 \
     do {                                                                                         \
+        lds_barrier();                                                                         \
         if (threadIdx.x == 0 && blockIdx.x < MAX_STAMP_WG)                                       \
+            g_stamps[blockIdx.x * NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime();              \
+    } while (0)
+#define STAMP_NB(k)                                                                              \
+    do {                                                                                         \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < MAX_STAMP_WG)                                \
             g_stamps[blockIdx.x * NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime();              \
     } while (0)
 #else
 #define STAMP(k) \
     do {         \
+    } while (0)
+#define STAMP_NB(k) \
+    do {            \
     } while (0)
 #endif
 constexpr int MAX_SEG = 128;     // intention / history segments per agent
@@ -98,6 +108,16 @@ __device__ __forceinline__ void b_atomic_or(B128 *dst, B128 v)
     if ((unsigned)(v.hi >> 32)) atomicOr(w + 3, (unsigned)(v.hi >> 32));
 }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() also waits vmcnt(0), i.e. for every
+// outstanding global STORE of the wave -- no barrier in this file protects global memory, and that
+// wait would expose the output write latency at every phase boundary.
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ------------------------------------------------------------------------------------------------
 // LDS layout
 // ------------------------------------------------------------------------------------------------
@@ -109,6 +129,7 @@ struct RobotP {
     int tpi, tpj;            // target end-effector pixel
     int bi0, bi1, bj0, bj1;  // global-pixel box outside which the rotated mask is surely 0
     float seg_val, pad;
+    uint32_t sbits[2][32];   // rotated stamp inside the box: [0] class mask, [1] lifted-cube mask
 };
 
 struct Seg {
@@ -136,6 +157,9 @@ struct Shared {
     RobotP rob[SIMAPS_MAX_ROBOTS];
     int colbest[2][SIMAPS_MAX_ROOM_W];
     int envg[2][SIMAPS_MAX_ROOM_W];  // Voronoi envelope (rect columns) per source
+    unsigned bar[2][4];              // group barriers {count, generation, timeout, -}: [0] sweeps, [1] render
+    int changed[3];                  // rotating per-round "some sweep improved a cell" flags
+    float dummy[8][64];              // sweep store sink for non-improving lanes (1 slot per lane)
     Seg seg[MAX_SEG];
 };
 
@@ -144,7 +168,6 @@ struct SsspScratch {
     uint64_t win[MAX_WIN_ROWS][WIN_WORDS];
     B128 blocked[MAX_ROWS];
     B128 freeb[MAX_ROWS];
-    int changed[3];  // rotating per-round "some sweep improved a cell" flags
 };
 
 constexpr int align16(int x) { return (x + 15) & ~15; }
@@ -180,21 +203,51 @@ __device__ void build_cspace(SsspScratch &S, const uint8_t *__restrict__ occ, in
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wh = h + 2 * r, ww = w + 2 * r;
     const int nwords = (ww + 63) >> 6;
-    // (a) window rows -> bits: one wave-ballot per 64 columns
+    // (a) every window byte loaded by one thread, all loads in flight together (<= 14 per thread),
+    //     staged as bytes in LDS (the raster-tile region, free until the render), then
+    // (b) window rows -> bit rows: one wave ballot per 64 columns, from LDS.
+    uint8_t *stage = reinterpret_cast<uint8_t *>(S.blocked) + sizeof(S.blocked) + sizeof(S.freeb) + 64;
+    {   // thread -> (row = tid / 128 + 8q, col = tid % 128 [+ 128]): ww <= 132, wh <= 124
+        constexpr int MAXLD = 16;
+        uint8_t v[MAXLD], v2[2];
+        const int c = tid & 127, r0 = tid >> 7;
+#pragma unroll
+        for (int q = 0; q < MAXLD; q++) {
+            const int rr = r0 + 8 * q, gi = i0 - r + rr, gj = j0 - r + c;
+            v[q] = (rr < wh && c < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
+        }
+        // columns 128..131 of the widest window
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int k = tid + q * NT, rr = k >> 2, cc = 128 + (k & 3), gi = i0 - r + rr, gj = j0 - r + cc;
+            v2[q] = (rr < wh && cc < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < MAXLD; q++) {
+            const int rr = r0 + 8 * q;
+            if (rr < wh && c < ww) stage[rr * ww + c] = v[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int k = tid + q * NT, rr = k >> 2, cc = 128 + (k & 3);
+            if (rr < wh && cc < ww) stage[rr * ww + cc] = v2[q];
+        }
+    }
+    lds_barrier();
     for (int item = wave; item < wh * WIN_WORDS; item += NT / 64) {
         const int wr = item / WIN_WORDS, wd = item % WIN_WORDS;
-        const int gi = i0 - r + wr, x = wd * 64 + lane, gj = j0 - r + x;
-        bool ob = false;
-        if (wd < nwords && x < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ob = occ[(size_t)gi * W + gj] != 0;
+        const int x = wd * 64 + lane;
+        const bool ob = wd < nwords && x < ww && stage[wr * ww + x] != 0;
         const uint64_t m = __ballot(ob);
         if (lane == 0) S.win[wr][wd] = m;
     }
     for (int rr = tid; rr < h; rr += NT) S.blocked[rr] = {0, 0};
-    __syncthreads();
+    lds_barrier();
     // (b) blocked[row] = OR over disk offsets (dy, |dx| <= hw(dy)) of the window bits
     const int span = 2 * r + 1;
-    for (int item = tid; item < h * span; item += NT) {
-        const int row = item / span, dy = item % span - r;
+    for (int item = tid; item < h * 16; item += NT) {  // 16 slots per row >= span (r <= 7)
+        const int row = item >> 4, dy = (item & 15) - r;
+        if (dy > r) continue;
         int hw = 0;
         while ((hw + 1) * (hw + 1) + dy * dy <= r * r) hw++;
         const uint64_t *wrow = S.win[row + r + dy];
@@ -202,13 +255,13 @@ __device__ void build_cspace(SsspScratch &S, const uint8_t *__restrict__ occ, in
         for (int k = -hw; k <= hw; k++) acc = b_or(acc, win_get(wrow, r + k));
         b_atomic_or(&S.blocked[row], acc);
     }
-    __syncthreads();
+    lds_barrier();
     const B128 m = b_mask(w);
     for (int rr = tid; rr < h; rr += NT) {
         const B128 b = S.blocked[rr];
         S.freeb[rr] = {~b.lo & m.lo, ~b.hi & m.hi};
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -219,8 +272,9 @@ __device__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc)
     const int tid = threadIdx.x;
     const int h = sh.h, w = sh.w, i0 = sh.i0, j0 = sh.j0;
     // pass 1 (scipy: per column along axis 0): nearest free row of each rect column, ties low
-    for (int item = tid; item < nsrc * w; item += NT) {
-        const int s = item / w, c = item % w;
+    for (int item = tid; item < nsrc * 128; item += NT) {  // w <= 120 columns per source
+        const int s = item >> 7, c = item & 127;
+        if (c >= w) continue;
         const int qi = sh.src_q[s][0];
         int best = -1, bestd = 1 << 30;
         for (int rr = 0; rr < h; rr++) {
@@ -231,7 +285,7 @@ __device__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc)
         }
         sh.colbest[s][c] = best;
     }
-    __syncthreads();
+    lds_barrier();
     // pass 2 (scipy _VoronoiFT along axis 1), one lane per source
     if ((tid & 63) == 0 && (tid >> 6) < nsrc) {
         const int s = tid >> 6;
@@ -286,8 +340,45 @@ __device__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc)
             }
         }
     }
-    __syncthreads();
+    lds_barrier();
 }
+
+// ------------------------------------------------------------------------------------------------
+// Wave groups: the workgroup splits into SSSP-sweep waves and render waves that run concurrently.
+// A group of fewer than 16 waves synchronises through an LDS barrier (lane 0 of each wave arrives
+// on a counter; the last one bumps a generation word the others poll with s_sleep; bounded spin).
+// ------------------------------------------------------------------------------------------------
+struct Group {
+    int t, n;           // thread index within the group, threads in the group
+    unsigned *bar;      // nullptr: the whole workgroup (__syncthreads)
+    int nw;             // waves in the group
+    __device__ void sync() const
+    {
+        if (!bar) {
+            lds_barrier();
+            return;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if ((threadIdx.x & 63) == 0) {
+            const unsigned g = __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const unsigned arrived = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (arrived == (unsigned)nw - 1) {
+                __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(&bar[1], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                unsigned spins = 0;
+                while (__hip_atomic_load(&bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == g) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 22)) {  // ~0.1 s: never in a correct run; flag and fall through
+                        __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        break;
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    }
+};
 
 // ------------------------------------------------------------------------------------------------
 // Phase: single-source shortest paths for nsrc sources over the free cells of the rect
@@ -353,8 +444,8 @@ __device__ bool sweep(float *D, float *dummy, int h, int w, int pw, int dir_in)
         // exactly 2 stores + 2 loads per step (non-improving lanes store into a private dummy slot),
         // so the compiler's LDS counter waits stay partial and the loads overlap the next step.
         // The final two prefetches read past the line range: still inside this kernel's LDS block.
-        *(u0 ? &D[ad0] : &dummy[2 * lane]) = c0;
-        *(u1 ? &D[ad1] : &dummy[2 * lane + 1]) = c1;
+        *(u0 ? &D[ad0] : &dummy[lane]) = c0;  // both sinks share the lane's slot (never read)
+        *(u1 ? &D[ad1] : &dummy[lane]) = c1;
         changed |= u0 | u1;
         p0 = c0;
         p1 = c1;
@@ -371,42 +462,57 @@ __device__ bool sweep(float *D, float *dummy, int h, int w, int pw, int dir_in)
     return __ballot(changed) != 0;
 }
 
-__device__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
+// all threads: free cells +inf, blocked / padding NaN, sources 0
+__device__ void sssp_init(Shared &sh, const SsspScratch &S, float *dist, int nsrc)
 {
-    const int tid = threadIdx.x, wave = tid >> 6;
+    const int tid = threadIdx.x;
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
     const int cells = (h + 2) * pw;
     const float QN = __int_as_float(QNAN_BITS);
-    // free cells +inf, blocked / padding NaN
-    for (int k = tid; k < nsrc * DIST_FLOATS; k += NT) {
-        const int q = k % DIST_FLOATS, r = q / pw - 1, c = q % pw - 1;
-        const bool fr = q < cells && r >= 0 && r < h && c >= 0 && c < w && b_test(S.freeb[r], c);
-        dist[k] = fr ? INFINITY : QN;
+    // (row, column) walk instead of k / pitch: integer division by a runtime value costs ~40 ops
+    for (int s = 0; s < nsrc; s++) {
+        float *D = dist + s * DIST_FLOATS;
+        for (int rr = tid >> 7; rr < h + 2; rr += NT >> 7) {
+            const B128 fb = (rr >= 1 && rr <= h) ? S.freeb[rr - 1] : B128{0, 0};
+            for (int c = tid & 127; c < pw; c += 128) {
+                const bool fr = c >= 1 && c <= w && b_test(fb, c - 1);
+                D[rr * pw + c] = fr ? INFINITY : QN;
+            }
+        }
+        for (int k = cells + tid; k < DIST_FLOATS; k += NT) D[k] = QN;
     }
-    if (tid < 3) S.changed[tid] = 0;
-    __syncthreads();
+    if (tid < 3) sh.changed[tid] = 0;
+    if (tid < 8) (&sh.bar[0][0])[tid] = 0u;
+    lds_barrier();
     for (int s = tid; s < nsrc; s += NT)
         if (sh.src_ok[s]) dist[s * DIST_FLOATS + (sh.src_s[s][0] - sh.i0 + 1) * pw + (sh.src_s[s][1] - sh.j0 + 1)] = 0.0f;
-    __syncthreads();
-    // a converged round changes nothing; the cap only guards against a bug hanging the GPU
-    const int max_rounds = h * w + 16;
-    sh.rounds = 0;
+    lds_barrier();
+}
+
+// the sweep group (waves 0 .. 4*nsrc-1): rounds of concurrent sweeps until one changes nothing
+__device__ void sssp_rounds(Shared &sh, float *dist, int nsrc, const Group &g)
+{
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
+    const int max_rounds = h * w + 16;  // a converged round changes nothing; the cap guards a bug
     for (int round = 0;; round++) {
-        if (tid == 0) S.changed[(round + 1) % 3] = 0;
-        if (wave < 4 * nsrc) {
-            const int s = wave >> 2;
-            float *dummy = reinterpret_cast<float *>(&S.win[0][0]) + 128 * wave;  // dead after build_cspace
-            if (sh.src_ok[s] && sweep(dist + s * DIST_FLOATS, dummy, h, w, pw, wave & 3) && (tid & 63) == 0)
-                S.changed[round % 3] = 1;
-        }
-        __syncthreads();
-        if (!S.changed[round % 3] || round >= max_rounds) {
+        if (tid == 0) sh.changed[(round + 1) % 3] = 0;
+        const int s = wave >> 2;
+        if (sh.src_ok[s] && sweep(dist + s * DIST_FLOATS, sh.dummy[wave], h, w, pw, wave & 3) && (tid & 63) == 0)
+            sh.changed[round % 3] = 1;
+        g.sync();
+        if (!sh.changed[round % 3] || round >= max_rounds) {
             if (tid == 0) sh.rounds = round >= max_rounds ? -1 : round + 1;
             break;
         }
     }
-    __syncthreads();
-    // NaN (blocked) -> +inf; max reachable distance per source
+}
+
+// all threads: NaN (blocked) -> +inf; max reachable distance per source
+__device__ void sssp_finish(Shared &sh, float *dist, int nsrc)
+{
+    const int tid = threadIdx.x;
+    const int cells = (sh.h + 2) * sssp_pitch(sh.w);
     for (int s = 0; s < nsrc; s++) {
         float m = -1.0f;
         for (int q = tid; q < cells; q += NT) {
@@ -416,14 +522,23 @@ __device__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
         }
         m = wave_max(m);
         if ((tid & 63) == 0) sh.red[0][tid >> 6] = m;
-        __syncthreads();
+        lds_barrier();
         if (tid == 0) {
             float mm = sh.red[0][0];
             for (int k = 1; k < NT / 64; k++) mm = fmaxf(mm, sh.red[0][k]);
             sh.dmax[s] = mm;
         }
-        __syncthreads();
+        lds_barrier();
     }
+}
+
+__device__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
+{
+    sssp_init(sh, S, dist, nsrc);
+    const int wave = threadIdx.x >> 6;
+    if (wave < 4 * nsrc) sssp_rounds(sh, dist, nsrc, Group{(int)threadIdx.x, 256 * nsrc, sh.bar[0], 4 * nsrc});
+    lds_barrier();
+    sssp_finish(sh, dist, nsrc);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -431,11 +546,11 @@ __device__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
 // ------------------------------------------------------------------------------------------------
 // enc: SIMAPS_ENC_* or 4 = history (ramp over the reversed history path)
 __device__ void raster_lines(Shared &sh, float *tile, const simaps_config &cfg, const simaps_robot *rb,
-                             const double *__restrict__ paths, int enc)
+                             const double *__restrict__ paths, int enc, const Group &g)
 {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = g.t, lane = threadIdx.x & 63, wave = g.t >> 6, nwaves = g.n >> 6;
     unsigned *tu = reinterpret_cast<unsigned *>(tile);
-    for (int k = tid; k < TILE * TILE; k += NT) tu[k] = 0u;
+    for (int k = tid; k < TILE * TILE; k += g.n) tu[k] = 0u;
     const double scale = cfg.intention_map_scale;
     const float scale_f = (float)scale;
     // per-robot segment tables (one lane per robot; path_length accumulates sequentially)
@@ -473,7 +588,7 @@ __device__ void raster_lines(Shared &sh, float *tile, const simaps_config &cfg, 
         }
         sh.seg_robot_cnt[k] = cnt;
     }
-    __syncthreads();
+    g.sync();
     const int ti0 = sh.pi - TILE_HALF, tj0 = sh.pj - TILE_HALF;
     if (enc == SIMAPS_ENC_CIRCLE) {
         if (tid < sh.nr && tid != sh.me && !sh.rob[tid].idle) {
@@ -483,7 +598,7 @@ __device__ void raster_lines(Shared &sh, float *tile, const simaps_config &cfg, 
     } else {
         // one wave per segment, lanes stride over its pixels
         const int total = sh.nr * SEG_PER_ROBOT;
-        for (int q = wave; q < total; q += NT / 64) {
+        for (int q = wave; q < total; q += nwaves) {
             const int k = q / SEG_PER_ROBOT, j = q % SEG_PER_ROBOT;
             if (j >= sh.seg_robot_cnt[k]) continue;
             const Seg &G = sh.seg[q];
@@ -515,7 +630,7 @@ __device__ void raster_lines(Shared &sh, float *tile, const simaps_config &cfg, 
             }
         }
     }
-    __syncthreads();
+    g.sync();
 }
 
 __device__ __forceinline__ float tile_sample(const float *tile, int thick, int gi, int gj, int pi, int pj)
@@ -534,8 +649,245 @@ __device__ __forceinline__ float tile_sample(const float *tile, int thick, int g
 // ------------------------------------------------------------------------------------------------
 // The fused per-agent kernel
 // ------------------------------------------------------------------------------------------------
+
+struct RenderCtx {
+    const simaps_config &cfg;
+    Shared &sh;
+    float *out;
+    int C, n;
+    __device__ __forceinline__ void put(int ch, int p, float v) const
+    {
+        if (cfg.layout_chw) out[(size_t)ch * LW * LW + p] = v;
+        else out[(size_t)p * C + ch] = v;
+    }
+    // global pixel sampled by output pixel p (Mapper._get_local_map, envs.py:2200-2211), packed
+    // gi << 16 | gj, or -1 where the scipy rotate falls outside the crop (cval 0)
+    __device__ __forceinline__ int gpix(int p) const
+    {
+        const Rot &R = sh.rot;
+        const int a = p / LW, b = p % LW;
+        int k0, k1;
+        if (!rot_src(R, CROP, a + R.S0 / 2 - LW / 2, b + R.S1 / 2 - LW / 2, k0, k1)) return -1;
+        const int gi = sh.pi - HALF_CROP + k0, gj = sh.pj - HALF_CROP + k1;
+        return (gi >= 0 && gi < cfg.H && gj >= 0 && gj < cfg.W) ? (gi << 16) | gj : -1;
+    }
+};
+
+// Channels that do not need the shortest-path maps, rendered by group g:
+// overhead (0), robot (1), history / intention maps, baseline intention channels.
+__device__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry &geo, const float *__restrict__ ovh,
+                            const simaps_robot *rb, const double *__restrict__ paths, float *tile)
+{
+    const simaps_config &cfg = rc.cfg;
+    Shared &sh = rc.sh;
+    const int nr = sh.nr, W = cfg.W;
+    constexpr int NP = LW * LW;
+    // overhead / robot channels.  The robots' rotated stamps (per-robot bit tiles, built once per
+    // workgroup) are first OR-ed into a 136 x 136 map over the agent's crop, in the raster-tile
+    // region: bit (g + 5) = seg value (g + 5) / 8 (SEG_VALUES robot_group_{g+1}), bit 16 = 0.5,
+    // bit 17 = 1.0 (non-seg values).  A pixel is then one LDS read; the highest bit of each field is
+    // the np.maximum over robots of _create_global_robot_map (envs.py:2251-2276).
+    unsigned *rmap = reinterpret_cast<unsigned *>(tile);
+    const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
+    {
+        uint4 *z = reinterpret_cast<uint4 *>(rmap);
+        for (int k = g.t; k < CROP * CROP / 4; k += g.n) z[k] = uint4{0u, 0u, 0u, 0u};
+    }
+    g.sync();
+    for (int item = g.t; item < nr * 1024; item += g.n) {
+        const int q = item >> 10, bi = (item >> 5) & 31, bj = item & 31;
+        const RobotP &P = sh.rob[q];
+        if (bi > P.bi1 - P.bi0 || bj > P.bj1 - P.bj0) continue;
+        const int a = P.bi0 + bi - ci0, b = P.bj0 + bj - cj0;
+        if (a < 0 || a >= CROP || b < 0 || b >= CROP) continue;
+        unsigned bits = 0;
+        if ((P.sbits[0][bi] >> bj) & 1u) {
+            bits |= 1u << (P.group + 5);
+            if (P.type != SIMAPS_LIFTING) bits |= 1u << 17;
+            else if (!P.lifting) bits |= 1u << 16;
+        }
+        if ((P.sbits[1][bi] >> bj) & 1u) bits |= 1u << 17;  // lifted-cube mask, value 1.0
+        if (bits) atomicOr(&rmap[a * CROP + b], bits);
+    }
+    g.sync();
+    for (int base = g.t; base < NP; base += 9 * g.n) {
+        int gp[9];
+        float ovv[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            const int p = base + k * g.n;
+            gp[k] = p < NP ? rc.gpix(p) : -1;
+#ifdef SIMAPS_ABL_NOGATHER
+            ovv[k] = 0.25f;
+            asm volatile("" ::"v"(gp[k]));
+#else
+            ovv[k] = gp[k] >= 0 ? ovh[(size_t)(gp[k] >> 16) * W + (gp[k] & 0xffff)] : 0.0f;
+#endif
+        }
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            const int p = base + k * g.n;
+            if (p >= NP) break;
+            float vseg = 0.0f, vrob = 0.0f, vov = 0.0f;
+            if (gp[k] >= 0) {
+                const unsigned m = rmap[((gp[k] >> 16) - ci0) * CROP + (gp[k] & 0xffff) - cj0];
+                const unsigned ms = m & 0x1ffu, mr = m >> 16;
+                vseg = ms ? (float)(31 - __builtin_clz(ms)) * 0.125f : 0.0f;
+                vrob = (mr & 2u) ? 1.0f : ((mr & 1u) ? 0.5f : 0.0f);
+                vov = vseg > 0.0f ? vseg : ovv[k];
+            }
+#ifdef SIMAPS_ABL_NOSTORE
+            asm volatile("" ::"v"(vov), "v"(vrob));
+#else
+            rc.put(0, p, vov);
+            if (cfg.use_robot_map) rc.put(1, p, vrob);
+#endif
+        }
+    }
+    g.sync();  // the raster below reuses the robot-map region
+    if (g.t == 0) STAMP_NB(11);
+    // channel index after overhead / robot / distance channels (envs.py:2071-2113 order)
+    int ch = 1 + !!cfg.use_robot_map + !!cfg.use_distance_to_receptacle_map + !!cfg.use_shortest_path_to_receptacle_map +
+             !!cfg.use_shortest_path_map;
+    // history / intention maps, rasterised into the LDS tile
+    const int thick = cfg.intention_map_line_thickness;
+    for (int pass = 0; pass < 2; pass++) {
+        const bool on = pass == 0 ? cfg.use_history_map : cfg.use_intention_map;
+        if (!on) continue;
+        raster_lines(sh, tile, cfg, rb, paths, pass == 0 ? 4 : cfg.intention_map_encoding, g);
+        if (g.t == 0) STAMP_NB(12);
+        for (int p = g.t; p < NP; p += g.n) {
+            const int gq = rc.gpix(p);
+            rc.put(ch, p, gq >= 0 ? tile_sample(tile, thick, gq >> 16, gq & 0xffff, sh.pi, sh.pj) : 0.0f);
+        }
+        ch++;
+        g.sync();
+    }
+    // baseline intention channels (Mapper._get_intention_channels, envs.py:2349-2378)
+    if (cfg.use_intention_channels) {
+        if (g.t == 0) {
+            // np.argsort of distances (insertion sort for n <= 16 -> stable)
+            double dd[SIMAPS_MAX_ROBOTS];
+            const RobotP &M = sh.rob[sh.me];
+            for (int q = 0; q < nr; q++) {
+                const double dx = sh.rob[q].x - M.x, dy = sh.rob[q].y - M.y;
+                dd[q] = sqrt(dx * dx + dy * dy);
+                int j = q;
+                while (j > 0 && dd[sh.order[j - 1]] > dd[q]) { sh.order[j] = sh.order[j - 1]; j--; }
+                sh.order[j] = q;
+            }
+            if (!cfg.intention_channel_spatial) {
+                int c2 = 0;
+                for (int q = 0; q < nr; q++) {
+                    const int k = sh.order[q];
+                    if (k == sh.me) continue;
+                    const RobotP &R = sh.rob[k];
+                    double rel0 = 0.0, rel1 = 0.0;
+                    if (!R.idle) {
+                        const double dx = R.tx - M.x, dy = R.ty - M.y;
+                        const double dist_t = sqrt(dx * dx + dy * dy);
+                        const double th = rb[sh.me].heading - atan2(R.ty - M.y, R.tx - M.x);
+                        rel0 = dist_t * sin(th);
+                        rel1 = dist_t * cos(th);
+                    }
+                    sh.nonsp[c2++] = (float)(cfg.intention_channel_nonspatial_scale * rel0);
+                    sh.nonsp[c2++] = (float)(cfg.intention_channel_nonspatial_scale * rel1);
+                }
+            }
+        }
+        g.sync();
+        int c2 = 0;
+        const float scale_f = (float)cfg.intention_map_scale;
+        for (int q = 0; q < nr; q++) {
+            const int kq = sh.order[q];
+            if (kq == sh.me) continue;
+            if (cfg.intention_channel_spatial) {
+                const RobotP &R = sh.rob[kq];
+                for (int p = g.t; p < NP; p += g.n) {
+                    const int gq = rc.gpix(p);
+                    float v = 0.0f;
+                    if (gq >= 0 && !R.idle) {
+                        const int di = abs((gq >> 16) - R.tpi), dj = abs((gq & 0xffff) - R.tpj);
+                        const bool hit = thick > 1 ? (di + dj <= 1) : (di == 0 && dj == 0);
+                        v = hit ? scale_f : 0.0f;
+                    }
+                    rc.put(ch, p, v);
+                }
+                ch++;
+            } else {
+                for (int e = 0; e < 2; e++, ch++, c2++)
+                    for (int p = g.t; p < NP; p += g.n) rc.put(ch, p, sh.nonsp[c2]);
+            }
+        }
+    }
+}
+
 constexpr int PPT = (LW * LW) / NT;  // 9 output pixels per thread
 static_assert(PPT * NT == LW * LW, "pixel split");
+
+// Distance channels (all 16 waves): Euclidean map, then shortest-path maps; local -= local.min()
+// (envs.py:2213-2216), so every value is kept in registers until the block minimum is known.
+__device__ void render_distance_channels(const RenderCtx &rc, const simaps_env &ev, const float *dist, int nsrc)
+{
+    const simaps_config &cfg = rc.cfg;
+    Shared &sh = rc.sh;
+    const int tid = threadIdx.x, H = cfg.H, W = cfg.W;
+    const int has_eu = cfg.use_distance_to_receptacle_map ? 1 : 0;
+    const int nd = has_eu + nsrc;
+    if (nd == 0) return;
+    const int ch = 1 + !!cfg.use_robot_map;
+    int gpix[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) gpix[k] = rc.gpix(tid + k * NT);
+    float vals[3][PPT];
+    float mins[3];
+    const float sps = (float)cfg.shortest_path_map_scale;
+    const float eus = (float)cfg.distance_to_receptacle_map_scale;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        mins[q] = INFINITY;
+        if (q >= nd) continue;
+        const bool eu = q < has_eu;  // Euclidean map first (envs.py:2083-2084)
+        const int s = q - has_eu;
+        const float *D = dist + (eu ? 0 : s) * DIST_FLOATS;
+        const float unreach = eu ? 0.0f : (sh.dmax[eu ? 0 : s] / 96.0f) * sps;
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            float v = 0.0f;
+            if (gpix[k] >= 0) {
+                const int gi = gpix[k] >> 16, gj = gpix[k] & 0xffff;
+                if (eu) {  // envs.py:2278-2286
+                    const double px = ((gj + 0.5) - (double)W / 2) / PPM, py = ((double)H / 2 - (gi + 0.5)) / PPM;
+                    const double dx = ev.receptacle_x - px, dy = ev.receptacle_y - py;
+                    v = (float)sqrt(dx * dx + dy * dy) * eus;
+                } else {  // envs.py:2288-2300, 2514-2517
+                    const int r = gi - sh.i0, c = gj - sh.j0;
+                    float dd = __int_as_float(INF_BITS);
+                    if (r >= 0 && r < sh.h && c >= 0 && c < sh.w) dd = D[(r + 1) * sssp_pitch(sh.w) + c + 1];
+                    v = dd != __int_as_float(INF_BITS) ? (dd / 96.0f) * sps : unreach;
+                }
+            }
+            vals[q][k] = v;
+            mins[q] = fminf(mins[q], v);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        if (q >= nd) continue;
+        const float m = wave_min(mins[q]);
+        if ((tid & 63) == 0) sh.red[q & 1][tid >> 6] = m;
+        lds_barrier();
+        float mm = sh.red[q & 1][0];
+        for (int k = 1; k < NT / 64; k++) mm = fminf(mm, sh.red[q & 1][k]);
+        mins[q] = mm;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        if (q >= nd) continue;
+#pragma unroll
+        for (int k = 0; k < PPT; k++) rc.put(ch + q, tid + k * NT, vals[q][k] - mins[q]);
+    }
+}
 
 __global__ void __launch_bounds__(NT) get_state_kernel(
     simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents, const simaps_env *__restrict__ envs,
@@ -611,12 +963,43 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             P.bi1 = min(P.st_i + R.S0 - 1, P.st_i + (int)ceil(mx0) + 2);
             P.bj0 = max(P.st_j, P.st_j + (int)floor(mn1) - 2);
             P.bj1 = min(P.st_j + R.S1 - 1, P.st_j + (int)ceil(mx1) + 2);
+            P.bi1 = min(P.bi1, P.bi0 + 31);  // the window is <= 17 x 13 px: its rotated box fits 32 x 32
+            P.bj1 = min(P.bj1, P.bj0 + 31);
+            for (int q = 0; q < 32; q++) P.sbits[0][q] = P.sbits[1][q] = 0u;
         }
         P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
     }
-    __syncthreads();
+    lds_barrier();
 
-    // ---- cspace + snap + SSSP
+    // ---- rotated robot stamps (Mapper._create_global_robot_map, envs.py:2251-2276): each robot's
+    // scipy-rotated mask, evaluated once per workgroup into a <= 32 x 32 bit tile at its global box.
+    // The 5 host-computed mask windows are staged in the (still unused) union region first.
+    uint32_t *mwin = reinterpret_cast<uint32_t *>(smem + OFF_UNION);  // [5][24] bits + [5][4] ints
+    if (tid < 5 * 24) mwin[tid] = geo.mbits[tid / 24][tid % 24];
+    if (tid >= 128 && tid < 128 + 20) {
+        const int q = tid - 128, m = q >> 2, f = q & 3;
+        mwin[120 + q] = f == 0 ? geo.mrow0[m] : f == 1 ? geo.mcol0[m] : f == 2 ? geo.mnrows[m] : geo.mncols[m];
+    }
+    lds_barrier();
+    for (int item = tid; item < ev.num_robots * 1024; item += NT) {
+        const int k = item >> 10, cell = item & 1023, bi = cell >> 5, bj = cell & 31;
+        RobotP &P = sh.rob[k];
+        const int gi = P.bi0 + bi, gj = P.bj0 + bj;
+        if (gi > P.bi1 || gj > P.bj1) continue;
+        const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
+        int m0, m1;
+        if (!rot_src(R, LW, gi - P.st_i, gj - P.st_j, m0, m1)) continue;
+        auto bit = [&](int m) {
+            const int *mi = reinterpret_cast<const int *>(mwin + 120 + 4 * m);
+            const int r = m0 - mi[0], c = m1 - mi[1];
+            return r >= 0 && r < mi[2] && c >= 0 && c < mi[3] && ((mwin[m * 24 + r] >> c) & 1u);
+        };
+        if (bit(P.type)) atomicOr(&P.sbits[0][bi], 1u << bj);
+        if (P.type == SIMAPS_LIFTING && P.lifting && bit(4)) atomicOr(&P.sbits[1][bi], 1u << bj);
+    }
+    lds_barrier();
+
+    // ---- cspace + snap (all waves)
     STAMP(1);
     const int nsrc = sh.nsrc;
     if (nsrc > 0 || dbg.cspace) {
@@ -629,9 +1012,36 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     STAMP(2);
     if (nsrc > 0) {
         snap_sources(sh, S, nsrc);
-        STAMP(3);
-        sssp(sh, S, dist, nsrc);
-        STAMP(4);
+        sssp_init(sh, S, dist, nsrc);
+    }
+    STAMP(3);
+
+    // ---- split: waves [0, 4*nsrc) sweep the distance arrays while the other waves render every
+    // channel that does not need them (overhead, robot, history / intention, intention channels).
+    // The raster tile reuses the cspace scratch, which the sweeps no longer read.
+    float *out = state + (size_t)n * LW * LW * C;
+    const RenderCtx rc{cfg, sh, out, C, n};
+    const int sweep_waves = 4 * nsrc;
+    if ((tid >> 6) < sweep_waves) {
+        sssp_rounds(sh, dist, nsrc, Group{tid, 64 * sweep_waves, sh.bar[0], sweep_waves});
+        STAMP_NB(7);
+    } else {
+        const int nw = NT / 64 - sweep_waves;
+        const Group g{tid - 64 * sweep_waves, 64 * nw, sweep_waves ? sh.bar[1] : nullptr, nw};
+        render_maps(rc, g, geo, overhead + (size_t)n * H * W, rb, paths, tile);
+        if (g.t == 0) STAMP_NB(8);
+    }
+    lds_barrier();
+    STAMP(4);
+
+    // ---- all waves: distance channels (need the converged sweeps)
+    if (nsrc > 0) sssp_finish(sh, dist, nsrc);
+    STAMP(5);
+    render_distance_channels(rc, ev, dist, nsrc);
+    STAMP(6);
+
+    // ---- debug outputs
+    if (nsrc > 0) {
         if (dbg.sources && tid < 2) {
             int32_t *o = dbg.sources + ((size_t)n * 2 + tid) * 4;
             const int s = sh.sp_slot[tid];
@@ -655,201 +1065,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         int st = 0;
         for (int s = 0; s < nsrc; s++) st |= sh.src_ok[s] ? 0 : 1;
         if (nsrc > 0 && sh.rounds < 0) st |= 2;
+        if (sh.bar[0][2] | sh.bar[1][2]) st |= 4;
         dbg.status[n] = st | ((nsrc > 0 ? sh.rounds : 0) << 8);
     }
-
-    // ---- render: each thread owns output pixels p = tid + k * NT
-    STAMP(5);
-    int gpix[PPT];  // packed (gi << 16 | gj), -1 = rotate fell outside the crop (cval 0)
-    {
-        const Rot R = sh.rot;
-        const int b0 = R.S0 / 2 - LW / 2, b1 = R.S1 / 2 - LW / 2;
-#pragma unroll
-        for (int k = 0; k < PPT; k++) {
-            const int p = tid + k * NT, a = p / LW, b = p % LW;
-            int k0, k1;
-            if (rot_src(R, CROP, a + b0, b + b1, k0, k1)) {
-                const int gi = sh.pi - HALF_CROP + k0, gj = sh.pj - HALF_CROP + k1;
-                gpix[k] = (gi >= 0 && gi < H && gj >= 0 && gj < W) ? (gi << 16) | gj : -1;
-            } else {
-                gpix[k] = -1;
-            }
-        }
-    }
-    float *out = state + (size_t)n * LW * LW * C;
-    auto put = [&](int ch, int p, float v) {
-        if (cfg.layout_chw) out[(size_t)ch * LW * LW + p] = v;
-        else out[(size_t)p * C + ch] = v;
-    };
-    const int nr = sh.nr;
-    int ch = 0;
-
-    // channels 0 (overhead) and 1 (robot map): robot stamps evaluated per global pixel
-    {
-        const float *ovh = overhead + (size_t)n * H * W;
-        float ovv[PPT];
-#pragma unroll
-        for (int k = 0; k < PPT; k++)  // issue every HBM gather before any use
-            ovv[k] = gpix[k] >= 0 ? ovh[(size_t)(gpix[k] >> 16) * W + (gpix[k] & 0xffff)] : 0.0f;
-#pragma unroll 1
-        for (int k = 0; k < PPT; k++) {
-            const int p = tid + k * NT;
-            float vseg = 0.0f, vrob = 0.0f, vov = 0.0f;
-            if (gpix[k] >= 0) {
-                const int gi = gpix[k] >> 16, gj = gpix[k] & 0xffff;
-                for (int q = 0; q < nr; q++) {
-                    const RobotP &P = sh.rob[q];
-                    if (gi < P.bi0 || gi > P.bi1 || gj < P.bj0 || gj > P.bj1) continue;
-                    const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
-                    int m0, m1;
-                    if (!rot_src(R, LW, gi - P.st_i, gj - P.st_j, m0, m1)) continue;
-                    if (mask_bit(geo, P.type, false, m0, m1)) {
-                        vseg = fmaxf(vseg, P.seg_val);
-                        if (P.type != SIMAPS_LIFTING || !P.lifting) vrob = fmaxf(vrob, (P.type == SIMAPS_LIFTING) ? 0.5f : 1.0f);
-                    }
-                    if (P.type == SIMAPS_LIFTING && P.lifting && mask_bit(geo, SIMAPS_LIFTING, true, m0, m1)) vrob = fmaxf(vrob, 1.0f);
-                }
-                vov = vseg > 0.0f ? vseg : ovv[k];
-            }
-            put(0, p, vov);
-            if (cfg.use_robot_map) put(1, p, vrob);
-        }
-        ch = cfg.use_robot_map ? 2 : 1;
-    }
-
-    // distance channels (local -= local.min(), envs.py:2213-2216): up to 3, kept in registers
-    STAMP(6);
-    {
-        const int has_eu = cfg.use_distance_to_receptacle_map ? 1 : 0;
-        const int nd = has_eu + nsrc;
-        if (nd > 0) {
-            float vals[3][PPT];
-            float mins[3];
-            const float sps = (float)cfg.shortest_path_map_scale;
-            const float eus = (float)cfg.distance_to_receptacle_map_scale;
-#pragma unroll
-            for (int q = 0; q < 3; q++) {
-                mins[q] = INFINITY;
-                if (q >= nd) continue;
-                const bool eu = q < has_eu;  // Euclidean map first (envs.py:2083-2084)
-                const int s = q - has_eu;
-                const float *D = dist + (eu ? 0 : s) * DIST_FLOATS;
-                const float unreach = eu ? 0.0f : (sh.dmax[eu ? 0 : s] / 96.0f) * sps;
-#pragma unroll
-                for (int k = 0; k < PPT; k++) {
-                    float v = 0.0f;
-                    if (gpix[k] >= 0) {
-                        const int gi = gpix[k] >> 16, gj = gpix[k] & 0xffff;
-                        if (eu) {  // envs.py:2278-2286
-                            const double px = ((gj + 0.5) - (double)W / 2) / PPM, py = ((double)H / 2 - (gi + 0.5)) / PPM;
-                            const double dx = ev.receptacle_x - px, dy = ev.receptacle_y - py;
-                            v = (float)sqrt(dx * dx + dy * dy) * eus;
-                        } else {  // envs.py:2288-2300, 2514-2517
-                            const int r = gi - sh.i0, c = gj - sh.j0;
-                            float dd = __int_as_float(INF_BITS);
-                            if (r >= 0 && r < sh.h && c >= 0 && c < sh.w) dd = D[(r + 1) * sssp_pitch(sh.w) + c + 1];
-                            v = dd != __int_as_float(INF_BITS) ? (dd / 96.0f) * sps : unreach;
-                        }
-                    }
-                    vals[q][k] = v;
-                    mins[q] = fminf(mins[q], v);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 3; q++) {
-                if (q >= nd) continue;
-                const float m = wave_min(mins[q]);
-                if ((tid & 63) == 0) sh.red[q & 1][tid >> 6] = m;
-                __syncthreads();
-                float mm = sh.red[q & 1][0];
-                for (int k = 1; k < NT / 64; k++) mm = fminf(mm, sh.red[q & 1][k]);
-                mins[q] = mm;
-            }
-#pragma unroll
-            for (int q = 0; q < 3; q++) {
-                if (q >= nd) continue;
-#pragma unroll
-                for (int k = 0; k < PPT; k++) put(ch + q, tid + k * NT, vals[q][k] - mins[q]);
-            }
-            ch += nd;
-            __syncthreads();
-        }
-    }
-
-    // history / intention maps (rasterised into the LDS tile, which reuses the SSSP scratch)
-    STAMP(7);
-    const int thick = cfg.intention_map_line_thickness;
-    for (int pass = 0; pass < 2; pass++) {
-        const bool on = pass == 0 ? cfg.use_history_map : cfg.use_intention_map;
-        if (!on) continue;
-        raster_lines(sh, tile, cfg, rb, paths, pass == 0 ? 4 : cfg.intention_map_encoding);
-        for (int k = 0; k < PPT; k++) {
-            float v = 0.0f;
-            if (gpix[k] >= 0) v = tile_sample(tile, thick, gpix[k] >> 16, gpix[k] & 0xffff, sh.pi, sh.pj);
-            put(ch, tid + k * NT, v);
-        }
-        ch++;
-        __syncthreads();
-    }
-
-    // baseline intention channels (Mapper._get_intention_channels, envs.py:2349-2378)
-    STAMP(8);
-    if (cfg.use_intention_channels) {
-        if (tid == 0) {
-            // np.argsort of distances (insertion sort for n <= 16 -> stable)
-            double dd[SIMAPS_MAX_ROBOTS];
-            const RobotP &M = sh.rob[sh.me];
-            for (int q = 0; q < nr; q++) {
-                const double dx = sh.rob[q].x - M.x, dy = sh.rob[q].y - M.y;
-                dd[q] = sqrt(dx * dx + dy * dy);
-                int j = q;
-                while (j > 0 && dd[sh.order[j - 1]] > dd[q]) { sh.order[j] = sh.order[j - 1]; j--; }
-                sh.order[j] = q;
-            }
-            if (!cfg.intention_channel_spatial) {
-                int c2 = 0;
-                for (int q = 0; q < nr; q++) {
-                    const int k = sh.order[q];
-                    if (k == sh.me) continue;
-                    const RobotP &R = sh.rob[k];
-                    double rel0 = 0.0, rel1 = 0.0;
-                    if (!R.idle) {
-                        const double dx = R.tx - M.x, dy = R.ty - M.y;
-                        const double dist_t = sqrt(dx * dx + dy * dy);
-                        const double th = rb[sh.me].heading - atan2(R.ty - M.y, R.tx - M.x);
-                        rel0 = dist_t * sin(th);
-                        rel1 = dist_t * cos(th);
-                    }
-                    sh.nonsp[c2++] = (float)(cfg.intention_channel_nonspatial_scale * rel0);
-                    sh.nonsp[c2++] = (float)(cfg.intention_channel_nonspatial_scale * rel1);
-                }
-            }
-        }
-        __syncthreads();
-        int c2 = 0;
-        const float scale_f = (float)cfg.intention_map_scale;
-        for (int q = 0; q < nr; q++) {
-            const int kq = sh.order[q];
-            if (kq == sh.me) continue;
-            if (cfg.intention_channel_spatial) {
-                const RobotP &R = sh.rob[kq];
-                for (int k = 0; k < PPT; k++) {
-                    float v = 0.0f;
-                    if (gpix[k] >= 0 && !R.idle) {
-                        const int di = abs((gpix[k] >> 16) - R.tpi), dj = abs((gpix[k] & 0xffff) - R.tpj);
-                        const bool hit = thick > 1 ? (di + dj <= 1) : (di == 0 && dj == 0);
-                        v = hit ? scale_f : 0.0f;
-                    }
-                    put(ch, tid + k * NT, v);
-                }
-                ch++;
-            } else {
-                for (int e = 0; e < 2; e++, ch++, c2++)
-                    for (int k = 0; k < PPT; k++) put(ch, tid + k * NT, sh.nonsp[c2]);
-            }
-        }
-    }
-    STAMP(9);
 #ifdef SIMAPS_PHASE_STAMPS
     if (tid == 0 && blockIdx.x < MAX_STAMP_WG) g_stamps[blockIdx.x * NSTAMP + 10] = (unsigned long long)sh.rounds;
 #endif
@@ -881,7 +1099,7 @@ __global__ void __launch_bounds__(NT) sssp_grid_kernel(int H, int W, const uint8
         const uint64_t m = __ballot(f);
         if (lane == 0) { if (wd == 0) S.freeb[rr].lo = m; else S.freeb[rr].hi = m; }
     }
-    __syncthreads();
+    lds_barrier();
     sssp(sh, S, dist, 1);
     for (int k = tid; k < H * W; k += NT) {
         const int i = k / W - wi0, j = k % W - wj0;
@@ -938,6 +1156,21 @@ Geometry make_geometry()
     g.cube_half = CUBE_WIDTH / 2;
     g.cube_width = CUBE_WIDTH;
     g.cube_base = (BACKPACK_OFFSET + BASE_LENGTH) + (-0.007);  // LiftingRobot END_EFFECTOR + LIFTED_CUBE_OFFSET
+    for (int m = 0; m < 5; m++) {
+        const int t = m < 4 ? m : SIMAPS_LIFTING;
+        const bool cube = m == 4;
+        const int st = g.mask_start[t], wd = g.mask_width[t];
+        g.mrow0[m] = cube ? st - g.cube_w : st;
+        g.mcol0[m] = st;
+        g.mnrows[m] = (st + wd) - g.mrow0[m];
+        g.mncols[m] = wd;
+        for (int r = 0; r < 24; r++) {
+            uint32_t bits = 0;
+            for (int c = 0; c < wd && r < g.mnrows[m]; c++)
+                if (mask_bit(g, t, cube, g.mrow0[m] + r, g.mcol0[m] + c)) bits |= 1u << c;
+            g.mbits[m][r] = bits;
+        }
+    }
     return g;
 }
 

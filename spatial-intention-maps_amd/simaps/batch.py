@@ -96,9 +96,13 @@ def _to_dev(a, device):
 
 
 class StateBatch:
-    """One configuration's batch of agent-state stacks, resident on `device`."""
+    """One configuration's batch of agent-state stacks, resident on `device`.
 
-    def __init__(self, scenes, agents=None, device='cuda', layout='hwc'):
+    layout='chw' (default, device-native: every channel plane is written with full cache lines and is
+    what a conv policy consumes) or 'hwc' (the reference's (96, 96, C) memory order).  as_hwc() gives
+    the reference's index order as a zero-copy view either way."""
+
+    def __init__(self, scenes, agents=None, device='cuda', layout='chw'):
         s0 = scenes[0]
         for s in scenes:
             if (s['H'], s['W'], s['room_width'], s['room_length']) != (s0['H'], s0['W'], s0['room_width'], s0['room_length']) \
@@ -137,6 +141,10 @@ class StateBatch:
 
     def alloc_state(self):
         return torch.empty(self.out_shape(), dtype=torch.float32, device=self.device)
+
+    def as_hwc(self, state):
+        """The reference's (N, 96, 96, C) view of a rendered batch (zero-copy for the CHW layout)."""
+        return state.permute(0, 2, 3, 1) if self.cfg.layout_chw else state
 
     def alloc_debug(self):
         h, w = self.cfg.room_h, self.cfg.room_w

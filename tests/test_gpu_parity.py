@@ -55,9 +55,9 @@ GOLD = list(G.scene_cases())
 def test_golden_scene_state_and_intermediates(S, case):
     batch, K, synthetic = S
     cfg, e, a, scene, pre, z = case
-    b = batch.StateBatch([scene], agents=[(0, a)])
+    b = batch.StateBatch([scene], agents=[(0, a)], layout='hwc' if e == 0 else 'chw')
     dbg = b.alloc_debug()
-    st = b.render(debug=dbg)
+    st = b.as_hwc(b.render(debug=dbg))
     torch.cuda.synchronize()
     flags = scene['flags']
     assert int(dbg['status'][0]) & 0xff == 0
@@ -76,7 +76,7 @@ def test_golden_scene_state_and_intermediates(S, case):
 def test_layout_chw_matches_hwc(S):
     batch, K, synthetic = S
     scenes = [synthetic.make_scene('lifting_2_pushing_2-large_empty-all', e) for e in range(3)]
-    hwc = batch.StateBatch(scenes).render().cpu().numpy()
+    hwc = batch.StateBatch(scenes, layout='hwc').render().cpu().numpy()
     chw = batch.StateBatch(scenes, layout='chw').render().cpu().numpy()
     assert _bitwise(np.transpose(chw, (0, 2, 3, 1)), hwc)
 
@@ -91,7 +91,7 @@ def test_oracle_parity_fresh_seeds(S, cfg):
     batch, K, synthetic = S
     scenes = [synthetic.make_scene(cfg, 100 + e) for e in range(6)]
     b = batch.StateBatch(scenes)
-    st = b.render().cpu().numpy()
+    st = b.as_hwc(b.render()).cpu().numpy()
     for n, (e, a) in enumerate(b.agents):
         _check_state(st[n], O.agent_state(scenes[e], a), scenes[e]['flags'], len(scenes[e]['robots']))
 
@@ -102,8 +102,8 @@ def test_full_size_lifting_4_small_divider_properties(S):
     batch, K, synthetic = S
     scenes = [synthetic.make_scene('lifting_4-small_divider', e) for e in range(64)]
     b = batch.StateBatch(scenes)
-    s1 = b.render().cpu().numpy()
-    s2 = b.render().cpu().numpy()
+    s1 = b.as_hwc(b.render()).cpu().numpy()
+    s2 = b.as_hwc(b.render()).cpu().numpy()
     assert _bitwise(s1, s2)                       # idempotent / deterministic
     assert s1.shape == (256, 96, 96, 5)
     assert np.all(s1[..., 0] <= 1) and np.all(s1 >= 0)
@@ -131,7 +131,7 @@ def test_snap_slow_path_and_idle(S):
         scenes.append(s)
     b = batch.StateBatch(scenes)
     dbg = b.alloc_debug()
-    st = b.render(debug=dbg).cpu().numpy()
+    st = b.as_hwc(b.render(debug=dbg)).cpu().numpy()
     src = dbg['sources'].cpu().numpy()
     assert (src[:, 1, :2] != src[:, 1, 2:]).any(), 'expected at least one snapped robot source'
     for n, (e, a) in enumerate(b.agents):

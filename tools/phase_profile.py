@@ -10,7 +10,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ['SIMAPS_LIB'] = os.path.join(ROOT, 'spatial-intention-maps_amd', 'simaps', 'libsimaps_prof.so')
+os.environ['SIMAPS_LIB'] = os.environ.get('SIMAPS_PROF_LIB', os.path.join(ROOT, 'spatial-intention-maps_amd', 'simaps', 'libsimaps_prof.so'))
 sys.path.insert(0, os.path.join(ROOT, 'spatial-intention-maps_amd'))
 
 import numpy as np  # noqa: E402
@@ -18,18 +18,19 @@ import torch  # noqa: E402
 
 from simaps import _lib, batch, synthetic  # noqa: E402
 
-PHASES = ['params', 'cspace', 'snap', 'sssp', 'dbg/status', 'render ch0-1', 'dist ch', 'raster ch', 'intent ch']
+PHASES = ['params+stamps', 'cspace', 'snap+sssp_init', 'split(sweeps || render maps)', 'sssp_finish', 'distance channels']
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--config', default='lifting_4-small_divider')
     ap.add_argument('--envs', type=int, default=64)
+    ap.add_argument('--layout', default='chw')
     args = ap.parse_args()
     L = _lib.lib
     L.simaps_debug_read_stamps.argtypes = [ctypes.c_void_p]
     scenes = [synthetic.make_scene(args.config, e) for e in range(args.envs)]
-    b = batch.StateBatch(scenes)
+    b = batch.StateBatch(scenes, layout=args.layout)
     out = b.alloc_state()
     for _ in range(3):
         b.render(out)
@@ -39,10 +40,16 @@ def main():
     torch.cuda.synchronize()
     assert L.simaps_debug_read_stamps(st.ctypes.data) == 0
     st = st[:b.N].astype(np.int64)
-    t = st[:, :10]
+    t = st[:, :7]
     d = np.diff(t, axis=1) / 100.0  # 100 MHz -> us
-    res = {'config': args.config, 'N': b.N, 'total_us_median': float(np.median((t[:, 9] - t[:, 0]) / 100.0)),
-           'span_us': float((t[:, 9].max() - t[:, 0].min()) / 100.0),
+    sweeps = (st[:, 7] - st[:, 3]) / 100.0
+    maps = (st[:, 8] - st[:, 3]) / 100.0
+    res = {'config': args.config, 'layout': args.layout, 'N': b.N, 'total_us_median': float(np.median((t[:, 6] - t[:, 0]) / 100.0)),
+           'span_us': float((t[:, 6].max() - t[:, 0].min()) / 100.0),
+           'split_groups_us': {'sweeps_median': float(np.median(sweeps)), 'render_maps_median': float(np.median(maps)),
+                               'maps_ch01': float(np.median((st[:, 11] - st[:, 3]) / 100.0)),
+                               'maps_raster': float(np.median((st[:, 12] - st[:, 11]) / 100.0)),
+                               'maps_sample': float(np.median((st[:, 8] - st[:, 12]) / 100.0))},
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())},
            'phases_us': {p: {'median': float(np.median(d[:, i])), 'max': float(d[:, i].max())}
                          for i, p in enumerate(PHASES)}}
