@@ -18,6 +18,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'spatial-intention-maps_amd'))
 
+METRIC = 'agent-state-stacks/sec (96\u00d796\u00d7C maps) at 1/2/4/8 MI355X; HBM GB/s vs peak'  # BASELINE.json
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 
 
@@ -35,7 +36,7 @@ def cpu_baseline(config, budget_s=15.0):
     from simaps import synthetic
     oracle.agent_state(synthetic.make_scene(config, 10_000), 0)  # warm: build / load liboracle
     n, e, el = 0, 0, 0.0
-    while el < budget_s and e < 256:
+    while el < budget_s and e < 100_000:
         s = synthetic.make_scene(config, e)
         for a in range(len(s['robots'])):
             t0 = time.perf_counter()
@@ -46,6 +47,45 @@ def cpu_baseline(config, budget_s=15.0):
     return {'value': n / el, 'unit': 'stacks/s', 'cores': 1, 'kind': 'port',
             'sample': '%d agent stacks (%d envs of %s), OccupancyMap.update minus point scatter + '
                       'Mapper.get_state via oracle/ (numpy + C SPFA), 1 thread, %.1f s' % (n, e, config, el)}
+
+
+def rank_envs(rank, envs_per_rank):
+    """Env ids (= scene seeds) of one rank: a contiguous block of whole envs.
+    Weak scaling: every rank renders envs_per_rank envs, the job renders world * envs_per_rank."""
+    return list(range(rank * envs_per_rank, (rank + 1) * envs_per_rank))
+
+
+def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu'):
+    """The bench contract's timed region: `warmup` untimed steps, then barrier + sync, EXACTLY
+    `steps` steps, sync + barrier; returns the wall time, max-reduced over ranks (every rank gets
+    the job time).  step(k) runs step k (k < 0 for warmup); sync() waits for the device."""
+    import torch
+    import torch.distributed as dist
+    for k in range(warmup):
+        step(-1 - k)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    return max_over_ranks([elapsed], world, reduce_device)[0]
+
+
+def max_over_ranks(values, world, device='cpu'):
+    """Element-wise max of per-rank floats (identity for world == 1)."""
+    if world == 1:
+        return list(values)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.cpu()]
 
 
 def main():
@@ -72,33 +112,23 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
 
     from simaps import batch, synthetic
-    scenes = [synthetic.make_scene(args.config, rank * args.envs + e) for e in range(args.envs)]
+    scenes = [synthetic.make_scene(args.config, e) for e in rank_envs(rank, args.envs)]
     b = batch.StateBatch(scenes, device='cuda', layout=args.layout)
     out = b.alloc_state()
     stream = torch.cuda.current_stream()
 
-    for _ in range(args.warmup):
-        b.render(out)
-    torch.cuda.synchronize()
-
+    # HIP events on the launch stream bracket every timed launch (kernel time for the roofline).
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
-        b.render(out)
-        ev[k][1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], device='cuda', dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    def step(k):
+        if k >= 0:
+            ev[k][0].record(stream)
+        b.render(out, stream=stream)
+        if k >= 0:
+            ev[k][1].record(stream)
+
+    elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, 'cuda')
+    kern_ms = max_over_ranks([float(np.mean([s.elapsed_time(e) for s, e in ev]))], world, 'cuda')[0]
 
     stacks_per_step = b.N * world
     value = stacks_per_step * args.steps / elapsed
@@ -109,14 +139,14 @@ def main():
     if os.path.exists(tf):
         try:
             t = json.load(open(tf))
-            if t.get('config') == args.config and t.get('stacks_per_launch') == b.N:
+            if (t.get('config'), t.get('stacks_per_launch'), t.get('layout')) == (args.config, b.N, args.layout):
                 traffic = t.get('hbm_bytes_per_launch')
         except Exception:
             traffic = None
 
     if rank == 0:
         res = {
-            'metric': 'agent-state-stacks/sec (96x96xC maps)',
+            'metric': METRIC,
             'value': value, 'unit': 'stacks/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic (seeded scenes, SURVEY 8(d))',

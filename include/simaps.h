@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SIMAPS_ABI_VERSION 1
+#define SIMAPS_ABI_VERSION 2
 
 /* error codes */
 #define SIMAPS_OK 0
@@ -78,10 +78,14 @@ typedef struct simaps_env {
     int32_t reserved;
 } simaps_env;
 
-/* One agent-state stack to render: robot `robot` of env `env`. */
+/* One agent-state stack to render: robot `robot` of env `env`, whose persistent per-agent maps
+ * (occupancy / overhead, the robot's own Mapper state) are slot `map_slot` of the map arrays.
+ * Output stack n of a call belongs to agents[n]; rendering a subset (the robots awaiting a new
+ * action, envs.py:322-323) is a shorter agents[] over the same map arrays. */
 typedef struct simaps_agent {
     int32_t env;
     int32_t robot;
+    int32_t map_slot;
 } simaps_agent;
 
 /* Batch-wide configuration: VectorEnv state-representation flags (envs.py:39-45) + grid. */
@@ -127,8 +131,9 @@ int simaps_robot_mask(int type, int with_cube, float *out);
 
 /* Batched Mapper.get_state (+ the OccupancyMap.update work it needs).
  *   agents[N], envs[E], robots[R], paths[P][2] (fp64 x, y), all DEVICE pointers;
- *   occupancy [N, H, W] uint8 and overhead [N, H, W] float32: the per-agent global maps
- *   (OccupancyMap.occupancy_map, Mapper.global_overhead_map_without_robots), DEVICE;
+ *   occupancy [M, H, W] uint8 and overhead [M, H, W] float32: the per-agent global maps
+ *   (OccupancyMap.occupancy_map, Mapper.global_overhead_map_without_robots), DEVICE, indexed by
+ *   agents[n].map_slot (M = number of map slots, any N <= M of them rendered per call);
  *   state: [N, 96, 96, C] (or [N, C, 96, 96] if cfg->layout_chw) float32, DEVICE, C =
  *   simaps_num_channels(cfg, num_robots) -- every env of one call must have the same robot count
  *   when intention channels are on.  `num_robots_per_env` is that count (or 0 if unused).

@@ -1,24 +1,32 @@
 // simaps.hip -- MI355X (gfx950) kernels of the Spatial Intention Maps observation path.
 //
 // One workgroup (1024 threads = 16 waves) renders one agent-state stack end to end with every
-// intermediate resident in LDS (~151 KiB, one workgroup per CU):
+// intermediate resident in LDS (~158 KiB, one workgroup per CU):
 //
+//   0. params    per-robot stamp rotations (scipy rotate geometry, fp64) and <= 32x32 rotated
+//                mask bit tiles (Mapper._create_global_robot_map, envs.py:2251-2276).
 //   1. cspace    OccupancyMap.update (envs.py:2453-2454): 1 - max(1 - room_mask,
-//                binary_dilation(occ, disk(r))) inside the room rect; occupancy rows turned into
-//                bit rows by wave ballots, disk dilation as OR of shifted bit rows.
+//                binary_dilation(occ, disk(r))) inside the room rect; occupancy rows staged
+//                through LDS, turned into bit rows by wave ballots, disk dilation as OR of
+//                shifted bit rows.
 //   2. snap      OccupancyMap._closest_valid_cspace_indices (envs.py:2523-2524) =
 //                scipy distance_transform_edt(return_indices) evaluated at the <= 2 query pixels
 //                with scipy's own separable Voronoi tie-breaking (column pass, then one lane).
-//   3. SSSP      GridGraph._spfa (pyx:69-114) from the <= 2 snapped sources: pull-style
-//                Bellman-Ford over the LDS-resident room rect, frontier kept as bit rows
-//                (only 8-neighbours of last round's changed cells are re-evaluated).  The float32
-//                fixpoint is unique (dist[v] = min over paths of the left-fold f32 sum), so any
-//                schedule that runs to convergence is bit-identical to the reference's SPFA.
-//   4. render    Mapper.get_state (envs.py:2068-2113): 96x96 output pixels x C channels; the
-//                scipy order-0 rotate is evaluated as a gather (same fp64 index rule), robot
-//                stamps / masks are evaluated analytically per pixel, intention / history lines
-//                are rasterised into an LDS tile (closed-form Bresenham, fp64 linspace ramp,
-//                atomicMax) and grey-dilated at sample time.
+//   3. SSSP      GridGraph._spfa (pyx:69-114) from the <= 2 snapped sources as rounds of four
+//                concurrent directional sweeps per source (one wave each: down / up / right /
+//                left; lane = column or row, DPP lane shifts carry the diagonal neighbours).
+//                The float32 fixpoint is unique (dist[v] = min over paths of the left-fold f32
+//                sum), so any schedule that runs to convergence is bit-identical to the
+//                reference's SPFA.  WHILE the sweep waves run, the other waves render:
+//   4. render    Mapper.get_state (envs.py:2068-2113) channels that do not need distances:
+//                overhead + robot (robot stamps OR-ed into a 136x136 one-hot code map in LDS,
+//                then one gather per output pixel through the scipy order-0 rotate index rule),
+//                history / intention lines rasterised into an LDS tile (closed-form Bresenham,
+//                fp64 linspace ramp, atomicMax) and grey-dilated at sample time, intention
+//                channels.
+//   5. distance  after the sweeps converge, all 16 waves render the distance channels
+//                (Euclidean-to-receptacle, shortest-path maps with the reference's max / scale
+//                / min-subtract order).
 //
 // HBM traffic per stack: the occupancy window (room rect + r halo, bytes), the overhead window
 // gathered through L2 (<= 136^2 f32 footprint), the state write (96*96*C f32).  No intermediate
@@ -1003,7 +1011,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     STAMP(1);
     const int nsrc = sh.nsrc;
     if (nsrc > 0 || dbg.cspace) {
-        build_cspace(S, occupancy + (size_t)n * H * W, H, W, sh.i0, sh.j0, sh.h, sh.w, sh.r);
+        build_cspace(S, occupancy + (size_t)ag.map_slot * H * W, H, W, sh.i0, sh.j0, sh.h, sh.w, sh.r);
         if (dbg.cspace) {
             for (int k = tid; k < sh.h * sh.w; k += NT)
                 dbg.cspace[(size_t)n * sh.h * sh.w + k] = b_test(S.freeb[k / sh.w], k % sh.w) ? 1 : 0;
@@ -1028,7 +1036,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     } else {
         const int nw = NT / 64 - sweep_waves;
         const Group g{tid - 64 * sweep_waves, 64 * nw, sweep_waves ? sh.bar[1] : nullptr, nw};
-        render_maps(rc, g, geo, overhead + (size_t)n * H * W, rb, paths, tile);
+        render_maps(rc, g, geo, overhead + (size_t)ag.map_slot * H * W, rb, paths, tile);
         if (g.t == 0) STAMP_NB(8);
     }
     lds_barrier();
@@ -1101,9 +1109,11 @@ __global__ void __launch_bounds__(NT) sssp_grid_kernel(int H, int W, const uint8
     }
     lds_barrier();
     sssp(sh, S, dist, 1);
+    // A blocked source has no edges but still dist 0 (pyx:84-88 set dists[source] before the loop).
+    const int src_k = sh.src_s[0][0] * W + sh.src_s[0][1];
     for (int k = tid; k < H * W; k += NT) {
         const int i = k / W - wi0, j = k % W - wj0;
-        float v = -1.0f;
+        float v = k == src_k ? 0.0f : -1.0f;
         if (i >= 0 && i < wh && j >= 0 && j < ww) {
             const float d = dist[(i + 1) * sssp_pitch(ww) + j + 1];
             if (d != __int_as_float(INF_BITS)) v = d;

@@ -27,8 +27,9 @@ ROBOT_DTYPE = np.dtype([('x', '<f8'), ('y', '<f8'), ('heading', '<f8'), ('target
                         ('history_len', '<i4')], align=True)
 ENV_DTYPE = np.dtype([('receptacle_x', '<f8'), ('receptacle_y', '<f8'), ('has_receptacle', '<i4'),
                       ('robot_off', '<i4'), ('num_robots', '<i4'), ('reserved', '<i4')], align=True)
-AGENT_DTYPE = np.dtype([('env', '<i4'), ('robot', '<i4')], align=True)
-assert ROBOT_DTYPE.itemsize == 72 and ENV_DTYPE.itemsize == 32 and AGENT_DTYPE.itemsize == 8
+ABI_VERSION = 2  # include/simaps.h SIMAPS_ABI_VERSION
+AGENT_DTYPE = np.dtype([('env', '<i4'), ('robot', '<i4'), ('map_slot', '<i4')], align=True)
+assert ROBOT_DTYPE.itemsize == 72 and ENV_DTYPE.itemsize == 32 and AGENT_DTYPE.itemsize == 12
 
 
 class Config(ctypes.Structure):
@@ -67,7 +68,7 @@ def _load():
     L.simaps_get_state.restype = i32
     L.simaps_sssp_grid.argtypes = [i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp]
     L.simaps_sssp_grid.restype = i32
-    if L.simaps_abi_version() != 1:
+    if L.simaps_abi_version() != ABI_VERSION:
         raise ImportError('libsimaps ABI version mismatch')
     return L
 

@@ -86,9 +86,17 @@ def pack_descriptors(scenes, agents):
             k += 1
     ag = np.zeros(len(agents), dtype=_lib.AGENT_DTYPE)
     for n, (e, a) in enumerate(agents):
-        ag[n]['env'], ag[n]['robot'] = e, a
+        ag[n]['env'], ag[n]['robot'], ag[n]['map_slot'] = e, a, n
     paths = np.array(paths if paths else [(0.0, 0.0)], dtype=np.float64).reshape(-1, 2)
     return robots, envs, ag, paths
+
+
+def resolve_device(device):
+    """torch.device with an explicit index ('cuda' -> 'cuda:<current>'), so tensors' devices compare equal."""
+    dev = torch.device(device)
+    if dev.type == 'cuda' and dev.index is None:
+        dev = torch.device('cuda', torch.cuda.current_device())
+    return dev
 
 
 def _to_dev(a, device):
@@ -110,7 +118,9 @@ class StateBatch:
                 raise ValueError('one StateBatch holds one configuration (grid + flags)')
         if agents is None:
             agents = [(e, a) for e, s in enumerate(scenes) for a in range(len(s['robots']))]
-        self.scenes, self.agents, self.device = scenes, list(agents), torch.device(device)
+        self.scenes, self.agents, self.device = scenes, list(agents), resolve_device(device)
+        if self.device.type != 'cuda':
+            raise ValueError('StateBatch renders on a GPU device (got %s); there is no CPU path' % self.device)
         self.flags = s0['flags']
         self.H, self.W = s0['H'], s0['W']
         self.cfg = make_config(self.flags, s0['room_width'], s0['room_length'], layout)
@@ -132,37 +142,82 @@ class StateBatch:
         self.robots_d = _to_dev(robots, self.device)
         self.envs_d = _to_dev(envs, self.device)
         self.agents_d = _to_dev(ag, self.device)
+        self._subsets = {}
         self.paths_d = torch.from_numpy(paths).to(self.device)
 
-    def out_shape(self):
-        if self.cfg.layout_chw:
-            return (self.N, self.C, K.LOCAL_MAP_PIXEL_WIDTH, K.LOCAL_MAP_PIXEL_WIDTH)
-        return (self.N, K.LOCAL_MAP_PIXEL_WIDTH, K.LOCAL_MAP_PIXEL_WIDTH, self.C)
+    def set_maps(self, occupancy=None, overhead=None, slots=None):
+        """Replace the per-agent global maps -- what Mapper.update / OccupancyMap.update produce each
+        step (envs.py:2056-2062, 2447-2450) -- for every map slot, or for `slots` only.  Inputs are
+        [n, H, W] arrays / tensors (uint8 occupancy, float32 overhead-without-robots)."""
+        idx = None if slots is None else torch.as_tensor(list(slots), dtype=torch.long, device=self.device)
+        for name, dst, dt in (('occupancy', self.occupancy, torch.uint8), ('overhead', self.overhead, torch.float32)):
+            src = occupancy if name == 'occupancy' else overhead
+            if src is None:
+                continue
+            src = torch.as_tensor(src).to(device=self.device, dtype=dt)
+            want = (self.N if idx is None else len(idx), self.H, self.W)
+            if tuple(src.shape) != want:
+                raise ValueError('%s must have shape %s, got %s' % (name, want, tuple(src.shape)))
+            if idx is None:
+                dst.copy_(src)
+            else:
+                dst[idx] = src
 
-    def alloc_state(self):
-        return torch.empty(self.out_shape(), dtype=torch.float32, device=self.device)
+    def subset_descriptor(self, slots):
+        """Device agent list rendering only map slots `slots` (indices into self.agents), e.g. the
+        robots awaiting a new action (envs.py:322-323).  Cached per distinct subset."""
+        key = tuple(int(k) for k in slots)
+        d = self._subsets.get(key)
+        if d is None:
+            ag = np.zeros(len(key), dtype=_lib.AGENT_DTYPE)
+            for n, k in enumerate(key):
+                if not 0 <= k < self.N:
+                    raise IndexError('map slot %d outside [0, %d)' % (k, self.N))
+                ag[n]['env'], ag[n]['robot'] = self.agents[k]
+                ag[n]['map_slot'] = k
+            d = self._subsets[key] = _to_dev(ag, self.device)
+        return d, len(key)
+
+    def out_shape(self, n=None):
+        n = self.N if n is None else n
+        if self.cfg.layout_chw:
+            return (n, self.C, K.LOCAL_MAP_PIXEL_WIDTH, K.LOCAL_MAP_PIXEL_WIDTH)
+        return (n, K.LOCAL_MAP_PIXEL_WIDTH, K.LOCAL_MAP_PIXEL_WIDTH, self.C)
+
+    def alloc_state(self, n=None):
+        return torch.empty(self.out_shape(n), dtype=torch.float32, device=self.device)
 
     def as_hwc(self, state):
         """The reference's (N, 96, 96, C) view of a rendered batch (zero-copy for the CHW layout)."""
         return state.permute(0, 2, 3, 1) if self.cfg.layout_chw else state
 
-    def alloc_debug(self):
+    def alloc_debug(self, n=None):
+        n = self.N if n is None else n
         h, w = self.cfg.room_h, self.cfg.room_w
         z = lambda *s, dt: torch.empty(s, dtype=dt, device=self.device)  # noqa: E731
-        return {'cspace': z(self.N, h, w, dt=torch.uint8), 'sources': z(self.N, 2, 4, dt=torch.int32),
-                'dist': z(self.N, 2, h, w, dt=torch.float32), 'status': z(self.N, dt=torch.int32)}
+        return {'cspace': z(n, h, w, dt=torch.uint8), 'sources': z(n, 2, 4, dt=torch.int32),
+                'dist': z(n, 2, h, w, dt=torch.float32), 'status': z(n, dt=torch.int32)}
 
-    def render(self, out=None, debug=None, stream=None):
-        """Launch the fused kernel: every agent's stack into `out` (allocated if None)."""
+    def render(self, out=None, debug=None, stream=None, slots=None):
+        """Launch the fused kernel: the stacks of every agent (or of map slots `slots`, in that
+        order) into `out` (allocated if None)."""
+        agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
         if out is None:
-            out = self.alloc_state()
-        assert out.is_contiguous() and tuple(out.shape) == self.out_shape() and out.dtype == torch.float32
+            out = self.alloc_state(n)
+        if not (out.is_contiguous() and tuple(out.shape) == self.out_shape(n) and out.dtype == torch.float32
+                and out.device == self.device):
+            raise ValueError('out must be a contiguous float32 %s tensor on %s' % (self.out_shape(n), self.device))
+        if n == 0:
+            return out
         dbg = None
         if debug is not None:
+            for k, v in debug.items():
+                if v is not None and (v.shape[0] != n or not v.is_contiguous() or v.device != self.device):
+                    raise ValueError('debug[%r] must be contiguous with leading dim %d on %s' % (k, n, self.device))
             dbg = _lib.Debug(*(debug[k].data_ptr() if debug.get(k) is not None else None
                                for k in ('cspace', 'sources', 'dist', 'status')))
         _lib.check(_lib.lib.simaps_get_state(
-            self.cfg, self.N, _lib.ptr(self.agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d),
+            self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d),
             _lib.ptr(self.paths_d), _lib.ptr(self.occupancy), _lib.ptr(self.overhead), _lib.ptr(out),
             self.num_robots if self.flags['use_intention_channels'] else 0,
             None if dbg is None else dbg, _lib.stream_handle(stream)))

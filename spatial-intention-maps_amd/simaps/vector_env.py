@@ -1,0 +1,136 @@
+"""Drop-in host interface for the observation path: VectorEnv.get_state() and GridGraph.
+
+The reference calls the path through Python methods:
+
+  VectorEnv.get_state(all_robots=False, save_figures=False)          envs.py:322-323
+      -> [[robot.get_state() if robot.awaiting_new_action or all_robots else None
+           for robot in robot_group] for robot_group in self.robot_groups]
+  Robot.get_state() -> Mapper.get_state() -> (96, 96, C) float32 HWC   envs.py:928-929, 2068-2185
+  GridGraph(grid).shortest_path_image(src) / shortest_path_distance    shortest_paths.pyx:24-67, 156-167
+
+VectorEnvObservations keeps that return structure for a batch of E envs of one configuration
+(one list-of-lists per env) and renders every requested stack in ONE launch of the fused HIP
+kernel (simaps_get_state).  The per-agent maps (OccupancyMap.occupancy_map and
+Mapper.global_overhead_map_without_robots) stay resident on the device across steps; per step
+only the scene descriptor (poses, controller state, paths) is uploaded.  There is no CPU
+fallback: constructing either class without libsimaps.so / a GPU raises.
+"""
+import numpy as np
+import torch
+
+from . import batch as _batch
+
+
+def robot_groups(scene):
+    """VectorEnv.robot_groups (envs.py:486-496): robot indices grouped by group_index, in order."""
+    ng = 1 + max(r['group_index'] for r in scene['robots'])
+    groups = [[] for _ in range(ng)]
+    for k, r in enumerate(scene['robots']):
+        groups[r['group_index']].append(k)
+    return groups
+
+
+class VectorEnvObservations:
+    """The observation half of E VectorEnvs of one configuration, device-resident.
+
+    scenes: list of scene dicts (simaps.synthetic format: flags, grid, robots with poses /
+    controller state / paths, receptacle, per-agent occupancy + overhead maps).
+    layout: 'hwc' returns (96, 96, C) stacks exactly like the reference; 'chw' renders
+    (C, 96, 96) planes (what a conv policy consumes, policies.py:44-45) -- states returned by
+    get_state() are always the reference's (96, 96, C) index order (views for 'chw')."""
+
+    def __init__(self, scenes, device='cuda', layout='hwc'):
+        self.batch = _batch.StateBatch(scenes, device=device, layout=layout)
+        self.groups = [robot_groups(s) for s in scenes]
+        self.slot = {ea: n for n, ea in enumerate(self.batch.agents)}
+        self.num_envs = len(scenes)
+
+    # -- per-step inputs -------------------------------------------------------------------------
+    def update(self, scenes=None, occupancy=None, overhead=None, slots=None):
+        """New scene descriptors (robot poses, lift state, idle flags, paths, receptacle) and/or
+        new per-agent maps for every slot or for map slots `slots` (Robot.update_map, envs.py:925)."""
+        if scenes is not None:
+            if len(scenes) != self.num_envs or any(len(s['robots']) != len(o['robots'])
+                                                   for s, o in zip(scenes, self.batch.scenes)):
+                raise ValueError('update() keeps the batch shape: same envs, same robots per env')
+            self.batch.set_descriptors(scenes)
+            self.batch.scenes = scenes
+        if occupancy is not None or overhead is not None:
+            self.batch.set_maps(occupancy, overhead, slots)
+
+    # -- VectorEnv.get_state ---------------------------------------------------------------------
+    def get_state(self, all_robots=False, awaiting=None, save_figures=False, numpy=False, stream=None):
+        """[env][group][robot] -> (96, 96, C) float32 state, or None for robots not awaiting a new
+        action (envs.py:322-323).  awaiting: per env, per robot truthy flags
+        (robot.awaiting_new_action); None means every robot.  numpy=True returns host NumPy arrays
+        like the reference (one device->host copy for the whole batch); otherwise device tensors."""
+        if save_figures:
+            raise NotImplementedError('save_figures is a host-side matplotlib debug path (out of scope)')
+        want = []
+        for e, s in enumerate(self.batch.scenes):
+            for a in range(len(s['robots'])):
+                if all_robots or awaiting is None or awaiting[e][a]:
+                    want.append(self.slot[(e, a)])
+        out = self.batch.as_hwc(self.batch.render(slots=want, stream=stream))
+        if numpy:
+            out = out.cpu().numpy()
+        pos = {k: n for n, k in enumerate(want)}
+        res = []
+        for e in range(self.num_envs):
+            res.append([[out[pos[self.slot[(e, a)]]] if self.slot[(e, a)] in pos else None for a in g]
+                        for g in self.groups[e]])
+        return res
+
+
+class GridGraph:
+    """shortest_paths.pyx GridGraph (pyx:10-167) on the device: 8-connected grid over cells with
+    grid != 0, weights 1 / float32(sqrt(2)), float32 distances, unreachable -> -1.
+
+    Results are bit-identical to the reference SPFA (the float32 fixpoint is unique, SURVEY.md
+    a10).  Like _spfa_with_cache (pyx:116-119) the images are cached per source for the life of
+    the graph.  The free cells must fit the LDS-resident window limit of include/simaps.h."""
+
+    def __init__(self, grid, device='cuda'):
+        g = torch.as_tensor(np.ascontiguousarray(grid) if isinstance(grid, np.ndarray) else grid)
+        if g.dim() != 2:
+            raise ValueError('grid must be 2-D')
+        self.device = _batch.resolve_device(device)
+        self.grid = g.to(device=self.device, dtype=torch.uint8).contiguous()
+        self.shape = tuple(self.grid.shape)
+        free = torch.nonzero(self.grid)
+        if free.numel():
+            (i0, j0), (i1, j1) = free.min(0).values.tolist(), free.max(0).values.tolist()
+            self.window = (i0, j0, i1 - i0 + 1, j1 - j0 + 1)
+        else:
+            self.window = (0, 0, 1, 1)
+        self._cache = {}
+
+    def _check_source(self, source):
+        i, j = int(source[0]), int(source[1])
+        if not (0 <= i < self.shape[0] and 0 <= j < self.shape[1]):
+            raise IndexError('cell %s outside the %dx%d grid' % (((i, j),) + self.shape))
+        return i, j
+
+    def shortest_path_images(self, sources, stream=None):
+        """Batched shortest_path_image for many sources: [len(sources), H, W] device tensor."""
+        srcs = [self._check_source(s) for s in sources]
+        todo = [s for s in dict.fromkeys(srcs) if s not in self._cache]
+        if todo:
+            grids = self.grid.unsqueeze(0).expand(len(todo), *self.shape).contiguous()
+            imgs = _batch.sssp_grid(grids, torch.tensor(todo, dtype=torch.int32), window=self.window, stream=stream)
+            for k, s in enumerate(todo):
+                self._cache[s] = imgs[k]
+        return torch.stack([self._cache[s] for s in srcs]) if srcs else \
+            torch.empty((0,) + self.shape, dtype=torch.float32, device=self.device)
+
+    def shortest_path_image(self, source):
+        """(H, W) float32 NumPy image of distances from `source` (pyx:165-167)."""
+        return self.shortest_path_images([source])[0].cpu().numpy()
+
+    def shortest_path_distance(self, source, target):
+        """dists[target] from `source` as a Python float (pyx:156-163); -1 if unreachable."""
+        i, j = self._check_source(target)
+        return float(self.shortest_path_images([source])[0][i, j])
+
+
+__all__ = ['VectorEnvObservations', 'GridGraph', 'robot_groups']

@@ -28,14 +28,14 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(_lib.lib, name), name
         assert isinstance(getattr(_lib.lib, name), ctypes._CFuncPtr)
     assert set(_lib.EXPORTED) == set(declared_symbols())
-    assert _lib.lib.simaps_abi_version() == 1
+    assert _lib.lib.simaps_abi_version() == 2
 
 
 def test_struct_layouts_match_header():
     from simaps import _lib
     assert _lib.ROBOT_DTYPE.itemsize == 72
     assert _lib.ENV_DTYPE.itemsize == 32
-    assert _lib.AGENT_DTYPE.itemsize == 8
+    assert _lib.AGENT_DTYPE.itemsize == 12
     assert ctypes.sizeof(_lib.Config) == 18 * 4 + 4 * 8
     assert ctypes.sizeof(_lib.Debug) == 4 * 8
 
@@ -70,3 +70,10 @@ def test_error_paths_do_not_launch():
     rc = _lib.lib.simaps_get_state(c, 1, None, None, None, None, None, None, None, 0, None, None)
     assert rc == -2 and b'thickness' in _lib.lib.simaps_last_error()
     assert _lib.lib.simaps_sssp_grid(1, 300, 300, None, None, None, 0, 0, 300, 300, None) == -1
+
+
+def test_statebatch_refuses_cpu_device():
+    """The product path has no CPU fallback: a host device is refused before any launch."""
+    from simaps import batch, synthetic
+    with pytest.raises(ValueError):
+        batch.StateBatch([synthetic.make_scene('lifting_1-small_empty', 0)], device='cpu')

@@ -1,0 +1,93 @@
+"""GPU tests of the drop-in host interface (simaps.vector_env) against the oracle.
+
+VectorEnv.get_state structure (envs.py:322-323): list over robot groups of lists over robots,
+None for robots not awaiting an action; GridGraph.shortest_path_image / _distance
+(shortest_paths.pyx:156-167) including the per-source cache and a blocked source.
+"""
+import numpy as np
+import pytest
+import torch
+
+import goldens as G
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def V():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a GPU (run with -m gpu on an MI355X)')
+    from simaps import synthetic, vector_env
+    return synthetic, vector_env
+
+
+def _bitwise(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and np.array_equal(a.view(np.int32), b.view(np.int32))
+
+
+@pytest.mark.parametrize('layout', ['hwc', 'chw'])
+def test_get_state_structure_and_awaiting_subset(V, layout):
+    synthetic, vector_env = V
+    cfg = 'lifting_2_throwing_2-large_empty'       # two robot groups
+    scenes = [synthetic.make_scene(cfg, 500 + e) for e in range(3)]
+    obs = vector_env.VectorEnvObservations(scenes, layout=layout)
+    rs = np.random.RandomState(3)
+    awaiting = [[bool(rs.randint(2)) for _ in s['robots']] for s in scenes]
+    awaiting[0] = [False] * 4                        # an env with nobody awaiting
+    st = obs.get_state(awaiting=awaiting, numpy=True)
+    full = obs.get_state(all_robots=True)
+    assert len(st) == 3
+    for e, s in enumerate(scenes):
+        groups = vector_env.robot_groups(s)
+        assert [len(g) for g in st[e]] == [len(g) for g in groups] == [2, 2]
+        for g, idx in zip(st[e], groups):
+            for x, a in zip(g, idx):
+                if not awaiting[e][a]:
+                    assert x is None
+                    continue
+                assert isinstance(x, np.ndarray) and x.shape == (96, 96, 5) and x.dtype == np.float32
+                assert _bitwise(x, O.agent_state(s, a))
+        for g, idx in zip(full[e], groups):
+            for x, a in zip(g, idx):
+                assert isinstance(x, torch.Tensor) and tuple(x.shape) == (96, 96, 5)
+                assert _bitwise(x.cpu().numpy(), O.agent_state(s, a))
+
+
+def test_update_descriptors_and_maps(V):
+    synthetic, vector_env = V
+    cfg = 'lifting_4-small_divider'
+    a = [synthetic.make_scene(cfg, 600 + e) for e in range(2)]
+    b = [synthetic.make_scene(cfg, 700 + e) for e in range(2)]
+    obs = vector_env.VectorEnvObservations(a)
+    obs.get_state()
+    # new step: descriptors of b, maps of b for agent slots 1 and 6 only -> those two match the
+    # oracle on a scene mixing b's descriptor with their own b maps
+    occ = np.stack([b[e]['occupancy'][r] for e, r in [(0, 1), (1, 2)]])
+    ovh = np.stack([b[e]['overhead'][r] for e, r in [(0, 1), (1, 2)]])
+    obs.update(scenes=b, occupancy=occ, overhead=ovh, slots=[1, 6])
+    st = obs.get_state(numpy=True)
+    assert _bitwise(st[0][0][1], O.agent_state(b[0], 1))
+    assert _bitwise(st[1][0][2], O.agent_state(b[1], 2))
+    mixed = dict(b[0], occupancy=a[0]['occupancy'], overhead=a[0]['overhead'])
+    assert _bitwise(st[0][0][0], O.agent_state(mixed, 0))   # slot 0 kept a's maps
+    with pytest.raises(ValueError):
+        obs.update(scenes=b[:1])
+
+
+def test_gridgraph_dropin(V):
+    synthetic, vector_env = V
+    g = G.load('sssp.npz')
+    grid = g['demo_cspace']
+    gg = vector_env.GridGraph(grid)
+    img = gg.shortest_path_image((75, 156))
+    assert _bitwise(img, g['demo_image'])
+    assert gg.shortest_path_distance((75, 156), (131, 112)) == float(g['demo_distance'])
+    assert (75, 156) in gg._cache                     # _spfa_with_cache semantics
+    # a blocked source: distance 0 at the source, -1 everywhere else (pyx:84-85, 110-112)
+    blocked = tuple(int(x) for x in np.argwhere(grid == 0)[len(np.argwhere(grid == 0)) // 2])
+    bi = gg.shortest_path_image(blocked)
+    assert _bitwise(bi, O.spfa_image(grid, blocked))
+    with pytest.raises(IndexError):
+        gg.shortest_path_distance((75, 156), (10_000, 0))
