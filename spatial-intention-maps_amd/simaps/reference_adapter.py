@@ -1,0 +1,61 @@
+"""Read a reference VectorEnv (envs.py) into the scene format the device path consumes.
+
+This is the glue a maintainer adds to the reference to switch VectorEnv.get_state() to the
+device path.  It only READS attributes the reference objects already have:
+
+  env.robots, env.robot_config, env.room_length / room_width, env.receptacle_position and the
+      state-representation flags                                          envs.py:39-45, 59-61, 150-151
+  robot.group_index, robot.get_position(), robot.get_heading(), robot.is_idle(),
+      robot.waypoint_positions, robot.controller.waypoint_index,
+      robot.target_end_effector_position, LiftingRobot.lift_state         envs.py:815-980, 1169-1282, 1475-1479
+  robot.mapper.global_overhead_map_without_robots                         envs.py:2026
+  robot.mapper.global_occupancy_map.occupancy_map                         envs.py:2029, 2417
+
+No simulator or reference import is needed here; objects are duck-typed.
+"""
+import numpy as np
+
+from . import constants as K
+
+ROBOT_TYPE_BY_CLASS = {'LiftingRobot': 'lifting_robot', 'PushingRobot': 'pushing_robot',
+                       'ThrowingRobot': 'throwing_robot', 'RescueRobot': 'rescue_robot'}
+
+
+def robot_type(robot):
+    for cls in type(robot).__mro__:
+        if cls.__name__ in ROBOT_TYPE_BY_CLASS:
+            return ROBOT_TYPE_BY_CLASS[cls.__name__]
+    raise TypeError('not a reference robot class: %s' % type(robot).__name__)
+
+
+def scene_from_env(env, with_maps=True):
+    """The scene dict (simaps.synthetic format) of one reference VectorEnv at its current step."""
+    flags = {k: getattr(env, k) for k in K.DEFAULT_FLAGS}
+    H, W = K.padded_room_shape(env.room_width, env.room_length)
+    robots = []
+    for r in env.robots:
+        typ = robot_type(r)
+        robots.append({
+            'type': typ, 'cls': K.ROBOT_TYPES.index(typ), 'group_index': int(r.group_index),
+            'position': tuple(r.get_position()), 'heading': float(r.get_heading()),
+            'lift_state': getattr(r, 'lift_state', None), 'idle': bool(r.is_idle()),
+            'waypoint_positions': [tuple(p) for p in r.waypoint_positions],
+            'waypoint_index': int(r.controller.waypoint_index),
+            'target_ee': tuple(r.target_end_effector_position),
+        })
+    scene = {
+        'config': None, 'env_name': None, 'room_length': env.room_length, 'room_width': env.room_width,
+        'flags': flags, 'robot_config': env.robot_config, 'H': H, 'W': W,
+        'receptacle_position': getattr(env, 'receptacle_position', None), 'robots': robots,
+    }
+    if with_maps:
+        scene['occupancy'] = np.stack([np.asarray(r.mapper.global_occupancy_map.occupancy_map, dtype=np.uint8)
+                                       for r in env.robots])
+        scene['overhead'] = np.stack([np.asarray(r.mapper.global_overhead_map_without_robots, dtype=np.float32)
+                                      for r in env.robots])
+    return scene
+
+
+def awaiting_flags(env):
+    """[robot.awaiting_new_action for robot in env.robots] (envs.py:322-323)."""
+    return [bool(r.awaiting_new_action) for r in env.robots]
