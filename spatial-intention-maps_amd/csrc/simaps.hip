@@ -167,7 +167,6 @@ struct Shared {
     int envg[2][SIMAPS_MAX_ROOM_W];  // Voronoi envelope (rect columns) per source
     unsigned bar[2][4];              // group barriers {count, generation, timeout, -}: [0] sweeps, [1] render
     int changed[3];                  // rotating per-round "some sweep improved a cell" flags
-    float dummy[8][64];              // sweep store sink for non-improving lanes (1 slot per lane)
     Seg seg[MAX_SEG];
 };
 
@@ -414,60 +413,94 @@ __device__ __forceinline__ float from_next_lane(float v)  // lane i <- lane i+1 
 
 __device__ __forceinline__ int sssp_pitch(int w) { return (w + 2) | 1; }
 
-// One sweep of one wave.  dir: 0 down, 1 up, 2 right, 3 left.  Returns true if it improved a cell.
+// One sweep of one wave.  DIR: 0 down, 1 up (lines = rows), 2 right, 3 left (lines = columns);
+// CPL: cells per lane across the line (1: span <= 64, 2: span <= 128).  Returns true if a lane
+// found an improvement.
 // Blocked and padding cells hold a quiet NaN: every comparison with NaN is false, so a blocked cell
 // is never written and its NaN never wins a min (v_min3 drops NaN operands) -- no free-bit tests.
+// Improvements are LDS atomic float mins: a cell's value never increases, even when another
+// sweep improved it after this wave prefetched it, so rounds terminate and the last round (no
+// candidate below the prefetched values, which are >= the current ones) proves the fixpoint.
+// Lines are prefetched P steps ahead into a register ring; lanes past the span read the NaN corner.
 constexpr unsigned QNAN_BITS = 0x7fc00000u;
 
-__device__ bool sweep(float *D, float *dummy, int h, int w, int pw, int dir_in)
+typedef __attribute__((address_space(3))) float lds_float;
+
+template <int DIR, int CPL>
+__device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw)
 {
+    constexpr bool VERT = DIR < 2, FWD = (DIR & 1) == 0;
+    constexpr int P = 4;
     const int lane = threadIdx.x & 63;
-    const int dir = __builtin_amdgcn_readfirstlane(dir_in);
-    const bool vert = dir < 2;
-    const int len = vert ? h : w, span = vert ? w : h;
-    const int sl = vert ? pw : 1, sa = vert ? 1 : pw;  // address strides along / across the line
-    const int a0 = 1 + 2 * lane;
-    const bool v0 = a0 <= span, v1 = a0 + 1 <= span;
-    const bool fwd = (dir & 1) == 0;
-    const int dl = fwd ? sl : -sl;
-    // lanes past the span read / never write: point them at a padding cell (NaN)
-    int ad0 = v0 ? (fwd ? 1 : len) * sl + a0 * sa : 0;
-    int ad1 = v1 ? ad0 + sa : 0;
-    const int st0 = v0 ? dl : 0, st1 = v1 ? dl : 0;
+    const int sl = VERT ? pw : 1;             // address stride along the sweep (line to line)
+    const int sa = VERT ? 1 : pw;             // across the line (cell 0 -> cell 1 of a lane)
+    const int a0 = 1 + CPL * lane;
+    const bool act = a0 <= span;              // cell 1 of the last lane may be the NaN border
+    const int st = act ? (FWD ? sl : -sl) : 0;
+    int cur = act ? (FWD ? 1 : len) * sl + a0 * sa : 0;
+    int pf = cur;
     const float QN = __int_as_float(QNAN_BITS);
+    // ring of P prefetched lines in named registers (A..D: lines t, t+1, t+2, t+3 at step t)
+    float A0 = D[pf], A1 = CPL == 2 ? D[pf + sa] : QN; pf += st;
+    float B0 = D[pf], B1 = CPL == 2 ? D[pf + sa] : QN; pf += st;
+    float C0 = D[pf], C1 = CPL == 2 ? D[pf + sa] : QN; pf += st;
+    float E0 = D[pf], E1 = CPL == 2 ? D[pf + sa] : QN; pf += st;
     float p0 = QN, p1 = QN;
-    bool changed = false;
-    // Two register pairs (A: even lines, B: odd lines), each refilled with the line two ahead
-    // right after its old value is consumed: no register rotation at the back-edge, so each
-    // load has a whole step to land.  Padding rows beyond the last line are NaN (never used).
-    float A0 = D[ad0], A1 = D[ad1];
-    float B0 = D[ad0 + st0], B1 = D[ad1 + st1];
-    auto step = [&](float &R0, float &R1, int) {
-        const float pm = from_prev_lane(p1);  // previous line, across index a0 - 1
-        const float pp = from_next_lane(p0);  // previous line, across index a0 + 2
-        const float m0 = fminf(fminf(p0 + 1.0f, pm + SQRT2F), p1 + SQRT2F);
-        const float m1 = fminf(fminf(p1 + 1.0f, p0 + SQRT2F), pp + SQRT2F);
-        const bool u0 = m0 < R0, u1 = m1 < R1;  // false for NaN (blocked) d or NaN m
-        const float c0 = u0 ? m0 : R0, c1 = u1 ? m1 : R1;
-        // exactly 2 stores + 2 loads per step (non-improving lanes store into a private dummy slot),
-        // so the compiler's LDS counter waits stay partial and the loads overlap the next step.
-        // The final two prefetches read past the line range: still inside this kernel's LDS block.
-        *(u0 ? &D[ad0] : &dummy[lane]) = c0;  // both sinks share the lane's slot (never read)
-        *(u1 ? &D[ad1] : &dummy[lane]) = c1;
-        changed |= u0 | u1;
-        p0 = c0;
-        p1 = c1;
-        R0 = D[ad0 + 2 * st0];
-        R1 = D[ad1 + 2 * st1];
-        ad0 += st0;
-        ad1 += st1;
-    };
-    // even trip count: an odd line count ends with one extra step on the NaN padding line (no writes)
-    for (int t = 0; t < len; t += 2) {
-        step(A0, A1, t);
-        step(B0, B1, t + 1);
+    bool chg = false;
+#define SWEEP_STEP(R0, R1, LIVE)                                                                        \
+    do {                                                                                                \
+        float m0, m1 = QN;                                                                              \
+        if (CPL == 2) {                                                                                 \
+            const float pm = from_prev_lane(p1), pp = from_next_lane(p0);                               \
+            m0 = fminf(fminf(p0 + 1.0f, pm + SQRT2F), p1 + SQRT2F);                                     \
+            m1 = fminf(fminf(p1 + 1.0f, p0 + SQRT2F), pp + SQRT2F);                                     \
+        } else {                                                                                        \
+            const float pm = from_prev_lane(p0), pp = from_next_lane(p0);                               \
+            m0 = fminf(fminf(p0 + 1.0f, pm + SQRT2F), pp + SQRT2F);                                     \
+        }                                                                                               \
+        const bool u0 = (LIVE) && m0 < R0;                                                              \
+        const bool u1 = CPL == 2 && (LIVE) && m1 < R1;                                                  \
+        if (u0) __hip_atomic_fetch_min(&D[cur], m0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);    \
+        if (u1) __hip_atomic_fetch_min(&D[cur + sa], m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+        chg |= u0 | u1;                                                                                 \
+        /* p = u ? m : R, branch-free: NaN (blocked) R propagates, NaN m (no live predecessor) drops */ \
+        p0 = __builtin_elementwise_minimum(R0, fminf(m0, INFINITY));                                   \
+        if (CPL == 2) p1 = __builtin_elementwise_minimum(R1, fminf(m1, INFINITY));                     \
+        R0 = D[pf];                                                                                     \
+        if (CPL == 2) R1 = D[pf + sa];                                                                  \
+        cur += st;                                                                                      \
+        pf += st;                                                                                       \
+    } while (0)
+    int t = 0;
+    for (; t + P <= len; t += P) {
+        SWEEP_STEP(A0, A1, true);
+        SWEEP_STEP(B0, B1, true);
+        SWEEP_STEP(C0, C1, true);
+        SWEEP_STEP(E0, E1, true);
     }
-    return __ballot(changed) != 0;
+    if (t < len) {  // 1..3 remaining lines; steps past the end store nothing
+        SWEEP_STEP(A0, A1, t < len);
+        SWEEP_STEP(B0, B1, t + 1 < len);
+        SWEEP_STEP(C0, C1, t + 2 < len);
+    }
+#undef SWEEP_STEP
+    return __ballot(chg) != 0;
+}
+
+__device__ bool sweep(float *Dg, int h, int w, int pw, int dir_in)
+{
+    lds_float *D = (lds_float *)Dg;  // the distance arrays live in LDS: keep ds_* addressing
+    // wave-uniform loop bounds: scalar loop control, no exec-mask merges at the back edge
+    const int dir = __builtin_amdgcn_readfirstlane(dir_in);
+    h = __builtin_amdgcn_readfirstlane(h);
+    w = __builtin_amdgcn_readfirstlane(w);
+    pw = __builtin_amdgcn_readfirstlane(pw);
+    switch (dir) {
+    case 0: return w <= 64 ? sweep_t<0, 1>(D, h, w, pw) : sweep_t<0, 2>(D, h, w, pw);
+    case 1: return w <= 64 ? sweep_t<1, 1>(D, h, w, pw) : sweep_t<1, 2>(D, h, w, pw);
+    case 2: return h <= 64 ? sweep_t<2, 1>(D, w, h, pw) : sweep_t<2, 2>(D, w, h, pw);
+    default: return h <= 64 ? sweep_t<3, 1>(D, w, h, pw) : sweep_t<3, 2>(D, w, h, pw);
+    }
 }
 
 // all threads: free cells +inf, blocked / padding NaN, sources 0
@@ -506,7 +539,7 @@ __device__ void sssp_rounds(Shared &sh, float *dist, int nsrc, const Group &g)
     for (int round = 0;; round++) {
         if (tid == 0) sh.changed[(round + 1) % 3] = 0;
         const int s = wave >> 2;
-        if (sh.src_ok[s] && sweep(dist + s * DIST_FLOATS, sh.dummy[wave], h, w, pw, wave & 3) && (tid & 63) == 0)
+        if (sh.src_ok[s] && sweep(dist + s * DIST_FLOATS, h, w, pw, wave & 3) && (tid & 63) == 0)
             sh.changed[round % 3] = 1;
         g.sync();
         if (!sh.changed[round % 3] || round >= max_rounds) {
@@ -1031,12 +1064,20 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const RenderCtx rc{cfg, sh, out, C, n};
     const int sweep_waves = 4 * nsrc;
     if ((tid >> 6) < sweep_waves) {
+#ifdef SIMAPS_SWEEP_PRIO
+        __builtin_amdgcn_s_setprio(SIMAPS_SWEEP_PRIO);
+#endif
         sssp_rounds(sh, dist, nsrc, Group{tid, 64 * sweep_waves, sh.bar[0], sweep_waves});
+#ifdef SIMAPS_SWEEP_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         STAMP_NB(7);
     } else {
         const int nw = NT / 64 - sweep_waves;
         const Group g{tid - 64 * sweep_waves, 64 * nw, sweep_waves ? sh.bar[1] : nullptr, nw};
+#ifndef SIMAPS_ABL_NORENDER  // diagnostic: sweeps alone (output channels 0.. left unwritten)
         render_maps(rc, g, geo, overhead + (size_t)ag.map_slot * H * W, rb, paths, tile);
+#endif
         if (g.t == 0) STAMP_NB(8);
     }
     lds_barrier();
