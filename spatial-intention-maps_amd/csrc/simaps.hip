@@ -160,7 +160,7 @@ struct Shared {
     int nseg;
     int seg_robot_cnt[SIMAPS_MAX_ROBOTS];
     int order[SIMAPS_MAX_ROBOTS];
-    float red[2][16];
+    float red[3][16];
     float nonsp[2 * SIMAPS_MAX_ROBOTS];
     RobotP rob[SIMAPS_MAX_ROBOTS];
     int colbest[2][SIMAPS_MAX_ROOM_W];
@@ -204,7 +204,7 @@ __device__ __forceinline__ float wave_max(float v)
 // Phase: occupancy window -> free-cell bit rows (cspace inside the room rect)
 // ------------------------------------------------------------------------------------------------
 // occ: the agent's occupancy map [H, W] (nonzero = obstacle).  r = disk radius.
-__device__ void build_cspace(SsspScratch &S, const uint8_t *__restrict__ occ, int H, int W, int i0, int j0,
+__device__ __forceinline__ void build_cspace(SsspScratch &S, const uint8_t *__restrict__ occ, int H, int W, int i0, int j0,
                              int h, int w, int r)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -274,14 +274,28 @@ __device__ void build_cspace(SsspScratch &S, const uint8_t *__restrict__ occ, in
 // ------------------------------------------------------------------------------------------------
 // Phase: snap the query pixels to the closest free cell (scipy EDT feature transform at q)
 // ------------------------------------------------------------------------------------------------
-__device__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc)
+__device__ __forceinline__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc)
 {
     const int tid = threadIdx.x;
     const int h = sh.h, w = sh.w, i0 = sh.i0, j0 = sh.j0;
+    // fast path (the common case): a free query pixel is its own nearest free cell (EDT distance 0)
+    if (tid < nsrc) {
+        const int qr = sh.src_q[tid][0] - i0, qc = sh.src_q[tid][1] - j0;
+        const bool fr = qr >= 0 && qr < h && qc >= 0 && qc < w && b_test(S.freeb[qr], qc);
+        sh.src_ok[tid] = fr;
+        if (fr) {
+            sh.src_s[tid][0] = sh.src_q[tid][0];
+            sh.src_s[tid][1] = sh.src_q[tid][1];
+        }
+    }
+    lds_barrier();
+    bool slow = false;
+    for (int s = 0; s < nsrc; s++) slow |= !sh.src_ok[s];
+    if (!slow) return;
     // pass 1 (scipy: per column along axis 0): nearest free row of each rect column, ties low
     for (int item = tid; item < nsrc * 128; item += NT) {  // w <= 120 columns per source
         const int s = item >> 7, c = item & 127;
-        if (c >= w) continue;
+        if (c >= w || sh.src_ok[s]) continue;
         const int qi = sh.src_q[s][0];
         int best = -1, bestd = 1 << 30;
         for (int rr = 0; rr < h; rr++) {
@@ -294,16 +308,10 @@ __device__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc)
     }
     lds_barrier();
     // pass 2 (scipy _VoronoiFT along axis 1), one lane per source
-    if ((tid & 63) == 0 && (tid >> 6) < nsrc) {
+    if ((tid & 63) == 0 && (tid >> 6) < nsrc && !sh.src_ok[tid >> 6]) {
         const int s = tid >> 6;
         const int qi = sh.src_q[s][0], qj = sh.src_q[s][1];
-        const int qr = qi - i0, qc = qj - j0;
-        sh.src_ok[s] = 0;
-        if (qr >= 0 && qr < h && qc >= 0 && qc < w && b_test(S.freeb[qr], qc)) {
-            sh.src_s[s][0] = qi;
-            sh.src_s[s][1] = qj;
-            sh.src_ok[s] = 1;
-        } else {
+        {
             int *g = sh.envg[s];  // envelope (indices into rect columns)
             int l = -1;
             for (int c = 0; c < w; c++) {
@@ -396,36 +404,39 @@ struct Group {
 // (straight + 2 diagonals); the previous line's new values stay in registers and reach the
 // neighbouring lanes by DPP wave shifts, so a path that is monotone in the sweep direction is
 // settled in ONE pass.  Rounds of 4 concurrent sweeps repeat until a round changes nothing.
-// Every write is min(current, fl(d_u + w)) for a real edge, i.e. a valid relaxation (plain stores:
-// a racing sweep can only lose an improvement, which re-triggers a round), so the result is the
-// unique float32 fixpoint = the reference SPFA's distances, bit for bit.
-// Layout: dist[s] = (h + 2) x pitch float32, +inf border, pitch = (w + 2) | 1 (odd: column-wise
-// sweeps hit at most 2-way LDS bank conflicts).  Blocked cells stay +inf.
+// Every write is an LDS atomic min(current, fl(d_u + w)) for a real edge -- a valid relaxation
+// that never raises a cell, even when another sweep improved it after this wave prefetched it --
+// so rounds terminate, and a round without any candidate below the prefetched values (which are
+// >= the current ones) proves the fixpoint: the unique float32 fixpoint = the reference SPFA's
+// distances, bit for bit.
+// Layout: dist[s] = (h + 2) x pitch float32 with a border, pitch = (w + 2) | 1 (odd: column-wise
+// sweeps hit at most 2-way LDS bank conflicts).  Free cells start at +inf, blocked and border
+// cells hold -inf: `candidate < cell` is false for them, so they are never written, and the value
+// a lane passes on to the next line, |min(candidate, cell)|, is +inf for them (propagates nothing;
+// the fabs is a free source modifier of the consumers).  No NaN anywhere, no free-bit tests.
 
-__device__ __forceinline__ float from_prev_lane(float v)  // lane i <- lane i-1 (lane 0 <- +inf)
+// Rotations (no invalid source lanes, no `old` operand): lane 0 / lane 63 receive lane 63 / lane 0,
+// which never own a cell (spans are <= 63 cells for 1 cell per lane, <= 120 for 2), so they carry
+// +inf.
+__device__ __forceinline__ float from_prev_lane(float v)  // lane i <- lane i-1
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp((int)INF_BITS, __float_as_int(v), 0x138, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x13c, 0xf, 0xf, false));  // wave_ror:1
 }
-__device__ __forceinline__ float from_next_lane(float v)  // lane i <- lane i+1 (lane 63 <- +inf)
+__device__ __forceinline__ float from_next_lane(float v)  // lane i <- lane i+1
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp((int)INF_BITS, __float_as_int(v), 0x130, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x134, 0xf, 0xf, false));  // wave_rol:1
 }
 
 __device__ __forceinline__ int sssp_pitch(int w) { return (w + 2) | 1; }
 
-// One sweep of one wave.  DIR: 0 down, 1 up (lines = rows), 2 right, 3 left (lines = columns);
-// CPL: cells per lane across the line (1: span <= 64, 2: span <= 128).  Returns true if a lane
-// found an improvement.
-// Blocked and padding cells hold a quiet NaN: every comparison with NaN is false, so a blocked cell
-// is never written and its NaN never wins a min (v_min3 drops NaN operands) -- no free-bit tests.
-// Improvements are LDS atomic float mins: a cell's value never increases, even when another
-// sweep improved it after this wave prefetched it, so rounds terminate and the last round (no
-// candidate below the prefetched values, which are >= the current ones) proves the fixpoint.
-// Lines are prefetched P steps ahead into a register ring; lanes past the span read the NaN corner.
-constexpr unsigned QNAN_BITS = 0x7fc00000u;
+constexpr unsigned NINF_BITS = 0xff800000u;  // blocked / border cells
 
 typedef __attribute__((address_space(3))) float lds_float;
 
+// One sweep of one wave.  DIR: 0 down, 1 up (lines = rows), 2 right, 3 left (lines = columns);
+// CPL: cells per lane across the line (1: span <= 63, 2: span <= 120).  Returns true if a lane
+// found an improvement.  Lines are prefetched P steps ahead into a ring of named registers;
+// lanes past the span sit on the -inf corner cell.
 template <int DIR, int CPL>
 __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw)
 {
@@ -435,21 +446,20 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw)
     const int sl = VERT ? pw : 1;             // address stride along the sweep (line to line)
     const int sa = VERT ? 1 : pw;             // across the line (cell 0 -> cell 1 of a lane)
     const int a0 = 1 + CPL * lane;
-    const bool act = a0 <= span;              // cell 1 of the last lane may be the NaN border
+    const bool act = a0 <= span;              // cell 1 of the last lane may be the border
     const int st = act ? (FWD ? sl : -sl) : 0;
     int cur = act ? (FWD ? 1 : len) * sl + a0 * sa : 0;
     int pf = cur;
-    const float QN = __int_as_float(QNAN_BITS);
-    // ring of P prefetched lines in named registers (A..D: lines t, t+1, t+2, t+3 at step t)
-    float A0 = D[pf], A1 = CPL == 2 ? D[pf + sa] : QN; pf += st;
-    float B0 = D[pf], B1 = CPL == 2 ? D[pf + sa] : QN; pf += st;
-    float C0 = D[pf], C1 = CPL == 2 ? D[pf + sa] : QN; pf += st;
-    float E0 = D[pf], E1 = CPL == 2 ? D[pf + sa] : QN; pf += st;
-    float p0 = QN, p1 = QN;
+    const float NI = -INFINITY;
+    float A0 = D[pf], A1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
+    float B0 = D[pf], B1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
+    float C0 = D[pf], C1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
+    float E0 = D[pf], E1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
+    float p0 = INFINITY, p1 = INFINITY;       // the line before the first one: nothing
     bool chg = false;
 #define SWEEP_STEP(R0, R1, LIVE)                                                                        \
     do {                                                                                                \
-        float m0, m1 = QN;                                                                              \
+        float m0, m1 = INFINITY;                                                                        \
         if (CPL == 2) {                                                                                 \
             const float pm = from_prev_lane(p1), pp = from_next_lane(p0);                               \
             m0 = fminf(fminf(p0 + 1.0f, pm + SQRT2F), p1 + SQRT2F);                                     \
@@ -463,9 +473,8 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw)
         if (u0) __hip_atomic_fetch_min(&D[cur], m0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);    \
         if (u1) __hip_atomic_fetch_min(&D[cur + sa], m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
         chg |= u0 | u1;                                                                                 \
-        /* p = u ? m : R, branch-free: NaN (blocked) R propagates, NaN m (no live predecessor) drops */ \
-        p0 = __builtin_elementwise_minimum(R0, fminf(m0, INFINITY));                                   \
-        if (CPL == 2) p1 = __builtin_elementwise_minimum(R1, fminf(m1, INFINITY));                     \
+        p0 = fabsf(__builtin_elementwise_minimum(m0, R0));                                              \
+        if (CPL == 2) p1 = fabsf(__builtin_elementwise_minimum(m1, R1));                                \
         R0 = D[pf];                                                                                     \
         if (CPL == 2) R1 = D[pf + sa];                                                                  \
         cur += st;                                                                                      \
@@ -487,7 +496,7 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw)
     return __ballot(chg) != 0;
 }
 
-__device__ bool sweep(float *Dg, int h, int w, int pw, int dir_in)
+__device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_in)
 {
     lds_float *D = (lds_float *)Dg;  // the distance arrays live in LDS: keep ds_* addressing
     // wave-uniform loop bounds: scalar loop control, no exec-mask merges at the back edge
@@ -496,20 +505,20 @@ __device__ bool sweep(float *Dg, int h, int w, int pw, int dir_in)
     w = __builtin_amdgcn_readfirstlane(w);
     pw = __builtin_amdgcn_readfirstlane(pw);
     switch (dir) {
-    case 0: return w <= 64 ? sweep_t<0, 1>(D, h, w, pw) : sweep_t<0, 2>(D, h, w, pw);
-    case 1: return w <= 64 ? sweep_t<1, 1>(D, h, w, pw) : sweep_t<1, 2>(D, h, w, pw);
-    case 2: return h <= 64 ? sweep_t<2, 1>(D, w, h, pw) : sweep_t<2, 2>(D, w, h, pw);
-    default: return h <= 64 ? sweep_t<3, 1>(D, w, h, pw) : sweep_t<3, 2>(D, w, h, pw);
+    case 0: return w <= 63 ? sweep_t<0, 1>(D, h, w, pw) : sweep_t<0, 2>(D, h, w, pw);
+    case 1: return w <= 63 ? sweep_t<1, 1>(D, h, w, pw) : sweep_t<1, 2>(D, h, w, pw);
+    case 2: return h <= 63 ? sweep_t<2, 1>(D, w, h, pw) : sweep_t<2, 2>(D, w, h, pw);
+    default: return h <= 63 ? sweep_t<3, 1>(D, w, h, pw) : sweep_t<3, 2>(D, w, h, pw);
     }
 }
 
-// all threads: free cells +inf, blocked / padding NaN, sources 0
-__device__ void sssp_init(Shared &sh, const SsspScratch &S, float *dist, int nsrc)
+// all threads: free cells +inf, blocked / border -inf, sources 0
+__device__ __forceinline__ void sssp_init(Shared &sh, const SsspScratch &S, float *dist, int nsrc)
 {
     const int tid = threadIdx.x;
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
     const int cells = (h + 2) * pw;
-    const float QN = __int_as_float(QNAN_BITS);
+    const float NI = -INFINITY;
     // (row, column) walk instead of k / pitch: integer division by a runtime value costs ~40 ops
     for (int s = 0; s < nsrc; s++) {
         float *D = dist + s * DIST_FLOATS;
@@ -517,10 +526,10 @@ __device__ void sssp_init(Shared &sh, const SsspScratch &S, float *dist, int nsr
             const B128 fb = (rr >= 1 && rr <= h) ? S.freeb[rr - 1] : B128{0, 0};
             for (int c = tid & 127; c < pw; c += 128) {
                 const bool fr = c >= 1 && c <= w && b_test(fb, c - 1);
-                D[rr * pw + c] = fr ? INFINITY : QN;
+                D[rr * pw + c] = fr ? INFINITY : NI;
             }
         }
-        for (int k = cells + tid; k < DIST_FLOATS; k += NT) D[k] = QN;
+        for (int k = cells + tid; k < DIST_FLOATS; k += NT) D[k] = NI;
     }
     if (tid < 3) sh.changed[tid] = 0;
     if (tid < 8) (&sh.bar[0][0])[tid] = 0u;
@@ -531,7 +540,7 @@ __device__ void sssp_init(Shared &sh, const SsspScratch &S, float *dist, int nsr
 }
 
 // the sweep group (waves 0 .. 4*nsrc-1): rounds of concurrent sweeps until one changes nothing
-__device__ void sssp_rounds(Shared &sh, float *dist, int nsrc, const Group &g)
+__device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, const Group &g)
 {
     const int tid = threadIdx.x, wave = tid >> 6;
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
@@ -549,44 +558,44 @@ __device__ void sssp_rounds(Shared &sh, float *dist, int nsrc, const Group &g)
     }
 }
 
-// all threads: NaN (blocked) -> +inf; max reachable distance per source
-__device__ void sssp_finish(Shared &sh, float *dist, int nsrc)
+// group g: -inf (blocked) -> +inf; max reachable distance per source (sh.dmax, visible after the
+// next workgroup barrier)
+__device__ __forceinline__ void sssp_finish(Shared &sh, float *dist, int nsrc, const Group &g)
 {
-    const int tid = threadIdx.x;
     const int cells = (sh.h + 2) * sssp_pitch(sh.w);
     for (int s = 0; s < nsrc; s++) {
         float m = -1.0f;
-        for (int q = tid; q < cells; q += NT) {
+        for (int q = g.t; q < cells; q += g.n) {
             float &d = dist[s * DIST_FLOATS + q];
-            if (d != d) d = INFINITY;
+            if (d == -INFINITY) d = INFINITY;
             else if (d != INFINITY) m = fmaxf(m, d);
         }
         m = wave_max(m);
-        if ((tid & 63) == 0) sh.red[0][tid >> 6] = m;
-        lds_barrier();
-        if (tid == 0) {
-            float mm = sh.red[0][0];
-            for (int k = 1; k < NT / 64; k++) mm = fmaxf(mm, sh.red[0][k]);
-            sh.dmax[s] = mm;
-        }
-        lds_barrier();
+        if ((g.t & 63) == 0) sh.red[s][g.t >> 6] = m;
+    }
+    g.sync();
+    if (g.t < nsrc) {
+        float mm = sh.red[g.t][0];
+        for (int k = 1; k < g.nw; k++) mm = fmaxf(mm, sh.red[g.t][k]);
+        sh.dmax[g.t] = mm;
     }
 }
 
-__device__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
+__device__ __forceinline__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
 {
     sssp_init(sh, S, dist, nsrc);
     const int wave = threadIdx.x >> 6;
     if (wave < 4 * nsrc) sssp_rounds(sh, dist, nsrc, Group{(int)threadIdx.x, 256 * nsrc, sh.bar[0], 4 * nsrc});
     lds_barrier();
-    sssp_finish(sh, dist, nsrc);
+    sssp_finish(sh, dist, nsrc, Group{(int)threadIdx.x, NT, nullptr, NT / 64});
+    lds_barrier();
 }
 
 // ------------------------------------------------------------------------------------------------
 // Intention / history raster (Mapper._create_global_intention_or_history_map, envs.py:2302-2347)
 // ------------------------------------------------------------------------------------------------
 // enc: SIMAPS_ENC_* or 4 = history (ramp over the reversed history path)
-__device__ void raster_lines(Shared &sh, float *tile, const simaps_config &cfg, const simaps_robot *rb,
+__device__ __forceinline__ void raster_lines(Shared &sh, float *tile, const simaps_config &cfg, const simaps_robot *rb,
                              const double *__restrict__ paths, int enc, const Group &g)
 {
     const int tid = g.t, lane = threadIdx.x & 63, wave = g.t >> 6, nwaves = g.n >> 6;
@@ -698,8 +707,9 @@ struct RenderCtx {
     int C, n;
     __device__ __forceinline__ void put(int ch, int p, float v) const
     {
-        if (cfg.layout_chw) out[(size_t)ch * LW * LW + p] = v;
-        else out[(size_t)p * C + ch] = v;
+        int idx = cfg.layout_chw ? ch * LW * LW + p : p * C + ch;  // < 96 * 96 * C: 32-bit
+        asm volatile("" : "+v"(idx));  // computed at the store: no per-pixel offsets hoisted across passes
+        out[idx] = v;
     }
     // global pixel sampled by output pixel p (Mapper._get_local_map, envs.py:2200-2211), packed
     // gi << 16 | gj, or -1 where the scipy rotate falls outside the crop (cval 0)
@@ -714,9 +724,44 @@ struct RenderCtx {
     }
 };
 
+// Mapper._get_intention_channels (envs.py:2349-2378), the per-agent part: robots ordered by
+// distance (np.argsort -> stable insertion sort) and the nonspatial (dist * sin, dist * cos) pairs.
+// One thread, in the params phase (fp64 libm calls need registers the render phase does not have).
+__device__ __forceinline__ void intention_channel_order(Shared &sh, const simaps_config &cfg, const simaps_robot *rb)
+{
+    const int nr = sh.nr;
+    double dd[SIMAPS_MAX_ROBOTS];
+    const RobotP &M = sh.rob[sh.me];
+    for (int q = 0; q < nr; q++) {
+        const double dx = sh.rob[q].x - M.x, dy = sh.rob[q].y - M.y;
+        dd[q] = sqrt(dx * dx + dy * dy);
+        int j = q;
+        while (j > 0 && dd[sh.order[j - 1]] > dd[q]) { sh.order[j] = sh.order[j - 1]; j--; }
+        sh.order[j] = q;
+    }
+    if (!cfg.intention_channel_spatial) {
+        int c2 = 0;
+        for (int q = 0; q < nr; q++) {
+            const int k = sh.order[q];
+            if (k == sh.me) continue;
+            const RobotP &R = sh.rob[k];
+            double rel0 = 0.0, rel1 = 0.0;
+            if (!R.idle) {
+                const double dx = R.tx - M.x, dy = R.ty - M.y;
+                const double dist_t = sqrt(dx * dx + dy * dy);
+                const double th = rb[sh.me].heading - atan2(R.ty - M.y, R.tx - M.x);
+                rel0 = dist_t * sin(th);
+                rel1 = dist_t * cos(th);
+            }
+            sh.nonsp[c2++] = (float)(cfg.intention_channel_nonspatial_scale * rel0);
+            sh.nonsp[c2++] = (float)(cfg.intention_channel_nonspatial_scale * rel1);
+        }
+    }
+}
+
 // Channels that do not need the shortest-path maps, rendered by group g:
 // overhead (0), robot (1), history / intention maps, baseline intention channels.
-__device__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry &geo, const float *__restrict__ ovh,
+__device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry &geo, const float *__restrict__ ovh,
                             const simaps_robot *rb, const double *__restrict__ paths, float *tile)
 {
     const simaps_config &cfg = rc.cfg;
@@ -751,27 +796,45 @@ __device__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry 
         if (bits) atomicOr(&rmap[a * CROP + b], bits);
     }
     g.sync();
-    for (int base = g.t; base < NP; base += 9 * g.n) {
-        int gp[9];
-        float ovv[9];
+    // the sample index of each of this thread's output pixels, computed once (fp64 scipy rule) and
+    // reused by every channel of the group, then handed to the distance phase through LDS
+    constexpr int MAXPG = 18;  // output pixels per render thread (>= 8 render waves)
+    // packed 2 per register: crop-relative (row << 8 | col), 0xffff = outside (cval)
+    uint32_t gqp[MAXPG / 2];
 #pragma unroll
-        for (int k = 0; k < 9; k++) {
-            const int p = base + k * g.n;
-            gp[k] = p < NP ? rc.gpix(p) : -1;
+    for (int k = 0; k < MAXPG; k++) {
+        const int p = g.t + k * g.n;
+        const int q = p < NP ? rc.gpix(p) : -1;
+        const uint32_t v = q >= 0 ? (uint32_t)((((q >> 16) - ci0) << 8) | ((q & 0xffff) - cj0)) : 0xffffu;
+        if (k & 1) gqp[k >> 1] |= v << 16;
+        else gqp[k >> 1] = v;
+        __builtin_amdgcn_sched_barrier(0);  // one fp64 index computation at a time (VGPR pressure)
+    }
+    // global (gi << 16 | gj) of pixel slot k, or -1
+    auto gq_at = [&](int k) -> int {
+        const uint32_t v = (gqp[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
+        return v == 0xffffu ? -1 : ((ci0 + (int)(v >> 8)) << 16) | (cj0 + (int)(v & 0xffu));
+    };
+#pragma unroll
+    for (int half = 0; half < MAXPG / 6; half++) {
+        float ovv[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int q = gq_at(half * 6 + k);
 #ifdef SIMAPS_ABL_NOGATHER
             ovv[k] = 0.25f;
-            asm volatile("" ::"v"(gp[k]));
+            asm volatile("" ::"v"(q));
 #else
-            ovv[k] = gp[k] >= 0 ? ovh[(size_t)(gp[k] >> 16) * W + (gp[k] & 0xffff)] : 0.0f;
+            ovv[k] = q >= 0 ? ovh[(size_t)(q >> 16) * W + (q & 0xffff)] : 0.0f;
 #endif
         }
 #pragma unroll
-        for (int k = 0; k < 9; k++) {
-            const int p = base + k * g.n;
+        for (int k = 0; k < 6; k++) {
+            const int p = g.t + (half * 6 + k) * g.n, q = gq_at(half * 6 + k);
             if (p >= NP) break;
             float vseg = 0.0f, vrob = 0.0f, vov = 0.0f;
-            if (gp[k] >= 0) {
-                const unsigned m = rmap[((gp[k] >> 16) - ci0) * CROP + (gp[k] & 0xffff) - cj0];
+            if (q >= 0) {
+                const unsigned m = rmap[((q >> 16) - ci0) * CROP + (q & 0xffff) - cj0];
                 const unsigned ms = m & 0x1ffu, mr = m >> 16;
                 vseg = ms ? (float)(31 - __builtin_clz(ms)) * 0.125f : 0.0f;
                 vrob = (mr & 2u) ? 1.0f : ((mr & 1u) ? 0.5f : 0.0f);
@@ -797,46 +860,16 @@ __device__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry 
         if (!on) continue;
         raster_lines(sh, tile, cfg, rb, paths, pass == 0 ? 4 : cfg.intention_map_encoding, g);
         if (g.t == 0) STAMP_NB(12);
-        for (int p = g.t; p < NP; p += g.n) {
-            const int gq = rc.gpix(p);
-            rc.put(ch, p, gq >= 0 ? tile_sample(tile, thick, gq >> 16, gq & 0xffff, sh.pi, sh.pj) : 0.0f);
+#pragma unroll
+        for (int k = 0; k < MAXPG; k++) {
+            const int p = g.t + k * g.n, q = gq_at(k);
+            if (p < NP) rc.put(ch, p, q >= 0 ? tile_sample(tile, thick, q >> 16, q & 0xffff, sh.pi, sh.pj) : 0.0f);
         }
         ch++;
         g.sync();
     }
     // baseline intention channels (Mapper._get_intention_channels, envs.py:2349-2378)
-    if (cfg.use_intention_channels) {
-        if (g.t == 0) {
-            // np.argsort of distances (insertion sort for n <= 16 -> stable)
-            double dd[SIMAPS_MAX_ROBOTS];
-            const RobotP &M = sh.rob[sh.me];
-            for (int q = 0; q < nr; q++) {
-                const double dx = sh.rob[q].x - M.x, dy = sh.rob[q].y - M.y;
-                dd[q] = sqrt(dx * dx + dy * dy);
-                int j = q;
-                while (j > 0 && dd[sh.order[j - 1]] > dd[q]) { sh.order[j] = sh.order[j - 1]; j--; }
-                sh.order[j] = q;
-            }
-            if (!cfg.intention_channel_spatial) {
-                int c2 = 0;
-                for (int q = 0; q < nr; q++) {
-                    const int k = sh.order[q];
-                    if (k == sh.me) continue;
-                    const RobotP &R = sh.rob[k];
-                    double rel0 = 0.0, rel1 = 0.0;
-                    if (!R.idle) {
-                        const double dx = R.tx - M.x, dy = R.ty - M.y;
-                        const double dist_t = sqrt(dx * dx + dy * dy);
-                        const double th = rb[sh.me].heading - atan2(R.ty - M.y, R.tx - M.x);
-                        rel0 = dist_t * sin(th);
-                        rel1 = dist_t * cos(th);
-                    }
-                    sh.nonsp[c2++] = (float)(cfg.intention_channel_nonspatial_scale * rel0);
-                    sh.nonsp[c2++] = (float)(cfg.intention_channel_nonspatial_scale * rel1);
-                }
-            }
-        }
-        g.sync();
+    if (cfg.use_intention_channels) {  // sh.order / sh.nonsp: intention_channel_order (params phase)
         int c2 = 0;
         const float scale_f = (float)cfg.intention_map_scale;
         for (int q = 0; q < nr; q++) {
@@ -844,11 +877,13 @@ __device__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry 
             if (kq == sh.me) continue;
             if (cfg.intention_channel_spatial) {
                 const RobotP &R = sh.rob[kq];
-                for (int p = g.t; p < NP; p += g.n) {
-                    const int gq = rc.gpix(p);
+#pragma unroll
+                for (int k = 0; k < MAXPG; k++) {
+                    const int p = g.t + k * g.n, q = gq_at(k);
+                    if (p >= NP) continue;
                     float v = 0.0f;
-                    if (gq >= 0 && !R.idle) {
-                        const int di = abs((gq >> 16) - R.tpi), dj = abs((gq & 0xffff) - R.tpj);
+                    if (q >= 0 && !R.idle) {
+                        const int di = abs((q >> 16) - R.tpi), dj = abs((q & 0xffff) - R.tpj);
                         const bool hit = thick > 1 ? (di + dj <= 1) : (di == 0 && dj == 0);
                         v = hit ? scale_f : 0.0f;
                     }
@@ -861,6 +896,14 @@ __device__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry 
             }
         }
     }
+    // hand the sample indices to the distance phase: crop-relative (row << 8 | col), 0xffff = cval
+    g.sync();  // the tile region is dead
+    uint16_t *tab = reinterpret_cast<uint16_t *>(tile);
+#pragma unroll
+    for (int k = 0; k < MAXPG; k++) {
+        const int p = g.t + k * g.n;
+        if (p < NP) tab[p] = (uint16_t)((gqp[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
+    }
 }
 
 constexpr int PPT = (LW * LW) / NT;  // 9 output pixels per thread
@@ -868,7 +911,8 @@ static_assert(PPT * NT == LW * LW, "pixel split");
 
 // Distance channels (all 16 waves): Euclidean map, then shortest-path maps; local -= local.min()
 // (envs.py:2213-2216), so every value is kept in registers until the block minimum is known.
-__device__ void render_distance_channels(const RenderCtx &rc, const simaps_env &ev, const float *dist, int nsrc)
+__device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, const simaps_env &ev, const float *dist, int nsrc,
+                                         const uint16_t *tab)
 {
     const simaps_config &cfg = rc.cfg;
     Shared &sh = rc.sh;
@@ -877,9 +921,13 @@ __device__ void render_distance_channels(const RenderCtx &rc, const simaps_env &
     const int nd = has_eu + nsrc;
     if (nd == 0) return;
     const int ch = 1 + !!cfg.use_robot_map;
-    int gpix[PPT];
+    int gpix[PPT];  // from the render group's table (render_maps), not recomputed
+    const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
 #pragma unroll
-    for (int k = 0; k < PPT; k++) gpix[k] = rc.gpix(tid + k * NT);
+    for (int k = 0; k < PPT; k++) {
+        const unsigned v = tab[tid + k * NT];
+        gpix[k] = v == 0xffffu ? -1 : ((ci0 + (int)(v >> 8)) << 16) | (cj0 + (int)(v & 0xffu));
+    }
     float vals[3][PPT];
     float mins[3];
     const float sps = (float)cfg.shortest_path_map_scale;
@@ -916,10 +964,14 @@ __device__ void render_distance_channels(const RenderCtx &rc, const simaps_env &
     for (int q = 0; q < 3; q++) {
         if (q >= nd) continue;
         const float m = wave_min(mins[q]);
-        if ((tid & 63) == 0) sh.red[q & 1][tid >> 6] = m;
-        lds_barrier();
-        float mm = sh.red[q & 1][0];
-        for (int k = 1; k < NT / 64; k++) mm = fminf(mm, sh.red[q & 1][k]);
+        if ((tid & 63) == 0) sh.red[q][tid >> 6] = m;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        if (q >= nd) continue;
+        float mm = sh.red[q][0];
+        for (int k = 1; k < NT / 64; k++) mm = fminf(mm, sh.red[q][k]);
         mins[q] = mm;
     }
 #pragma unroll
@@ -1012,6 +1064,8 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     }
     lds_barrier();
 
+    if (cfg.use_intention_channels && tid == 256) intention_channel_order(sh, cfg, rb);
+
     // ---- rotated robot stamps (Mapper._create_global_robot_map, envs.py:2251-2276): each robot's
     // scipy-rotated mask, evaluated once per workgroup into a <= 32 x 32 bit tile at its global box.
     // The 5 host-computed mask windows are staged in the (still unused) union region first.
@@ -1067,7 +1121,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
 #ifdef SIMAPS_SWEEP_PRIO
         __builtin_amdgcn_s_setprio(SIMAPS_SWEEP_PRIO);
 #endif
-        sssp_rounds(sh, dist, nsrc, Group{tid, 64 * sweep_waves, sh.bar[0], sweep_waves});
+        const Group g{tid, 64 * sweep_waves, sh.bar[0], sweep_waves};
+        sssp_rounds(sh, dist, nsrc, g);
+        sssp_finish(sh, dist, nsrc, g);  // while the render waves finish
 #ifdef SIMAPS_SWEEP_PRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1084,9 +1140,8 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     STAMP(4);
 
     // ---- all waves: distance channels (need the converged sweeps)
-    if (nsrc > 0) sssp_finish(sh, dist, nsrc);
     STAMP(5);
-    render_distance_channels(rc, ev, dist, nsrc);
+    render_distance_channels(rc, ev, dist, nsrc, reinterpret_cast<const uint16_t *>(tile));
     STAMP(6);
 
     // ---- debug outputs
