@@ -184,6 +184,8 @@ constexpr int OFF_UNION = OFF_DIST + align16(2 * DIST_FLOATS * 4);
 constexpr int TILE_BYTES = TILE * TILE * 4;
 constexpr int UNION_BYTES = align16((int)sizeof(SsspScratch) > TILE_BYTES ? (int)sizeof(SsspScratch) : TILE_BYTES);
 constexpr int LDS_BYTES = OFF_UNION + UNION_BYTES;
+constexpr int RMAP_BYTES = align16(CROP * CROP);  // u8 robot-code map over the crop (render_maps)
+static_assert(RMAP_BYTES + 4 * LW * 8 <= UNION_BYTES, "robot map + rotation tables fit the union");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 
 // ------------------------------------------------------------------------------------------------
@@ -203,48 +205,54 @@ __device__ __forceinline__ float wave_max(float v)
 // ------------------------------------------------------------------------------------------------
 // Phase: occupancy window -> free-cell bit rows (cspace inside the room rect)
 // ------------------------------------------------------------------------------------------------
-// occ: the agent's occupancy map [H, W] (nonzero = obstacle).  r = disk radius.
-__device__ __forceinline__ void build_cspace(SsspScratch &S, const uint8_t *__restrict__ occ, int H, int W, int i0, int j0,
-                             int h, int w, int r)
+// occ: the agent's occupancy map [H, W] (nonzero = obstacle).  r = disk radius (<= RMAX).
+// The window loads are issued at kernel start (cspace_load, for the largest radius, so they do not
+// wait for the robot descriptor) and land in registers while the params phase runs.
+constexpr int RMAX = 7;  // floor(RADIUS * 96) <= 6 for every robot class (envs.py:2421)
+struct OccLoad {
+    uint8_t v[16], v2;
+};
+__device__ __forceinline__ void cspace_load(OccLoad &L, const uint8_t *__restrict__ occ, int H, int W, int i0, int j0,
+                                            int h, int w)
+{
+    const int tid = threadIdx.x;
+    const int wh = h + 2 * RMAX, ww = w + 2 * RMAX;  // <= 126 x 134
+    const int c = tid & 127, r0 = tid >> 7;          // thread -> (row r0 + 8q, column c [+ 128])
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int rr = r0 + 8 * q, gi = i0 - RMAX + rr, gj = j0 - RMAX + c;
+        L.v[q] = (rr < wh && c < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
+    }
+    {   // columns 128..133 of the widest window
+        const int rr = tid / 6, cc = 128 + tid % 6, gi = i0 - RMAX + rr, gj = j0 - RMAX + cc;
+        L.v2 = (rr < wh && cc < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
+    }
+}
+
+__device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad &L, int h, int w, int r)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wh = h + 2 * r, ww = w + 2 * r;
+    const int whM = h + 2 * RMAX, wwM = w + 2 * RMAX, o = RMAX - r;
     const int nwords = (ww + 63) >> 6;
-    // (a) every window byte loaded by one thread, all loads in flight together (<= 14 per thread),
-    //     staged as bytes in LDS (the raster-tile region, free until the render), then
+    // (a) the loaded window bytes -> LDS stage (the raster-tile region, free until the render), then
     // (b) window rows -> bit rows: one wave ballot per 64 columns, from LDS.
     uint8_t *stage = reinterpret_cast<uint8_t *>(S.blocked) + sizeof(S.blocked) + sizeof(S.freeb) + 64;
-    {   // thread -> (row = tid / 128 + 8q, col = tid % 128 [+ 128]): ww <= 132, wh <= 124
-        constexpr int MAXLD = 16;
-        uint8_t v[MAXLD], v2[2];
+    {
         const int c = tid & 127, r0 = tid >> 7;
 #pragma unroll
-        for (int q = 0; q < MAXLD; q++) {
-            const int rr = r0 + 8 * q, gi = i0 - r + rr, gj = j0 - r + c;
-            v[q] = (rr < wh && c < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
-        }
-        // columns 128..131 of the widest window
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const int k = tid + q * NT, rr = k >> 2, cc = 128 + (k & 3), gi = i0 - r + rr, gj = j0 - r + cc;
-            v2[q] = (rr < wh && cc < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
-        }
-#pragma unroll
-        for (int q = 0; q < MAXLD; q++) {
+        for (int q = 0; q < 16; q++) {
             const int rr = r0 + 8 * q;
-            if (rr < wh && c < ww) stage[rr * ww + c] = v[q];
+            if (rr < whM && c < wwM) stage[rr * wwM + c] = L.v[q];
         }
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const int k = tid + q * NT, rr = k >> 2, cc = 128 + (k & 3);
-            if (rr < wh && cc < ww) stage[rr * ww + cc] = v2[q];
-        }
+        const int rr = tid / 6, cc = 128 + tid % 6;
+        if (rr < whM && cc < wwM) stage[rr * wwM + cc] = L.v2;
     }
     lds_barrier();
     for (int item = wave; item < wh * WIN_WORDS; item += NT / 64) {
         const int wr = item / WIN_WORDS, wd = item % WIN_WORDS;
         const int x = wd * 64 + lane;
-        const bool ob = wd < nwords && x < ww && stage[wr * ww + x] != 0;
+        const bool ob = wd < nwords && x < ww && stage[(wr + o) * wwM + x + o] != 0;
         const uint64_t m = __ballot(ob);
         if (lane == 0) S.win[wr][wd] = m;
     }
@@ -517,7 +525,6 @@ __device__ __forceinline__ void sssp_init(Shared &sh, const SsspScratch &S, floa
 {
     const int tid = threadIdx.x;
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
-    const int cells = (h + 2) * pw;
     const float NI = -INFINITY;
     // (row, column) walk instead of k / pitch: integer division by a runtime value costs ~40 ops
     for (int s = 0; s < nsrc; s++) {
@@ -529,7 +536,6 @@ __device__ __forceinline__ void sssp_init(Shared &sh, const SsspScratch &S, floa
                 D[rr * pw + c] = fr ? INFINITY : NI;
             }
         }
-        for (int k = cells + tid; k < DIST_FLOATS; k += NT) D[k] = NI;
     }
     if (tid < 3) sh.changed[tid] = 0;
     if (tid < 8) (&sh.bar[0][0])[tid] = 0u;
@@ -713,6 +719,18 @@ struct RenderCtx {
     }
     // global pixel sampled by output pixel p (Mapper._get_local_map, envs.py:2200-2211), packed
     // gi << 16 | gj, or -1 where the scipy rotate falls outside the crop (cval 0)
+    // gpix from the per-agent product tables T (render_maps): the same fp64 operations, 4 products fewer
+    __device__ __forceinline__ int gpix_tab(const double *T, int p) const
+    {
+        const Rot &R = sh.rot;
+        const int a = p / LW, b = p % LW;
+        const double s0 = (T[a] + T[LW + b]) + R.f0;
+        const double s1 = (T[2 * LW + a] + T[3 * LW + b]) + R.f1;
+        const double hi = CROP - 1;
+        if (!(s0 >= 0.0 && s0 <= hi && s1 >= 0.0 && s1 <= hi)) return -1;
+        const int gi = sh.pi - HALF_CROP + (int)floor(s0 + 0.5), gj = sh.pj - HALF_CROP + (int)floor(s1 + 0.5);
+        return (gi >= 0 && gi < cfg.H && gj >= 0 && gj < cfg.W) ? (gi << 16) | gj : -1;
+    }
     __device__ __forceinline__ int gpix(int p) const
     {
         const Rot &R = sh.rot;
@@ -773,27 +791,21 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     // region: bit (g + 5) = seg value (g + 5) / 8 (SEG_VALUES robot_group_{g+1}), bit 16 = 0.5,
     // bit 17 = 1.0 (non-seg values).  A pixel is then one LDS read; the highest bit of each field is
     // the np.maximum over robots of _create_global_robot_map (envs.py:2251-2276).
-    unsigned *rmap = reinterpret_cast<unsigned *>(tile);
+    uint8_t *rmap = reinterpret_cast<uint8_t *>(tile);
+    unsigned *rmapw = reinterpret_cast<unsigned *>(tile);
+    // products of the local rotation (fp64, exactly the terms of rot_src): T[0][a] = o0 * c,
+    // T[1][b] = o1 * s, T[2][a] = o0 * -s, T[3][b] = o1 * c for output row a / column b
+    double *T = reinterpret_cast<double *>(reinterpret_cast<char *>(tile) + RMAP_BYTES);
     const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
     {
         uint4 *z = reinterpret_cast<uint4 *>(rmap);
-        for (int k = g.t; k < CROP * CROP / 4; k += g.n) z[k] = uint4{0u, 0u, 0u, 0u};
-    }
-    g.sync();
-    for (int item = g.t; item < nr * 1024; item += g.n) {
-        const int q = item >> 10, bi = (item >> 5) & 31, bj = item & 31;
-        const RobotP &P = sh.rob[q];
-        if (bi > P.bi1 - P.bi0 || bj > P.bj1 - P.bj0) continue;
-        const int a = P.bi0 + bi - ci0, b = P.bj0 + bj - cj0;
-        if (a < 0 || a >= CROP || b < 0 || b >= CROP) continue;
-        unsigned bits = 0;
-        if ((P.sbits[0][bi] >> bj) & 1u) {
-            bits |= 1u << (P.group + 5);
-            if (P.type != SIMAPS_LIFTING) bits |= 1u << 17;
-            else if (!P.lifting) bits |= 1u << 16;
+        for (int k = g.t; k < RMAP_BYTES / 16; k += g.n) z[k] = uint4{0u, 0u, 0u, 0u};
+        const Rot &R = sh.rot;
+        for (int k = g.t; k < 4 * LW; k += g.n) {
+            const int which = k / LW, i = k % LW;
+            const double o = (which & 1) ? (double)(i + R.S1 / 2 - LW / 2) : (double)(i + R.S0 / 2 - LW / 2);
+            T[k] = which == 0 ? o * R.c : which == 1 ? o * R.s : which == 2 ? o * (-R.s) : o * R.c;
         }
-        if ((P.sbits[1][bi] >> bj) & 1u) bits |= 1u << 17;  // lifted-cube mask, value 1.0
-        if (bits) atomicOr(&rmap[a * CROP + b], bits);
     }
     g.sync();
     // the sample index of each of this thread's output pixels, computed once (fp64 scipy rule) and
@@ -804,49 +816,61 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
         const int p = g.t + k * g.n;
-        const int q = p < NP ? rc.gpix(p) : -1;
+        const int q = p < NP ? rc.gpix_tab(T, p) : -1;
         const uint32_t v = q >= 0 ? (uint32_t)((((q >> 16) - ci0) << 8) | ((q & 0xffff) - cj0)) : 0xffffu;
         if (k & 1) gqp[k >> 1] |= v << 16;
         else gqp[k >> 1] = v;
-        __builtin_amdgcn_sched_barrier(0);  // one fp64 index computation at a time (VGPR pressure)
     }
     // global (gi << 16 | gj) of pixel slot k, or -1
     auto gq_at = [&](int k) -> int {
         const uint32_t v = (gqp[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
         return v == 0xffffu ? -1 : ((ci0 + (int)(v >> 8)) << 16) | (cj0 + (int)(v & 0xffu));
     };
+    // every overhead gather of the thread in flight at once; the robot map is built meanwhile
+    float ovv[MAXPG];
 #pragma unroll
-    for (int half = 0; half < MAXPG / 6; half++) {
-        float ovv[6];
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-            const int q = gq_at(half * 6 + k);
-#ifdef SIMAPS_ABL_NOGATHER
-            ovv[k] = 0.25f;
-            asm volatile("" ::"v"(q));
-#else
-            ovv[k] = q >= 0 ? ovh[(size_t)(q >> 16) * W + (q & 0xffff)] : 0.0f;
+    for (int k = 0; k < MAXPG; k++) {
+        const int q = gq_at(k);
+        ovv[k] = q >= 0 ? ovh[(size_t)(q >> 16) * W + (q & 0xffff)] : 0.0f;
+    }
+#ifdef SIMAPS_PHASE_STAMPS
+    if (g.t == 0) {
+        asm volatile("" ::"v"(gqp[0]), "v"(gqp[8]));
+        STAMP_NB(14);
+    }
 #endif
+    for (int item = g.t; item < nr * 1024; item += g.n) {
+        const int q = item >> 10, bi = (item >> 5) & 31, bj = item & 31;
+        const RobotP &P = sh.rob[q];
+        if (bi > P.bi1 - P.bi0 || bj > P.bj1 - P.bj0) continue;
+        const int a = P.bi0 + bi - ci0, b = P.bj0 + bj - cj0;
+        if (a < 0 || a >= CROP || b < 0 || b >= CROP) continue;
+        unsigned bits = 0;  // byte code: bit g = seg value (g + 5) / 8, bit 4 = 0.5, bit 5 = 1.0
+        if ((P.sbits[0][bi] >> bj) & 1u) {
+            bits |= 1u << P.group;
+            if (P.type != SIMAPS_LIFTING) bits |= 1u << 5;
+            else if (!P.lifting) bits |= 1u << 4;
         }
+        if ((P.sbits[1][bi] >> bj) & 1u) bits |= 1u << 5;  // lifted-cube mask, value 1.0
+        const int idx = a * CROP + b;
+        if (bits) atomicOr(&rmapw[idx >> 2], bits << (8 * (idx & 3)));
+    }
+    g.sync();
+    if (g.t == 0) STAMP_NB(13);
 #pragma unroll
-        for (int k = 0; k < 6; k++) {
-            const int p = g.t + (half * 6 + k) * g.n, q = gq_at(half * 6 + k);
-            if (p >= NP) break;
-            float vseg = 0.0f, vrob = 0.0f, vov = 0.0f;
-            if (q >= 0) {
-                const unsigned m = rmap[((q >> 16) - ci0) * CROP + (q & 0xffff) - cj0];
-                const unsigned ms = m & 0x1ffu, mr = m >> 16;
-                vseg = ms ? (float)(31 - __builtin_clz(ms)) * 0.125f : 0.0f;
-                vrob = (mr & 2u) ? 1.0f : ((mr & 1u) ? 0.5f : 0.0f);
-                vov = vseg > 0.0f ? vseg : ovv[k];
-            }
-#ifdef SIMAPS_ABL_NOSTORE
-            asm volatile("" ::"v"(vov), "v"(vrob));
-#else
-            rc.put(0, p, vov);
-            if (cfg.use_robot_map) rc.put(1, p, vrob);
-#endif
+    for (int k = 0; k < MAXPG; k++) {
+        const int p = g.t + k * g.n, q = gq_at(k);
+        if (p >= NP) break;
+        float vseg = 0.0f, vrob = 0.0f, vov = 0.0f;
+        if (q >= 0) {
+            const unsigned m = rmap[((q >> 16) - ci0) * CROP + (q & 0xffff) - cj0];
+            const unsigned ms = m & 0xfu, mr = m >> 4;
+            vseg = ms ? (float)(31 - __builtin_clz(ms) + 5) * 0.125f : 0.0f;
+            vrob = (mr & 2u) ? 1.0f : ((mr & 1u) ? 0.5f : 0.0f);
+            vov = vseg > 0.0f ? vseg : ovv[k];
         }
+        rc.put(0, p, vov);
+        if (cfg.use_robot_map) rc.put(1, p, vrob);
     }
     g.sync();  // the raster below reuses the robot-map region
     if (g.t == 0) STAMP_NB(11);
@@ -997,6 +1021,12 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const int tid = threadIdx.x;
     const int H = cfg.H, W = cfg.W;
     const simaps_agent ag = agents[n];
+    // the occupancy window loads first: they depend on the map slot only
+    const bool need_cspace = cfg.use_shortest_path_to_receptacle_map || cfg.use_shortest_path_map || dbg.cspace;
+    OccLoad occ_regs;
+    if (need_cspace)
+        cspace_load(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
+                    cfg.room_w);
     const simaps_env ev = envs[ag.env];
     const simaps_robot *rb = robots + ev.robot_off;
     STAMP(0);
@@ -1097,8 +1127,8 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     // ---- cspace + snap (all waves)
     STAMP(1);
     const int nsrc = sh.nsrc;
-    if (nsrc > 0 || dbg.cspace) {
-        build_cspace(S, occupancy + (size_t)ag.map_slot * H * W, H, W, sh.i0, sh.j0, sh.h, sh.w, sh.r);
+    if (need_cspace) {
+        build_cspace(S, occ_regs, sh.h, sh.w, sh.r);
         if (dbg.cspace) {
             for (int k = tid; k < sh.h * sh.w; k += NT)
                 dbg.cspace[(size_t)n * sh.h * sh.w + k] = b_test(S.freeb[k / sh.w], k % sh.w) ? 1 : 0;
@@ -1131,6 +1161,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     } else {
         const int nw = NT / 64 - sweep_waves;
         const Group g{tid - 64 * sweep_waves, 64 * nw, sweep_waves ? sh.bar[1] : nullptr, nw};
+#ifdef SIMAPS_RENDER_PRIO
+        __builtin_amdgcn_s_setprio(SIMAPS_RENDER_PRIO);
+#endif
 #ifndef SIMAPS_ABL_NORENDER  // diagnostic: sweeps alone (output channels 0.. left unwritten)
         render_maps(rc, g, geo, overhead + (size_t)ag.map_slot * H * W, rb, paths, tile);
 #endif
@@ -1335,6 +1368,9 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
                      float *state, int num_robots_per_env, const simaps_debug *dbg, void *stream)
 {
     int rc = check_cfg(cfg);
+    const Geometry geo = make_geometry();
+    for (int t = 0; t < 4; t++)
+        if (geo.cspace_r[t] > RMAX) return fail(SIMAPS_EUNSUPPORTED, "cspace radius %d > %d", geo.cspace_r[t], RMAX);
     if (rc) return rc;
     if (N < 0) return fail(SIMAPS_EINVAL, "N < 0");
     if (N == 0) return 0;
@@ -1346,7 +1382,7 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
     simaps_debug d;
     memset(&d, 0, sizeof(d));
     if (dbg) d = *dbg;
-    hipLaunchKernelGGL(get_state_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, make_geometry(), agents, envs,
+    hipLaunchKernelGGL(get_state_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, geo, agents, envs,
                        robots, paths, occupancy, overhead, state, C, d);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "get_state launch: %s", hipGetErrorString(e));

@@ -163,3 +163,25 @@ def test_sssp_grid_random(S):
         src = torch.tensor([tuple(int(x) for x in g['rand_src_%d' % q])], dtype=torch.int32)
         out = batch.sssp_grid(torch.from_numpy(grid[None].copy()).cuda(), src).cpu().numpy()
         assert _bitwise(out[0], g['rand_img_%d' % q]), q
+
+
+@pytest.mark.parametrize('mode', ['random', 'eighths_and_negzero'])
+def test_overhead_values_outside_seg_codes(S, mode):
+    """The overhead crop is staged in LDS as k/8 byte codes (every SEG_VALUES entry); any other
+    value must switch that agent to the exact HBM gather path."""
+    batch, K, synthetic = S
+    rs = np.random.RandomState(11)
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 900 + e) for e in range(4)]
+    for e, s in enumerate(scenes):
+        ov = s['overhead']
+        if e % 2 == 0:   # envs 0, 2: perturbed; envs 1, 3 stay on the code path
+            if mode == 'random':
+                ov[:, 60:120, 60:160] = rs.rand(ov.shape[0], 60, 100).astype(np.float32)
+            else:
+                ov[:, 70:110, 70:150] = np.float32(7 / 8)    # a code no seg value of this scene uses
+                ov[:, 90, 100] = np.float32(-0.0)             # -0.0 is not the code 0
+                ov[:, 95, 101] = np.float32(0.3)              # not a multiple of 1/8
+    b = batch.StateBatch(scenes)
+    st = b.as_hwc(b.render()).cpu().numpy()
+    for n, (e, a) in enumerate(b.agents):
+        assert _bitwise(st[n], O.agent_state(scenes[e], a))

@@ -48,6 +48,9 @@ def main():
            'span_us': float((t[:, 6].max() - t[:, 0].min()) / 100.0),
            'split_groups_us': {'sweeps_median': float(np.median(sweeps)), 'render_maps_median': float(np.median(maps)),
                                'maps_ch01': float(np.median((st[:, 11] - st[:, 3]) / 100.0)),
+                               'ch01_tables_sampleidx_issue': float(np.median((st[:, 14] - st[:, 3]) / 100.0)),
+                               'ch01_robotmap': float(np.median((st[:, 13] - st[:, 14]) / 100.0)),
+                               'ch01_consume_store': float(np.median((st[:, 11] - st[:, 13]) / 100.0)),
                                'maps_raster': float(np.median((st[:, 12] - st[:, 11]) / 100.0)),
                                'maps_sample': float(np.median((st[:, 8] - st[:, 12]) / 100.0))},
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())},
