@@ -15,6 +15,9 @@
  *                          VectorEnv.get_state(all_robots=True) (envs.py:322-323) returns.
  *   simaps_sssp_grid    <- GridGraph(grid).shortest_path_image(source)
  *                          (shortest_paths/shortest_paths.pyx:24-67, 69-119, 165-167), batched.
+ *   simaps_sp_distance  <- OccupancyMap.shortest_path_distance (envs.py:2507-2512), i.e. the reward
+ *                          lookup Mapper.distance_to_receptacle (envs.py:2190-2194) used by the
+ *                          partial rewards (envs.py:1083-1088, 1211-1216, 1332-1336), batched.
  *   simaps_robot_mask   <- Mapper._create_robot_mask (envs.py:2218-2242) (host helper).
  *   simaps_num_channels <- the channel list of Mapper.get_state (envs.py:2071-2113).
  */
@@ -142,6 +145,15 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
                      const simaps_robot *robots, const double *paths, const uint8_t *occupancy,
                      const float *overhead, float *state, int num_robots_per_env, const simaps_debug *dbg,
                      void *stream);
+
+/* Batched OccupancyMap.shortest_path_distance(source_position, target_position) / 96 (Python float
+ * semantics: the float32 SPFA distance converted to double, divided by 96.0; unreachable -> -1 / 96):
+ *   on agent n's own map (occupancy slot agents[n].map_slot, its robot class's cspace radius),
+ *   sources [N][2] and targets [N][Q][2] are fp64 (x, y) positions, out [N][Q] fp64, all DEVICE.
+ *   Both ends are snapped to the nearest free cspace cell exactly like the reference (scipy EDT). */
+int simaps_sp_distance(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                       const simaps_robot *robots, const uint8_t *occupancy, const double *sources,
+                       const double *targets, int Q, double *out, void *stream);
 
 /* Batched GridGraph(grid).shortest_path_image(source):
  *   grids [B, H, W] uint8 (nonzero = free), sources [B, 2] int32 (row, col), out dists [B, H, W]

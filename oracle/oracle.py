@@ -290,6 +290,14 @@ class AgentOracle:
             self._sp_cache[src] = spfa_image(self.cspace, src)
         return self._sp_cache[src] / np.float32(PPM)
 
+    def shortest_path_distance(self, source_position, target_position):
+        """OccupancyMap.shortest_path_distance (envs.py:2507-2512): both ends snapped through the EDT
+        indices, dists[target] of the SPFA from the source (pyx:156-163) as a Python float, / 96."""
+        src, tgt = self.snap(source_position), self.snap(target_position)
+        if src not in self._sp_cache:
+            self._sp_cache[src] = spfa_image(self.cspace, src)
+        return float(self._sp_cache[src][tgt]) / PPM
+
     def _sp_global(self, pos):
         g = self.shortest_path_image(pos)
         g[g < 0] = g.max()

@@ -1251,6 +1251,65 @@ __global__ void __launch_bounds__(NT) sssp_grid_kernel(int H, int W, const uint8
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Reward lookups: OccupancyMap.shortest_path_distance (envs.py:2507-2512) from one source position to
+// Q target positions on each agent's own map (Mapper.distance_to_receptacle, envs.py:2190-2194)
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geometry geo,
+                                                         const simaps_agent *__restrict__ agents,
+                                                         const simaps_env *__restrict__ envs,
+                                                         const simaps_robot *__restrict__ robots,
+                                                         const uint8_t *__restrict__ occupancy,
+                                                         const double *__restrict__ sources,
+                                                         const double *__restrict__ targets, int Q,
+                                                         double *__restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    Shared &sh = *reinterpret_cast<Shared *>(smem);
+    float *dist = reinterpret_cast<float *>(smem + OFF_DIST);
+    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
+    const int n = blockIdx.x, tid = threadIdx.x;
+    const int H = cfg.H, W = cfg.W;
+    const simaps_agent ag = agents[n];
+    OccLoad occ_regs;
+    cspace_load(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
+                cfg.room_w);
+    if (tid == 0) {
+        const simaps_env ev = envs[ag.env];
+        sh.h = cfg.room_h;
+        sh.w = cfg.room_w;
+        sh.i0 = cfg.room_i0;
+        sh.j0 = cfg.room_j0;
+        sh.r = geo.cspace_r[robots[ev.robot_off + ag.robot].type];
+        pos_to_pix(sources[2 * n], sources[2 * n + 1], H, W, sh.src_q[0][0], sh.src_q[0][1]);
+        sh.nsrc = 1;
+    }
+    lds_barrier();
+    build_cspace(S, occ_regs, sh.h, sh.w, sh.r);
+    snap_sources(sh, S, 1);
+    const bool src_ok = sh.src_ok[0];
+    sssp(sh, S, dist, 1);  // the source's distance image (GridGraph._spfa_with_cache, pyx:116-119)
+    const int pw = sssp_pitch(sh.w);
+    for (int q0 = 0; q0 < Q; q0 += 2) {  // targets snapped two at a time (snap_sources' slots)
+        const int nq = Q - q0 < 2 ? Q - q0 : 2;
+        if (tid < nq) {
+            const double *t = targets + 2 * ((size_t)n * Q + q0 + tid);
+            pos_to_pix(t[0], t[1], H, W, sh.src_q[tid][0], sh.src_q[tid][1]);
+        }
+        lds_barrier();
+        snap_sources(sh, S, nq);
+        if (tid < nq) {
+            float d = -1.0f;  // dists[target] (pyx:156-163); unreachable -> -1 (pyx:110-112)
+            if (src_ok && sh.src_ok[tid]) {
+                const float v = dist[(sh.src_s[tid][0] - sh.i0 + 1) * pw + (sh.src_s[tid][1] - sh.j0 + 1)];
+                if (v != INFINITY) d = v;
+            }
+            out[(size_t)n * Q + q0 + tid] = (double)d / PPM;  // Python float / LOCAL_MAP_PIXELS_PER_METER
+        }
+        lds_barrier();
+    }
+}
+
 }  // namespace
 
 // =================================================================================================
@@ -1386,6 +1445,24 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
                        robots, paths, occupancy, overhead, state, C, d);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "get_state launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int simaps_sp_distance(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                       const simaps_robot *robots, const uint8_t *occupancy, const double *sources,
+                       const double *targets, int Q, double *out, void *stream)
+{
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (N < 0 || Q < 0) return fail(SIMAPS_EINVAL, "N < 0 or Q < 0");
+    if (N == 0 || Q == 0) return 0;
+    if (!agents || !envs || !robots || !occupancy || !sources || !targets || !out)
+        return fail(SIMAPS_EINVAL, "NULL buffer");
+    const Geometry geo = make_geometry();
+    hipLaunchKernelGGL(sp_distance_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, geo, agents, envs, robots,
+                       occupancy, sources, targets, Q, out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "sp_distance launch: %s", hipGetErrorString(e));
     return 0;
 }
 

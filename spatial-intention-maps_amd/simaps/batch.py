@@ -224,6 +224,25 @@ class StateBatch:
         return out
 
 
+    def shortest_path_distances(self, sources, targets, slots=None, stream=None):
+        """OccupancyMap.shortest_path_distance(source, target) (envs.py:2507-2512) on each agent's own
+        map: sources [n, 2] and targets [n, Q, 2] fp64 (x, y) positions for map slots `slots` (all
+        agents if None) -> [n, Q] float64 device tensor (metres; -1/96 where unreachable)."""
+        agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
+        src = torch.as_tensor(sources, dtype=torch.float64).to(self.device).contiguous()
+        tgt = torch.as_tensor(targets, dtype=torch.float64).to(self.device).contiguous()
+        if tuple(src.shape) != (n, 2) or tgt.dim() != 3 or tgt.shape[0] != n or tgt.shape[2] != 2:
+            raise ValueError('sources must be [%d, 2] and targets [%d, Q, 2]' % (n, n))
+        Q = tgt.shape[1]
+        out = torch.empty((n, Q), dtype=torch.float64, device=self.device)
+        if n == 0 or Q == 0:
+            return out
+        _lib.check(_lib.lib.simaps_sp_distance(
+            self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d), _lib.ptr(self.occupancy),
+            _lib.ptr(src), _lib.ptr(tgt), Q, _lib.ptr(out), _lib.stream_handle(stream)))
+        return out
+
+
 def sssp_grid(grids, sources, window=None, stream=None):
     """Batched GridGraph(grid).shortest_path_image(source) on device.
 

@@ -82,6 +82,28 @@ class VectorEnvObservations:
         return res
 
 
+    # -- reward lookups -----------------------------------------------------
+    def distance_to_receptacle(self, positions, stream=None):
+        """Mapper.distance_to_receptacle with use_shortest_path_partial_rewards (envs.py:2190-2194):
+        positions [E][A][Q] (x, y[, z]) per robot (e.g. the cubes it just moved) -> [E][A] lists of
+        Python floats, each robot's own map, the receptacle as the SPFA source.  One launch."""
+        Qs = [len(p) for pe in positions for p in pe]
+        Q = max(Qs) if Qs else 0
+        n = self.batch.N
+        src = np.zeros((n, 2))
+        tgt = np.zeros((n, max(Q, 1), 2))
+        for (e, a), k in self.slot.items():
+            rec = self.batch.scenes[e]['receptacle_position']
+            if rec is None:
+                raise ValueError('distance_to_receptacle needs a receptacle (not a rescue env)')
+            src[k] = rec[:2]
+            for q, p in enumerate(positions[e][a]):
+                tgt[k, q] = p[:2]
+        d = self.batch.shortest_path_distances(src, tgt[:, :Q], stream=stream).cpu().numpy() if Q else np.zeros((n, 0))
+        return [[[float(x) for x in d[self.slot[(e, a)], :len(positions[e][a])]] for a in range(len(positions[e]))]
+                for e in range(self.num_envs)]
+
+
 class GridGraph:
     """shortest_paths.pyx GridGraph (pyx:10-167) on the device: 8-connected grid over cells with
     grid != 0, weights 1 / float32(sqrt(2)), float32 distances, unreachable -> -1.

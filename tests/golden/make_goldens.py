@@ -287,6 +287,42 @@ def gen_micro(envs, sp):
     print('wrote micro goldens')
 
 
+def gen_sp_distance(envs):
+    """Reward lookups: Mapper.distance_to_receptacle with shortest-path
+    partial rewards (envs.py:2190-2194) = OccupancyMap.shortest_path_distance (envs.py:2507-2512),
+    and shortest_path_distance between arbitrary positions, on each agent's own map."""
+    out = {}
+    rs = np.random.RandomState(777)
+    for cfg in ('lifting_4-small_divider', 'pushing_4-large_empty', 'rescue_4-small_empty'):
+        for e in range(2):
+            scene = synthetic.make_scene(cfg, 40 + e)
+            env = build_env(envs, scene)
+            env.use_shortest_path_partial_rewards = True
+            rw, rl = scene['room_width'], scene['room_length']
+            for a in range(len(scene['robots'])):
+                m = envs.Mapper(env, env.robots[a])
+                H, W = scene['H'], scene['W']
+                X, Y = synthetic.pixel_center_positions(H, W)
+                points = np.stack([X, Y, np.full_like(X, 0.02)], axis=2)
+                seg = np.where(scene['occupancy'][a] == 1, K.SEG_VALUES['obstacle'], K.SEG_VALUES['floor'])
+                m.global_occupancy_map.update(points, seg, K.SEG_VALUES['obstacle'])
+                # queries: uniform in (and slightly beyond) the room, incl. obstacle / wall pixels
+                q = np.stack([rs.uniform(-rl / 2 - 0.05, rl / 2 + 0.05, 24), rs.uniform(-rw / 2 - 0.05, rw / 2 + 0.05, 24)], 1)
+                src = (np.array(scene['robots'][a]['position'][:2]) if scene['receptacle_position'] is None
+                       else np.array(scene['receptacle_position'][:2]))
+                if scene['receptacle_position'] is not None:
+                    d = [m.distance_to_receptacle((float(x), float(y), 0)) for x, y in q]
+                else:
+                    d = [m.global_occupancy_map.shortest_path_distance((float(src[0]), float(src[1]), 0), (float(x), float(y), 0))
+                         for x, y in q]
+                key = '%s_e%d_a%d' % (cfg, e, a)
+                out[key + '_src'] = src.astype(np.float64)
+                out[key + '_queries'] = q.astype(np.float64)
+                out[key + '_dist'] = np.array(d, dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, 'sp_distance.npz'), **out)
+    print('wrote sp_distance goldens')
+
+
 def main():
     envs, sp = import_reference()
     which = sys.argv[1:] or ['micro', 'scenes']
@@ -294,6 +330,8 @@ def main():
         gen_micro(envs, sp)
     if 'scenes' in which:
         gen_scenes(envs)
+    if 'sp_distance' in which or not sys.argv[1:]:
+        gen_sp_distance(envs)
 
 
 if __name__ == '__main__':

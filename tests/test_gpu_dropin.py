@@ -91,3 +91,40 @@ def test_gridgraph_dropin(V):
     assert _bitwise(bi, O.spfa_image(grid, blocked))
     with pytest.raises(IndexError):
         gg.shortest_path_distance((75, 156), (10_000, 0))
+
+
+def test_sp_distance_reference_goldens(V):
+    """Reward lookups through simaps_sp_distance vs values produced by the
+    reference's own Mapper.distance_to_receptacle / OccupancyMap.shortest_path_distance."""
+    synthetic, vector_env = V
+    from simaps import batch
+    z = G.load('sp_distance.npz')
+    keys = sorted(k[:-len('_dist')] for k in z.files if k.endswith('_dist'))
+    by_cfg = {}
+    for key in keys:
+        cfg, rest = key.rsplit('_e', 1)
+        e, a = (int(x) for x in rest.split('_a'))
+        by_cfg.setdefault(cfg, []).append((e, a, key))
+    for cfg, items in by_cfg.items():
+        scenes = [synthetic.make_scene(cfg, 40 + e) for e in range(2)]
+        b = batch.StateBatch(scenes)
+        slots = [b.agents.index((e, a)) for e, a, _ in items]
+        src = np.stack([z[k + '_src'] for _, _, k in items])
+        tgt = np.stack([z[k + '_queries'] for _, _, k in items])
+        got = b.shortest_path_distances(src, tgt, slots=slots).cpu().numpy()
+        want = np.stack([z[k + '_dist'] for _, _, k in items])
+        assert np.array_equal(got, want), cfg
+
+
+def test_distance_to_receptacle_dropin(V):
+    synthetic, vector_env = V
+    scenes = [synthetic.make_scene('lifting_2_throwing_2-large_empty', 70 + e) for e in range(3)]
+    obs = vector_env.VectorEnvObservations(scenes)
+    rs = np.random.RandomState(5)
+    pos = [[[tuple(rs.uniform(-0.55, 0.55, 2)) + (0.0,) for _ in range(rs.randint(0, 7))] for _ in s['robots']]
+           for s in scenes]
+    got = obs.distance_to_receptacle(pos)
+    for e, s in enumerate(scenes):
+        for a in range(len(s['robots'])):
+            ao = O.AgentOracle(s, a)
+            assert got[e][a] == [ao.shortest_path_distance(s['receptacle_position'], p) for p in pos[e][a]]

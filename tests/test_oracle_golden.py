@@ -125,3 +125,19 @@ def test_agent_state_matches_reference(case):
     ref = z[pre + 'state']
     assert st.shape == ref.shape and st.dtype == np.float32
     assert np.array_equal(st.view(np.int32), ref.view(np.int32))
+
+
+def test_oracle_shortest_path_distance_vs_reference():
+    """Reward lookups: Mapper.distance_to_receptacle / OccupancyMap.
+    shortest_path_distance (envs.py:2190-2194, 2507-2512) from the reference itself."""
+    from simaps import synthetic
+    z = G.load('sp_distance.npz')
+    keys = sorted(k[:-len('_dist')] for k in z.files if k.endswith('_dist'))
+    assert len(keys) >= 20
+    for key in keys:
+        cfg, rest = key.rsplit('_e', 1)
+        e, a = (int(x) for x in rest.split('_a'))
+        ao = O.AgentOracle(synthetic.make_scene(cfg, 40 + e), a)
+        src = z[key + '_src']
+        got = [ao.shortest_path_distance((src[0], src[1]), (x, y)) for x, y in z[key + '_queries']]
+        assert got == list(z[key + '_dist']), key
