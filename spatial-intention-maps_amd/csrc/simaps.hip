@@ -441,6 +441,24 @@ constexpr unsigned NINF_BITS = 0xff800000u;  // blocked / border cells
 
 typedef __attribute__((address_space(3))) float lds_float;
 
+// ds_min_f32 for the lanes with `on` set, as ONE inline-asm block: an `if (on) atomicMin(...)` makes
+// the compiler split the sweep step into exec-masked basic blocks, which no instruction scheduling
+// crosses, so each step's latency chain would be fully exposed.  The asm's LDS op is invisible to
+// the compiler's lgkmcnt bookkeeping; an extra in-order op AFTER a load only makes its waits more
+// conservative, and every barrier waits lgkmcnt(0).
+__device__ __forceinline__ void lds_min_masked(lds_float *p, float v, bool on)
+{
+    const uint64_t m = __ballot(on);
+    uint64_t save;
+    asm volatile(
+        "s_and_saveexec_b64 %0, %1\n\t"
+        "ds_min_f32 %2, %3\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(save)
+        : "s"(m), "v"((unsigned)(uintptr_t)p), "v"(v)
+        : "memory");
+}
+
 // One sweep of one wave.  DIR: 0 down, 1 up (lines = rows), 2 right, 3 left (lines = columns);
 // CPL: cells per lane across the line (1: span <= 63, 2: span <= 120).  Returns true if a lane
 // found an improvement.  Lines are prefetched P steps ahead into a ring of named registers;
@@ -478,8 +496,8 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw)
         }                                                                                               \
         const bool u0 = (LIVE) && m0 < R0;                                                              \
         const bool u1 = CPL == 2 && (LIVE) && m1 < R1;                                                  \
-        if (u0) __hip_atomic_fetch_min(&D[cur], m0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);    \
-        if (u1) __hip_atomic_fetch_min(&D[cur + sa], m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+        lds_min_masked(&D[cur], m0, u0);                                                                \
+        if (CPL == 2) lds_min_masked(&D[cur + sa], m1, u1);                                             \
         chg |= u0 | u1;                                                                                 \
         p0 = fabsf(__builtin_elementwise_minimum(m0, R0));                                              \
         if (CPL == 2) p1 = fabsf(__builtin_elementwise_minimum(m1, R1));                                \
