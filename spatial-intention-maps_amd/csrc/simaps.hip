@@ -32,6 +32,10 @@
 // gathered through L2 (<= 136^2 f32 footprint), the state write (96*96*C f32).  No intermediate
 // map ever leaves the CU.
 //
+// Diagnostic-only build macros (tools/phase_profile.py with `make variant`, never the product):
+// SIMAPS_PHASE_STAMPS (per-phase s_memrealtime stamps), SIMAPS_ABL_NOSWEEP / _NORENDER (one group
+// of the split alone), SIMAPS_ABL_NOGATHER / _NOGPIX (overhead gathers / fp64 sample indices off).
+//
 // Compiled with -ffp-contract=off: every fp32/fp64 operation rounds exactly like the reference
 // (see geom.h for the one explicit fma).
 #include <hip/hip_runtime.h>
@@ -834,7 +838,11 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
         const int p = g.t + k * g.n;
+#if defined(SIMAPS_ABL_NOGPIX)
+        const int q = p < NP ? ((sh.pi - 48 + p / LW) << 16) | (sh.pj - 48 + p % LW) : -1;
+#else
         const int q = p < NP ? rc.gpix_tab(T, p) : -1;
+#endif
         const uint32_t v = q >= 0 ? (uint32_t)((((q >> 16) - ci0) << 8) | ((q & 0xffff) - cj0)) : 0xffffu;
         if (k & 1) gqp[k >> 1] |= v << 16;
         else gqp[k >> 1] = v;
@@ -849,7 +857,11 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
         const int q = gq_at(k);
+#ifdef SIMAPS_ABL_NOGATHER
+        ovv[k] = q >= 0 ? 0.125f : 0.0f;
+#else
         ovv[k] = q >= 0 ? ovh[(size_t)(q >> 16) * W + (q & 0xffff)] : 0.0f;
+#endif
     }
 #ifdef SIMAPS_PHASE_STAMPS
     if (g.t == 0) {
@@ -1166,22 +1178,15 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const RenderCtx rc{cfg, sh, out, C, n};
     const int sweep_waves = 4 * nsrc;
     if ((tid >> 6) < sweep_waves) {
-#ifdef SIMAPS_SWEEP_PRIO
-        __builtin_amdgcn_s_setprio(SIMAPS_SWEEP_PRIO);
-#endif
         const Group g{tid, 64 * sweep_waves, sh.bar[0], sweep_waves};
+#ifndef SIMAPS_ABL_NOSWEEP  // diagnostic: render alone (distance channels wrong)
         sssp_rounds(sh, dist, nsrc, g);
-        sssp_finish(sh, dist, nsrc, g);  // while the render waves finish
-#ifdef SIMAPS_SWEEP_PRIO
-        __builtin_amdgcn_s_setprio(0);
 #endif
+        sssp_finish(sh, dist, nsrc, g);  // while the render waves finish
         STAMP_NB(7);
     } else {
         const int nw = NT / 64 - sweep_waves;
         const Group g{tid - 64 * sweep_waves, 64 * nw, sweep_waves ? sh.bar[1] : nullptr, nw};
-#ifdef SIMAPS_RENDER_PRIO
-        __builtin_amdgcn_s_setprio(SIMAPS_RENDER_PRIO);
-#endif
 #ifndef SIMAPS_ABL_NORENDER  // diagnostic: sweeps alone (output channels 0.. left unwritten)
         render_maps(rc, g, geo, overhead + (size_t)ag.map_slot * H * W, rb, paths, tile);
 #endif
