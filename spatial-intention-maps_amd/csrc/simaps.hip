@@ -177,7 +177,6 @@ struct Shared {
 // SSSP scratch (aliases the raster tile, which is only used after the SSSP phase)
 struct SsspScratch {
     uint64_t win[MAX_WIN_ROWS][WIN_WORDS];
-    B128 blocked[MAX_ROWS];
     B128 freeb[MAX_ROWS];
 };
 
@@ -216,69 +215,75 @@ constexpr int RMAX = 7;  // floor(RADIUS * 96) <= 6 for every robot class (envs.
 struct OccLoad {
     uint8_t v[16], v2;
 };
+// Words 0-1 of a window row: thread -> (row tid / 128 + 8q, column tid % 128), so every wave holds
+// 64 consecutive columns of one row (one ballot per row word).  Word 2 (columns 128..133): thread ->
+// (row 8 * wave + lane / 8, column 128 + lane % 8).
 __device__ __forceinline__ void cspace_load(OccLoad &L, const uint8_t *__restrict__ occ, int H, int W, int i0, int j0,
                                             int h, int w)
 {
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wh = h + 2 * RMAX, ww = w + 2 * RMAX;  // <= 126 x 134
-    const int c = tid & 127, r0 = tid >> 7;          // thread -> (row r0 + 8q, column c [+ 128])
+    const int c = tid & 127, r0 = tid >> 7;
 #pragma unroll
     for (int q = 0; q < 16; q++) {
         const int rr = r0 + 8 * q, gi = i0 - RMAX + rr, gj = j0 - RMAX + c;
         L.v[q] = (rr < wh && c < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
     }
-    {   // columns 128..133 of the widest window
-        const int rr = tid / 6, cc = 128 + tid % 6, gi = i0 - RMAX + rr, gj = j0 - RMAX + cc;
+    {
+        const int rr = 8 * wave + (lane >> 3), cc = 128 + (lane & 7), gi = i0 - RMAX + rr, gj = j0 - RMAX + cc;
         L.v2 = (rr < wh && cc < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
     }
 }
 
+// OR of x over the 16 lanes of its DPP row (quad swaps, then half-row and row mirrors)
+__device__ __forceinline__ unsigned row16_or(unsigned x)
+{
+    x |= (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    x |= (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    x |= (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    x |= (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xf, 0xf, false);  // row_mirror
+    return x;
+}
+
+// S.win rows (RMAX-window coordinates) -> S.freeb: 1 - max(1 - room_mask, binary_dilation(occ, disk(r)))
+// inside the room rect (envs.py:2453).  No LDS staging, no atomics: window words come straight from
+// the loaded registers by ballots; each 16-lane DPP row computes one output row, lane = disk row dy.
 __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad &L, int h, int w, int r)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wh = h + 2 * r, ww = w + 2 * r;
-    const int whM = h + 2 * RMAX, wwM = w + 2 * RMAX, o = RMAX - r;
-    const int nwords = (ww + 63) >> 6;
-    // (a) the loaded window bytes -> LDS stage (the raster-tile region, free until the render), then
-    // (b) window rows -> bit rows: one wave ballot per 64 columns, from LDS.
-    uint8_t *stage = reinterpret_cast<uint8_t *>(S.blocked) + sizeof(S.blocked) + sizeof(S.freeb) + 64;
+    const int whM = h + 2 * RMAX, wwM = w + 2 * RMAX;
     {
         const int c = tid & 127, r0 = tid >> 7;
 #pragma unroll
         for (int q = 0; q < 16; q++) {
             const int rr = r0 + 8 * q;
-            if (rr < whM && c < wwM) stage[rr * wwM + c] = L.v[q];
+            const uint64_t m = __ballot(rr < whM && c < wwM && L.v[q] != 0);
+            if (lane == 0 && rr < whM) S.win[rr][wave & 1] = m;
         }
-        const int rr = tid / 6, cc = 128 + tid % 6;
-        if (rr < whM && cc < wwM) stage[rr * wwM + cc] = L.v2;
+        const int rr = 8 * wave + (lane >> 3), cc = 128 + (lane & 7);
+        const uint64_t m = __ballot(rr < whM && cc < wwM && L.v2 != 0);
+        if (lane < 8 && 8 * wave + lane < whM) S.win[8 * wave + lane][2] = (m >> (8 * lane)) & 0xffu;
     }
     lds_barrier();
-    for (int item = wave; item < wh * WIN_WORDS; item += NT / 64) {
-        const int wr = item / WIN_WORDS, wd = item % WIN_WORDS;
-        const int x = wd * 64 + lane;
-        const bool ob = wd < nwords && x < ww && stage[(wr + o) * wwM + x + o] != 0;
-        const uint64_t m = __ballot(ob);
-        if (lane == 0) S.win[wr][wd] = m;
-    }
-    for (int rr = tid; rr < h; rr += NT) S.blocked[rr] = {0, 0};
-    lds_barrier();
-    // (b) blocked[row] = OR over disk offsets (dy, |dx| <= hw(dy)) of the window bits
-    const int span = 2 * r + 1;
-    for (int item = tid; item < h * 16; item += NT) {  // 16 slots per row >= span (r <= 7)
-        const int row = item >> 4, dy = (item & 15) - r;
-        if (dy > r) continue;
-        int hw = 0;
+    if (threadIdx.x == 0) STAMP_NB(15);
+    const B128 fm = b_mask(w);
+    const int dy = (tid & 15) - r;
+    int hw = -1;  // disk(r) half-width of row dy (skimage disk: dx^2 + dy^2 <= r^2)
+    if (dy <= r)
         while ((hw + 1) * (hw + 1) + dy * dy <= r * r) hw++;
-        const uint64_t *wrow = S.win[row + r + dy];
+    for (int base = 0; base < h; base += NT / 16) {  // uniform: every lane takes part in the DPP ORs
+        const int row = base + (tid >> 4);
         B128 acc = {0, 0};
-        for (int k = -hw; k <= hw; k++) acc = b_or(acc, win_get(wrow, r + k));
-        b_atomic_or(&S.blocked[row], acc);
-    }
-    lds_barrier();
-    const B128 m = b_mask(w);
-    for (int rr = tid; rr < h; rr += NT) {
-        const B128 b = S.blocked[rr];
-        S.freeb[rr] = {~b.lo & m.lo, ~b.hi & m.hi};
+        if (row < h && hw >= 0) {
+            const uint64_t *wrow = S.win[row + RMAX + dy];
+            for (int k = -hw; k <= hw; k++) acc = b_or(acc, win_get(wrow, RMAX + k));
+        }
+        const unsigned a0 = row16_or((unsigned)acc.lo), a1 = row16_or((unsigned)(acc.lo >> 32));
+        const unsigned a2 = row16_or((unsigned)acc.hi), a3 = row16_or((unsigned)(acc.hi >> 32));
+        if ((tid & 15) == 0 && row < h) {
+            const uint64_t lo = ((uint64_t)a1 << 32) | a0, hi = ((uint64_t)a3 << 32) | a2;
+            S.freeb[row] = {~lo & fm.lo, ~hi & fm.hi};
+        }
     }
     lds_barrier();
 }
@@ -542,28 +547,26 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
     }
 }
 
-// all threads: free cells +inf, blocked / border -inf, sources 0
+// all threads: free cells +inf, blocked / border -inf, sources 0 (one pass over the rect rows)
 __device__ __forceinline__ void sssp_init(Shared &sh, const SsspScratch &S, float *dist, int nsrc)
 {
     const int tid = threadIdx.x;
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
     const float NI = -INFINITY;
+    int sidx[2];  // flat index of each (snapped, free) source, -1 if none
+    for (int s = 0; s < 2; s++)
+        sidx[s] = (s < nsrc && sh.src_ok[s]) ? (sh.src_s[s][0] - sh.i0 + 1) * pw + (sh.src_s[s][1] - sh.j0 + 1) : -1;
     // (row, column) walk instead of k / pitch: integer division by a runtime value costs ~40 ops
-    for (int s = 0; s < nsrc; s++) {
-        float *D = dist + s * DIST_FLOATS;
-        for (int rr = tid >> 7; rr < h + 2; rr += NT >> 7) {
-            const B128 fb = (rr >= 1 && rr <= h) ? S.freeb[rr - 1] : B128{0, 0};
-            for (int c = tid & 127; c < pw; c += 128) {
-                const bool fr = c >= 1 && c <= w && b_test(fb, c - 1);
-                D[rr * pw + c] = fr ? INFINITY : NI;
-            }
+    for (int rr = tid >> 7; rr < h + 2; rr += NT >> 7) {
+        const B128 fb = (rr >= 1 && rr <= h) ? S.freeb[rr - 1] : B128{0, 0};
+        for (int c = tid & 127; c < pw; c += 128) {
+            const int k = rr * pw + c;
+            const float v = (c >= 1 && c <= w && b_test(fb, c - 1)) ? INFINITY : NI;
+            for (int s = 0; s < nsrc; s++) dist[s * DIST_FLOATS + k] = k == sidx[s] ? 0.0f : v;
         }
     }
     if (tid < 3) sh.changed[tid] = 0;
     if (tid < 8) (&sh.bar[0][0])[tid] = 0u;
-    lds_barrier();
-    for (int s = tid; s < nsrc; s += NT)
-        if (sh.src_ok[s]) dist[s * DIST_FLOATS + (sh.src_s[s][0] - sh.i0 + 1) * pw + (sh.src_s[s][1] - sh.j0 + 1)] = 0.0f;
     lds_barrier();
 }
 
@@ -1118,11 +1121,11 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             P.bj1 = min(P.st_j + R.S1 - 1, P.st_j + (int)ceil(mx1) + 2);
             P.bi1 = min(P.bi1, P.bi0 + 31);  // the window is <= 17 x 13 px: its rotated box fits 32 x 32
             P.bj1 = min(P.bj1, P.bj0 + 31);
-            for (int q = 0; q < 32; q++) P.sbits[0][q] = P.sbits[1][q] = 0u;
         }
         P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
     }
     lds_barrier();
+    if (tid == 0) STAMP_NB(9);
 
     if (cfg.use_intention_channels && tid == 256) intention_channel_order(sh, cfg, rb);
 
@@ -1136,21 +1139,30 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         mwin[120 + q] = f == 0 ? geo.mrow0[m] : f == 1 ? geo.mcol0[m] : f == 2 ? geo.mnrows[m] : geo.mncols[m];
     }
     lds_barrier();
+    // a wave covers tile rows bi, bi + 1 of one robot (64 cells): bits by ballot, no atomics
     for (int item = tid; item < ev.num_robots * 1024; item += NT) {
         const int k = item >> 10, cell = item & 1023, bi = cell >> 5, bj = cell & 31;
         RobotP &P = sh.rob[k];
         const int gi = P.bi0 + bi, gj = P.bj0 + bj;
-        if (gi > P.bi1 || gj > P.bj1) continue;
-        const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
+        bool b0 = false, b1 = false;
         int m0, m1;
-        if (!rot_src(R, LW, gi - P.st_i, gj - P.st_j, m0, m1)) continue;
-        auto bit = [&](int m) {
-            const int *mi = reinterpret_cast<const int *>(mwin + 120 + 4 * m);
-            const int r = m0 - mi[0], c = m1 - mi[1];
-            return r >= 0 && r < mi[2] && c >= 0 && c < mi[3] && ((mwin[m * 24 + r] >> c) & 1u);
-        };
-        if (bit(P.type)) atomicOr(&P.sbits[0][bi], 1u << bj);
-        if (P.type == SIMAPS_LIFTING && P.lifting && bit(4)) atomicOr(&P.sbits[1][bi], 1u << bj);
+        const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
+        if (gi <= P.bi1 && gj <= P.bj1 && rot_src(R, LW, gi - P.st_i, gj - P.st_j, m0, m1)) {
+            auto bit = [&](int m) {
+                const int *mi = reinterpret_cast<const int *>(mwin + 120 + 4 * m);
+                const int r = m0 - mi[0], c = m1 - mi[1];
+                return r >= 0 && r < mi[2] && c >= 0 && c < mi[3] && ((mwin[m * 24 + r] >> c) & 1u);
+            };
+            b0 = bit(P.type);
+            b1 = P.type == SIMAPS_LIFTING && P.lifting && bit(4);
+        }
+        const uint64_t w0 = __ballot(b0), w1 = __ballot(b1);
+        if ((tid & 63) == 0) {
+            P.sbits[0][bi] = (uint32_t)w0;
+            P.sbits[0][bi + 1] = (uint32_t)(w0 >> 32);
+            P.sbits[1][bi] = (uint32_t)w1;
+            P.sbits[1][bi + 1] = (uint32_t)(w1 >> 32);
+        }
     }
     lds_barrier();
 

@@ -53,6 +53,10 @@ def main():
                                'ch01_consume_store': float(np.median((st[:, 11] - st[:, 13]) / 100.0)),
                                'maps_raster': float(np.median((st[:, 12] - st[:, 11]) / 100.0)),
                                'maps_sample': float(np.median((st[:, 8] - st[:, 12]) / 100.0))},
+           'pre_split_us': {'robot_params': float(np.median((st[:, 9] - st[:, 0]) / 100.0)),
+                            'stamp_tiles': float(np.median((st[:, 1] - st[:, 9]) / 100.0)),
+                            'cspace_stage': float(np.median((st[:, 15] - st[:, 1]) / 100.0)),
+                            'cspace_bits': float(np.median((st[:, 2] - st[:, 15]) / 100.0))},
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())},
            'phases_us': {p: {'median': float(np.median(d[:, i])), 'max': float(d[:, i].max())}
                          for i, p in enumerate(PHASES)}}
