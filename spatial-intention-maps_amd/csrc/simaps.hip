@@ -50,7 +50,7 @@ namespace {
 constexpr int NT = 1024;
 #ifdef SIMAPS_PHASE_STAMPS
 // Diagnostic build only (libsimaps_prof.so): per-workgroup s_memrealtime (100 MHz) stamps.
-constexpr int MAX_STAMP_WG = 8192, NSTAMP = 16;
+constexpr int MAX_STAMP_WG = 8192, NSTAMP = 24;
 __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
 // (a barrier first, so a stamp marks the moment the SLOWEST wave finished the previous phase)
 #define STAMP(k)                                                                                 \
@@ -159,6 +159,8 @@ struct Shared {
     int src_q[2][2], src_s[2][2], src_ok[2];
     int sp_slot[2];      // which dist buffer each sp channel uses (-1 = off)
     float dmax[2];
+    float unreach[2];    // scaled value of unreachable / outside cells when dist_scaled
+    int dist_scaled;     // dist[] already holds the channel values (sp / 96 * scale)
     int flag[2];
     int rounds;          // SSSP rounds to convergence (-1: cap hit)
     int nseg;
@@ -612,6 +614,24 @@ __device__ __forceinline__ void sssp_finish(Shared &sh, float *dist, int nsrc, c
     }
 }
 
+// group g, after sssp_finish: dist[] -> the global shortest-path map values in place, so the division
+// runs in the sweep group's slack instead of the distance phase (envs.py:2288-2300: img = sp / 96,
+// img[img < 0] = img.max(), img *= scale; max(sp) / 96 == max(sp / 96): division is monotone)
+__device__ __forceinline__ void sssp_scale(Shared &sh, float *dist, int nsrc, float scale, const Group &g)
+{
+    g.sync();  // sh.dmax
+    const int cells = (sh.h + 2) * sssp_pitch(sh.w);
+    for (int s = 0; s < nsrc; s++) {
+        const float un = (sh.dmax[s] / 96.0f) * scale;
+        for (int q = g.t; q < cells; q += g.n) {
+            float &d = dist[s * DIST_FLOATS + q];
+            d = d != INFINITY ? (d / 96.0f) * scale : un;
+        }
+        if (g.t == 0) sh.unreach[s] = un;
+    }
+    if (g.t == 0) sh.dist_scaled = 1;
+}
+
 __device__ __forceinline__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
 {
     sssp_init(sh, S, dist, nsrc);
@@ -988,6 +1008,7 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
     float vals[3][PPT];
     float mins[3];
     const float sps = (float)cfg.shortest_path_map_scale;
+    const bool scaled = sh.dist_scaled;
     const float eus = (float)cfg.distance_to_receptacle_map_scale;
 #pragma unroll
     for (int q = 0; q < 3; q++) {
@@ -996,7 +1017,7 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
         const bool eu = q < has_eu;  // Euclidean map first (envs.py:2083-2084)
         const int s = q - has_eu;
         const float *D = dist + (eu ? 0 : s) * DIST_FLOATS;
-        const float unreach = eu ? 0.0f : (sh.dmax[eu ? 0 : s] / 96.0f) * sps;
+        const float unreach = eu ? 0.0f : scaled ? sh.unreach[s] : (sh.dmax[s] / 96.0f) * sps;
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
             float v = 0.0f;
@@ -1008,15 +1029,17 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
                     v = (float)sqrt(dx * dx + dy * dy) * eus;
                 } else {  // envs.py:2288-2300, 2514-2517
                     const int r = gi - sh.i0, c = gj - sh.j0;
-                    float dd = __int_as_float(INF_BITS);
-                    if (r >= 0 && r < sh.h && c >= 0 && c < sh.w) dd = D[(r + 1) * sssp_pitch(sh.w) + c + 1];
-                    v = dd != __int_as_float(INF_BITS) ? (dd / 96.0f) * sps : unreach;
+                    const bool in = r >= 0 && r < sh.h && c >= 0 && c < sh.w;
+                    const float dd = in ? D[(r + 1) * sssp_pitch(sh.w) + c + 1] : __int_as_float(INF_BITS);
+                    if (scaled) v = in ? dd : unreach;
+                    else v = dd != __int_as_float(INF_BITS) ? (dd / 96.0f) * sps : unreach;
                 }
             }
             vals[q][k] = v;
             mins[q] = fminf(mins[q], v);
         }
     }
+    if (tid == 0) STAMP_NB(16);
 #pragma unroll
     for (int q = 0; q < 3; q++) {
         if (q >= nd) continue;
@@ -1024,6 +1047,7 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
         if ((tid & 63) == 0) sh.red[q][tid >> 6] = m;
     }
     lds_barrier();
+    if (tid == 0) STAMP_NB(17);
 #pragma unroll
     for (int q = 0; q < 3; q++) {
         if (q >= nd) continue;
@@ -1086,6 +1110,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             sh.sp_slot[1] = ns++;
         }
         sh.nsrc = ns;
+        sh.dist_scaled = 0;
     }
     if (tid == 64) {
         const simaps_robot &me = rb[ag.robot];
@@ -1195,6 +1220,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         sssp_rounds(sh, dist, nsrc, g);
 #endif
         sssp_finish(sh, dist, nsrc, g);  // while the render waves finish
+        if (!dbg.dist) sssp_scale(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);
         STAMP_NB(7);
     } else {
         const int nw = NT / 64 - sweep_waves;
@@ -1429,7 +1455,7 @@ extern "C" {
 int simaps_abi_version(void) { return SIMAPS_ABI_VERSION; }
 
 #ifdef SIMAPS_PHASE_STAMPS
-// Diagnostic build only: copy the stamp table (uint64 [8192][16]) to host memory.
+// Diagnostic build only: copy the stamp table (uint64 [8192][24]) to host memory.
 int simaps_debug_read_stamps(unsigned long long *host_out)
 {
     return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : SIMAPS_EHIP;

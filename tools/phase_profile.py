@@ -35,7 +35,7 @@ def main():
     for _ in range(3):
         b.render(out)
     torch.cuda.synchronize()
-    st = np.zeros((8192, 16), dtype=np.uint64)
+    st = np.zeros((8192, 24), dtype=np.uint64)
     b.render(out)
     torch.cuda.synchronize()
     assert L.simaps_debug_read_stamps(st.ctypes.data) == 0
@@ -57,6 +57,9 @@ def main():
                             'stamp_tiles': float(np.median((st[:, 1] - st[:, 9]) / 100.0)),
                             'cspace_stage': float(np.median((st[:, 15] - st[:, 1]) / 100.0)),
                             'cspace_bits': float(np.median((st[:, 2] - st[:, 15]) / 100.0))},
+           'distance_us': {'values': float(np.median((st[:, 16] - st[:, 5]) / 100.0)),
+                           'block_min': float(np.median((st[:, 17] - st[:, 16]) / 100.0)),
+                           'stores': float(np.median((st[:, 6] - st[:, 17]) / 100.0))},
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())},
            'phases_us': {p: {'median': float(np.median(d[:, i])), 'max': float(d[:, i].max())}
                          for i, p in enumerate(PHASES)}}
