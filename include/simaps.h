@@ -18,6 +18,9 @@
  *   simaps_sp_distance  <- OccupancyMap.shortest_path_distance (envs.py:2507-2512), i.e. the reward
  *                          lookup Mapper.distance_to_receptacle (envs.py:2190-2194) used by the
  *                          partial rewards (envs.py:1083-1088, 1211-1216, 1332-1336), batched.
+ *   simaps_shortest_path <- OccupancyMap.shortest_path (envs.py:2478-2505) + GridGraph.shortest_path
+ *                          (shortest_paths.pyx:121-154): the movement path of Robot.store_new_action
+ *                          (envs.py:875-876), batched, exact SPFA parents.
  *   simaps_robot_mask   <- Mapper._create_robot_mask (envs.py:2218-2242) (host helper).
  *   simaps_num_channels <- the channel list of Mapper.get_state (envs.py:2071-2113).
  */
@@ -154,6 +157,15 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
 int simaps_sp_distance(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
                        const simaps_robot *robots, const uint8_t *occupancy, const double *sources,
                        const double *targets, int Q, double *out, void *stream);
+
+/* Batched OccupancyMap.shortest_path(source_position, target_position) on agent n's own map:
+ *   sources [N][2], targets [N][2] fp64 (x, y); out_xy [N][max_points][2] fp64 waypoints (first =
+ *   source, last = target, as the reference returns them), out_count [N] = number of waypoints, or
+ *   -needed if max_points is too small.  All DEVICE.  The SPFA runs exactly like pyx:69-114 (edge
+ *   order, SLF swap), so the parents -- and hence the waypoints -- are the reference's. */
+int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                         const simaps_robot *robots, const uint8_t *occupancy, const double *sources,
+                         const double *targets, int max_points, double *out_xy, int32_t *out_count, void *stream);
 
 /* Batched GridGraph(grid).shortest_path_image(source):
  *   grids [B, H, W] uint8 (nonzero = free), sources [B, 2] int32 (row, col), out dists [B, H, W]

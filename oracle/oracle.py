@@ -80,6 +80,76 @@ def spfa_image(grid_u8, source):
     return d.reshape(H, W)
 
 
+def spfa(grid_u8, source):
+    """GridGraph._spfa (pyx:69-114): (dists f32 [H*W] with -1 unreachable, parents i32 [H*W])."""
+    grid = np.ascontiguousarray(grid_u8, dtype=np.uint8)
+    H, W = grid.shape
+    d = np.empty(H * W, dtype=np.float32)
+    p = np.empty(H * W, dtype=np.int32)
+    if lib().oracle_spfa(grid.ravel(), H, W, int(source[0]), int(source[1]), d, p) != 0:
+        raise RuntimeError('oracle SPFA queue overflow')
+    return d, p
+
+
+def approximate_polygon(coords, tolerance):
+    """skimage.measure.approximate_polygon (scikit-image 0.18.3, measure/_polygon.py): Douglas-Peucker
+    with an explicit stack; perpendicular distance inside the segment's span, else the distance to
+    the nearer end point; the first maximum splits."""
+    if tolerance <= 0:
+        return coords
+    chain = np.zeros(coords.shape[0], 'bool')
+    dists = np.zeros(coords.shape[0])
+    chain[0] = True
+    chain[-1] = True
+    stack = [(0, chain.shape[0] - 1)]
+    while stack:
+        start, end = stack.pop()
+        r0, c0 = coords[start, :]
+        r1, c1 = coords[end, :]
+        dr, dc = r1 - r0, c1 - c0
+        ang = -np.arctan2(dr, dc)
+        sdist = c0 * np.sin(ang) + r0 * np.cos(ang)
+        seg = coords[start + 1:end, :]
+        sd = dists[start + 1:end]
+        dr0, dc0 = seg[:, 0] - r0, seg[:, 1] - c0
+        dr1, dc1 = seg[:, 0] - r1, seg[:, 1] - c1
+        perp = np.logical_and(dr0 * dr + dc0 * dc > 0, -dr1 * dr - dc1 * dc > 0)
+        eucl = np.logical_not(perp)
+        sd[perp] = np.abs(seg[perp, 0] * np.cos(ang) + seg[perp, 1] * np.sin(ang) - sdist)
+        sd[eucl] = np.minimum(np.sqrt(dc0[eucl] ** 2 + dr0[eucl] ** 2), np.sqrt(dc1[eucl] ** 2 + dr1[eucl] ** 2))
+        if np.any(sd > tolerance):
+            new_end = start + np.argmax(sd) + 1
+            stack.append((new_end, end))
+            stack.append((start, new_end))
+            chain[new_end] = True
+    return coords[chain, :]
+
+
+def grid_shortest_path(grid_u8, source, target):
+    """GridGraph.shortest_path (pyx:121-154): parent walk target -> source, approximate_polygon
+    (tolerance 1), drop waypoints whose neighbours see each other on the grid, reversed."""
+    grid = np.ascontiguousarray(grid_u8, dtype=np.uint8)
+    H, W = grid.shape
+    _, parents = spfa(grid, source)
+    u = int(source[0]) * W + int(source[1])
+    v = int(target[0]) * W + int(target[1])
+    dense = [[v // W, v % W]]
+    while v != u:
+        v = int(parents[v])
+        if v < 0:
+            break
+        dense.append([v // W, v % W])
+    sparse = approximate_polygon(np.array(dense), tolerance=1)
+    path = [sparse[0]]
+    for k in range(1, sparse.shape[0] - 1):
+        rr, cc = line(*path[-1], *sparse[k + 1])
+        if (1 - grid[rr, cc]).sum() > 0:
+            path.append(sparse[k])
+    if len(sparse) > 1:
+        path.append(sparse[-1])
+    return path[::-1]
+
+
 def edt_indices(img):
     """scipy.ndimage.distance_transform_edt(img, return_distances=False, return_indices=True)."""
     a = np.ascontiguousarray(img != 0, dtype=np.uint8)
@@ -277,6 +347,8 @@ class AgentOracle:
         dil = binary_dilation(self.occupancy, selem).astype(np.uint8)
         self.cspace = (1 - np.maximum(1 - rm, dil)).astype(np.uint8)
         self.closest = edt_indices(1 - self.cspace)
+        # cspace_thin: no walls, disk(ceil(HALF_WIDTH * 96)) = disk(3) (envs.py:2426, 2456)
+        self.cspace_thin = (1 - binary_dilation(np.minimum(rm, self.occupancy), disk(K.THIN_RADIUS_PX))).astype(np.uint8)
         self._sp_cache = {}
 
     def snap(self, pos):
@@ -297,6 +369,21 @@ class AgentOracle:
         if src not in self._sp_cache:
             self._sp_cache[src] = spfa_image(self.cspace, src)
         return float(self._sp_cache[src][tgt]) / PPM
+
+    def shortest_path(self, source_position, target_position):
+        """OccupancyMap.shortest_path (envs.py:2478-2505) -> list of (x, y) positions."""
+        si, sj = position_to_pixel_indices(source_position[0], source_position[1], self.shape)
+        ti, tj = position_to_pixel_indices(target_position[0], target_position[1], self.shape)
+        rr, cc = line(si, sj, ti, tj)
+        if (1 - self.cspace_thin[rr, cc]).sum() == 0:
+            return [tuple(source_position[:2]), tuple(target_position[:2])]
+        src, tgt = self.snap(source_position), self.snap(target_position)
+        path = [pixel_indices_to_position(i, j, self.shape) for i, j in grid_shortest_path(self.cspace, src, tgt)]
+        if len(path) < 2:
+            return [tuple(source_position[:2]), tuple(target_position[:2])]
+        path[0] = tuple(source_position[:2])
+        path[-1] = tuple(target_position[:2])
+        return path
 
     def _sp_global(self, pos):
         g = self.shortest_path_image(pos)

@@ -1371,6 +1371,275 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Movement paths: OccupancyMap.shortest_path (envs.py:2478-2505) = straight-line test on cspace_thin,
+// EDT snap, GridGraph.shortest_path (pyx:121-154): SPFA parents, approximate_polygon, pruning.
+// ------------------------------------------------------------------------------------------------
+// skimage.draw.line pixel t of (r0, c0) -> (r1, c1): closed-form Bresenham, last pixel = end point
+__device__ __forceinline__ void line_pixel(int r0, int c0, int r1, int c1, int t, int &pr, int &pc)
+{
+    const int dr = abs(r1 - r0), dc = abs(c1 - c0), n = (dr > dc ? dr : dc) + 1;
+    if (t == n - 1) { pr = r1; pc = c1; return; }
+    const bool steep = dr > dc;
+    const int major = steep ? dr : dc, minor = steep ? dc : dr;
+    const int smaj = steep ? (r1 - r0 > 0 ? 1 : -1) : (c1 - c0 > 0 ? 1 : -1);
+    const int smin = steep ? (c1 - c0 > 0 ? 1 : -1) : (r1 - r0 > 0 ? 1 : -1);
+    const int kt = major > 0 ? (2 * minor * t + major) / (2 * major) : 0;
+    if (steep) { pr = r0 + smaj * t; pc = c0 + smin * kt; }
+    else { pc = c0 + smaj * t; pr = r0 + smin * kt; }
+}
+
+// cspace (the GridGraph grid): free iff inside the room rect and a free cspace bit
+__device__ __forceinline__ bool cs_free(const Shared &sh, const SsspScratch &S, int i, int j)
+{
+    const int r = i - sh.i0, c = j - sh.j0;
+    return r >= 0 && r < sh.h && c >= 0 && c < sh.w && b_test(S.freeb[r], c);
+}
+
+// cspace_thin = 1 - binary_dilation(min(room_mask, occupancy), disk(3)) (envs.py:2456): free iff no
+// in-room occupied pixel within disk(3); S.win holds the occupancy window (rect + RMAX halo).
+__device__ __forceinline__ bool thin_free(const Shared &sh, const SsspScratch &S, int i, int j)
+{
+    constexpr int R = 3;  // disk(ceil(HALF_WIDTH * 96)) (envs.py:2426)
+    for (int dy = -R; dy <= R; dy++)
+        for (int dx = -R; dx <= R; dx++) {
+            if (dx * dx + dy * dy > R * R) continue;
+            const int y = i + dy, x = j + dx;
+            if (y < sh.i0 || y >= sh.i0 + sh.h || x < sh.j0 || x >= sh.j0 + sh.w) continue;  // room mask
+            const int wr = y - (sh.i0 - RMAX), wc = x - (sh.j0 - RMAX);
+            if ((S.win[wr][wc >> 6] >> (wc & 63)) & 1ull) return false;
+        }
+    return true;
+}
+
+// wave-parallel: is every pixel of line (r0, c0) -> (r1, c1) free (thin ? cspace_thin : cspace)?
+__device__ __forceinline__ bool line_free(const Shared &sh, const SsspScratch &S, int r0, int c0, int r1, int c1,
+                                          bool thin)
+{
+    const int lane = threadIdx.x & 63;
+    const int n = max(abs(r1 - r0), abs(c1 - c0)) + 1;
+    bool blocked = false;
+    for (int t = lane; t < n; t += 64) {
+        int pr, pc;
+        line_pixel(r0, c0, r1, c1, t, pr, pc);
+        blocked |= thin ? !thin_free(sh, S, pr, pc) : !cs_free(sh, S, pr, pc);
+    }
+    return __ballot(blocked) == 0;
+}
+
+constexpr int PATH_MAX_PTS = 64;
+
+__global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents,
+                                                  const simaps_env *__restrict__ envs,
+                                                  const simaps_robot *__restrict__ robots,
+                                                  const uint8_t *__restrict__ occupancy,
+                                                  const double *__restrict__ sources, const double *__restrict__ targets,
+                                                  int max_pts, double *__restrict__ out_xy, int *__restrict__ out_n)
+{
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    Shared &sh = *reinterpret_cast<Shared *>(smem);
+    float *dist = reinterpret_cast<float *>(smem + OFF_DIST);
+    int *parent = reinterpret_cast<int *>(smem + OFF_DIST) + DIST_FLOATS;
+    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
+    int *queue = reinterpret_cast<int *>(smem + OFF_UNION + align16((int)sizeof(SsspScratch)));
+    static_assert(align16((int)sizeof(SsspScratch)) + DIST_FLOATS * 5 <= UNION_BYTES, "SPFA queue + flags fit the union");
+    uint8_t *inq = reinterpret_cast<uint8_t *>(queue + DIST_FLOATS);  // later: chain flags
+    int *dense = queue;  // after the SPFA: the dense path
+    // after the parent walk the distance + parent arrays are free: the Douglas-Peucker stack
+    // (<= 2 * points ints), then the sparse points and the kept waypoints
+    int *stack = reinterpret_cast<int *>(smem + OFF_DIST);
+    int *sparse = stack, *outp = stack + DIST_FLOATS;
+    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int H = cfg.H, W = cfg.W;
+    const simaps_agent ag = agents[n];
+    OccLoad occ_regs;
+    cspace_load(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
+                cfg.room_w);
+    const double sx = sources[2 * n], sy = sources[2 * n + 1], tx = targets[2 * n], ty = targets[2 * n + 1];
+    if (tid == 0) {
+        const simaps_env ev = envs[ag.env];
+        sh.h = cfg.room_h;
+        sh.w = cfg.room_w;
+        sh.i0 = cfg.room_i0;
+        sh.j0 = cfg.room_j0;
+        sh.r = geo.cspace_r[robots[ev.robot_off + ag.robot].type];
+        pos_to_pix(sx, sy, H, W, sh.src_q[0][0], sh.src_q[0][1]);
+        pos_to_pix(tx, ty, H, W, sh.src_q[1][0], sh.src_q[1][1]);
+        sh.nsrc = 2;
+    }
+    lds_barrier();
+    build_cspace(S, occ_regs, sh.h, sh.w, sh.r);
+    double *o = out_xy + (size_t)n * max_pts * 2;
+    // (1) straight line on cspace_thin between the unsnapped pixels (envs.py:2484-2486)
+    if (tid < 64) {
+        const bool straight = line_free(sh, S, sh.src_q[0][0], sh.src_q[0][1], sh.src_q[1][0], sh.src_q[1][1], true);
+        if (lane == 0) sh.flag[0] = straight;
+    }
+    lds_barrier();
+    if (sh.flag[0]) {
+        if (tid == 0) { o[0] = sx; o[1] = sy; o[2] = tx; o[3] = ty; out_n[n] = 2; }
+        return;
+    }
+    // (2) snap both ends (envs.py:2489-2490)
+    snap_sources(sh, S, 2);
+    const int h = sh.h, w = sh.w, pw = sssp_pitch(w), cells = (h + 2) * pw;
+    // (3) GridGraph._spfa (pyx:69-114) from the snapped source, exactly: one wave, the 8 out-edges of
+    // a popped vertex evaluated by lanes 0..7 (distinct heads, so in parallel), then the pushes and
+    // SLF swaps in edge order.  inf = 2 * H * W (pyx:38); queue as a ring (live entries <= cells).
+    const float INFR = (float)(2 * H * W);
+    for (int k = tid; k < cells; k += NT) { dist[k] = INFR; parent[k] = -1; inq[k] = 0; }
+    lds_barrier();
+    const bool src_ok = sh.src_ok[0] && sh.src_ok[1];
+    const int su = (sh.src_s[0][0] - sh.i0 + 1) * pw + (sh.src_s[0][1] - sh.j0 + 1);
+    const int tv = (sh.src_s[1][0] - sh.i0 + 1) * pw + (sh.src_s[1][1] - sh.j0 + 1);
+    if (tid < 64 && src_ok) {
+        // pyx:30 direction order [0,-1],[0,1],[-1,-1],[-1,0],[-1,1],[1,-1],[1,0],[1,1] -> lanes 0..7
+        const int di = lane >= 8 ? 0 : lane < 2 ? 0 : (lane < 5 ? -1 : 1);
+        const int dj = lane >= 8 ? 0 : lane < 2 ? (lane == 0 ? -1 : 1) : ((lane - 2) % 3) - 1;
+        const float wl = (lane < 8 && di != 0 && dj != 0) ? SQRT2F : 1.0f;
+        const int doff = di * pw + dj;
+        if (lane == 0) { dist[su] = 0.0f; queue[1 % cells] = su; inq[su] = 1; }
+        int head = 0, tail = 1, pops = 0;
+        while (head < tail && ++pops < (1 << 24)) {  // the guard is never reached by a correct SPFA
+            head++;
+            const int u = __builtin_amdgcn_readfirstlane(queue[head % cells]);
+            if (lane == 0) inq[u] = 0;
+            const float du = dist[u];
+            const int v = u + doff;
+            const int vr = v / pw - 1, vc = v % pw - 1;
+            const bool ok = lane < 8 && vr >= 0 && vr < h && vc >= 0 && vc < w && b_test(S.freeb[vr], vc);
+            const float nd = du + wl;
+            uint64_t imp = __ballot(ok && nd < dist[v]);
+            while (imp) {
+                const int k = __builtin_ctzll(imp);
+                imp &= imp - 1;
+                const int vk = __builtin_amdgcn_readlane(v, k);
+                const float ndk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), k));
+                if (lane == 0) {
+                    parent[vk] = u;
+                    dist[vk] = ndk;
+                    if (!inq[vk]) {
+                        tail++;
+                        queue[tail % cells] = vk;
+                        inq[vk] = 1;
+                        const int qa = queue[(head + 1) % cells];
+                        if (dist[vk] < dist[qa]) { queue[tail % cells] = qa; queue[(head + 1) % cells] = vk; }
+                    }
+                }
+                tail = __builtin_amdgcn_readfirstlane(tail);
+            }
+        }
+    }
+    lds_barrier();
+    // (4) dense path: parents from the target back to the source (pyx:131-138), global (i, j) packed
+    if (tid == 0) {
+        int cnt = 0, v = tv;
+        if (src_ok) {
+            dense[cnt++] = v;
+            while (v != su) {
+                v = parent[v];
+                if (v < 0) break;
+                dense[cnt++] = v;
+            }
+        }
+        for (int k = 0; k < cnt; k++) {
+            const int r = dense[k] / pw - 1 + sh.i0, c = dense[k] % pw - 1 + sh.j0;
+            dense[k] = (r << 16) | c;
+        }
+        sh.nseg = cnt;
+    }
+    lds_barrier();
+    const int nd = sh.nseg;
+    // (5) approximate_polygon(dense, tolerance=1) (skimage 0.18.3 measure/_polygon.py), one wave
+    uint8_t *chain = inq;
+    for (int k = tid; k < nd; k += NT) chain[k] = (k == 0 || k == nd - 1) ? 1 : 0;
+    lds_barrier();
+    if (tid < 64 && nd > 0) {
+        int sp = 0, iters = 0;
+        if (lane == 0) { stack[0] = 0; stack[1] = nd - 1; }
+        sp = 1;
+        while (sp > 0 && ++iters <= 2 * nd) {  // each pop either splits at a new chain point or ends
+            sp--;
+            const int start = stack[2 * sp], end = stack[2 * sp + 1];
+            const int r0 = dense[start] >> 16, c0 = dense[start] & 0xffff, r1 = dense[end] >> 16, c1 = dense[end] & 0xffff;
+            const long dr = r1 - r0, dc = c1 - c0;
+            const double ang = -atan2((double)dr, (double)dc);
+            const double sn = sin(ang), cs = cos(ang);
+            const double sdist = (double)c0 * sn + (double)r0 * cs;
+            double best = -1.0;
+            int besti = -1;
+            for (int k = start + 1 + lane; k < end; k += 64) {
+                const int rr = dense[k] >> 16, cc = dense[k] & 0xffff;
+                const long dr0 = rr - r0, dc0 = cc - c0, dr1 = rr - r1, dc1 = cc - c1;
+                const bool perp = dr0 * dr + dc0 * dc > 0 && -dr1 * dr - dc1 * dc > 0;
+                double d;
+                if (perp) d = fabs(((double)rr * cs + (double)cc * sn) - sdist);
+                else d = fmin(sqrt((double)(dc0 * dc0 + dr0 * dr0)), sqrt((double)(dc1 * dc1 + dr1 * dr1)));
+                if (d > best) { best = d; besti = k; }  // per lane: first maximum (ascending k)
+            }
+            // wave argmax with the first index on ties (np.argmax)
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ob = __shfl_xor(best, off);
+                const int oi = __shfl_xor(besti, off);
+                if (ob > best || (ob == best && oi >= 0 && (besti < 0 || oi < besti))) { best = ob; besti = oi; }
+            }
+            if (best > 1.0) {  // np.any(segment_dists > tolerance)
+                const int ne = besti;
+                if (lane == 0) {
+                    stack[2 * sp] = ne; stack[2 * sp + 1] = end;
+                    stack[2 * sp + 2] = start; stack[2 * sp + 3] = ne;
+                    chain[ne] = 1;
+                }
+                sp += 2;
+            }
+        }
+    }
+    lds_barrier();
+    // (6) line-of-sight pruning on the grid (pyx:143-150), then reversed (pyx:152)
+    if (tid < 64) {
+        int m = 0;  // sparse points = chain-flagged dense points, in order
+        for (int k0 = 0; k0 < nd; k0 += 64) {
+            const int k = k0 + lane;
+            const bool f = k < nd && chain[k];
+            const uint64_t b = __ballot(f);
+            if (f) sparse[m + __popcll(b & ((1ull << lane) - 1))] = dense[k];
+            m += __popcll(b);
+        }
+        int cnt = 0;
+        if (m > 0) {
+            if (lane == 0) outp[0] = sparse[0];
+            cnt = 1;
+            for (int k = 1; k < m - 1; k++) {
+                const int a = outp[cnt - 1], b2 = sparse[k + 1];
+                if (!line_free(sh, S, a >> 16, a & 0xffff, b2 >> 16, b2 & 0xffff, false)) {
+                    if (lane == 0) outp[cnt] = sparse[k];
+                    cnt++;
+                }
+            }
+            if (m > 1) {
+                if (lane == 0) outp[cnt] = sparse[m - 1];
+                cnt++;
+            }
+        }
+        // (7) positions (envs.py:2494-2503); path[0] / path[-1] replaced by the given positions
+        if (cnt < 2) {
+            if (lane == 0) { o[0] = sx; o[1] = sy; o[2] = tx; o[3] = ty; out_n[n] = 2; }
+        } else if (cnt > max_pts) {
+            if (lane == 0) out_n[n] = -cnt;  // caller's buffer too small
+        } else {
+            for (int k = lane; k < cnt; k += 64) {
+                const int pv = outp[cnt - 1 - k], pi = pv >> 16, pj = pv & 0xffff;
+                double x = ((pj + 0.5) - (double)W / 2) / PPM, y = ((double)H / 2 - (pi + 0.5)) / PPM;
+                if (k == 0) { x = sx; y = sy; }
+                if (k == cnt - 1) { x = tx; y = ty; }
+                o[2 * k] = x;
+                o[2 * k + 1] = y;
+            }
+            if (lane == 0) out_n[n] = cnt;
+        }
+    }
+}
+
 }  // namespace
 
 // =================================================================================================
@@ -1524,6 +1793,24 @@ int simaps_sp_distance(const simaps_config *cfg, int N, const simaps_agent *agen
                        occupancy, sources, targets, Q, out);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "sp_distance launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                         const simaps_robot *robots, const uint8_t *occupancy, const double *sources,
+                         const double *targets, int max_points, double *out_xy, int32_t *out_count, void *stream)
+{
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (N < 0 || max_points < 2) return fail(SIMAPS_EINVAL, "N < 0 or max_points < 2");
+    if (N == 0) return 0;
+    if (!agents || !envs || !robots || !occupancy || !sources || !targets || !out_xy || !out_count)
+        return fail(SIMAPS_EINVAL, "NULL buffer");
+    const Geometry geo = make_geometry();
+    hipLaunchKernelGGL(path_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, geo, agents, envs, robots,
+                       occupancy, sources, targets, max_points, out_xy, out_count);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "shortest_path launch: %s", hipGetErrorString(e));
     return 0;
 }
 

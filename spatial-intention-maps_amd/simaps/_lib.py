@@ -68,6 +68,8 @@ def _load():
     L.simaps_get_state.restype = i32
     L.simaps_sp_distance.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, i32, vp, vp]
     L.simaps_sp_distance.restype = i32
+    L.simaps_shortest_path.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp]
+    L.simaps_shortest_path.restype = i32
     L.simaps_sssp_grid.argtypes = [i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp]
     L.simaps_sssp_grid.restype = i32
     if L.simaps_abi_version() != ABI_VERSION:
@@ -78,7 +80,7 @@ def _load():
 lib = _load()
 
 EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_num_channels', 'simaps_robot_mask',
-            'simaps_get_state', 'simaps_sp_distance', 'simaps_sssp_grid')
+            'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_sssp_grid')
 
 
 def check(rc):

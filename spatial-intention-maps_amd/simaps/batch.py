@@ -243,6 +243,29 @@ class StateBatch:
         return out
 
 
+    def shortest_paths(self, sources, targets, slots=None, max_points=64, stream=None):
+        """OccupancyMap.shortest_path(source, target) (envs.py:2478-2505) on each agent's own map:
+        sources / targets [n, 2] fp64 (x, y) for map slots `slots` (all agents if None) -> list of n
+        waypoint lists [(x, y, 0), ...] like the reference returns (Robot.store_new_action,
+        envs.py:875-876)."""
+        agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
+        src = torch.as_tensor(sources, dtype=torch.float64).to(self.device).contiguous()
+        tgt = torch.as_tensor(targets, dtype=torch.float64).to(self.device).contiguous()
+        if tuple(src.shape) != (n, 2) or tuple(tgt.shape) != (n, 2):
+            raise ValueError('sources and targets must be [%d, 2]' % n)
+        xy = torch.empty((n, max_points, 2), dtype=torch.float64, device=self.device)
+        cnt = torch.empty((n,), dtype=torch.int32, device=self.device)
+        if n == 0:
+            return []
+        _lib.check(_lib.lib.simaps_shortest_path(
+            self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d), _lib.ptr(self.occupancy),
+            _lib.ptr(src), _lib.ptr(tgt), max_points, _lib.ptr(xy), _lib.ptr(cnt), _lib.stream_handle(stream)))
+        xy, cnt = xy.cpu().numpy(), cnt.cpu().numpy()
+        if (cnt < 0).any():
+            raise RuntimeError('a path has %d waypoints > max_points=%d' % (-cnt.min(), max_points))
+        return [[(float(x), float(y), 0) for x, y in xy[k, :cnt[k]]] for k in range(n)]
+
+
 def sssp_grid(grids, sources, window=None, stream=None):
     """Batched GridGraph(grid).shortest_path_image(source) on device.
 

@@ -49,6 +49,9 @@ SEG_VALUES = {
 }
 
 # VectorEnv.__init__ defaults for the state-representation flags (envs.py:39-45)
+# OccupancyMap.selem_thin = disk(ceil(Robot.HALF_WIDTH * 96)) (envs.py:2426), HALF_WIDTH = 0.03 (envs.py:802)
+THIN_RADIUS_PX = 3
+
 DEFAULT_FLAGS = {
     'use_robot_map': True,
     'use_distance_to_receptacle_map': False,

@@ -323,6 +323,45 @@ def gen_sp_distance(envs):
     print('wrote sp_distance goldens')
 
 
+def gen_paths(envs, sp):
+    """Movement paths: OccupancyMap.shortest_path (envs.py:2478-2505) with
+    GridGraph.shortest_path (pyx:121-154: SPFA parents, approximate_polygon, line-of-sight pruning),
+    on each agent's own map; plus GridGraph.shortest_path on the shortest_paths/demo.py sample."""
+    out = {}
+    rs = np.random.RandomState(4242)
+    for cfg in ('lifting_4-small_divider', 'pushing_4-large_empty', 'lifting_2_throwing_2-large_empty'):
+        for e in range(2):
+            scene = synthetic.make_scene(cfg, 60 + e)
+            env = build_env(envs, scene)
+            rw, rl = scene['room_width'], scene['room_length']
+            for a in range(len(scene['robots'])):
+                m = envs.Mapper(env, env.robots[a])
+                H, W = scene['H'], scene['W']
+                X, Y = synthetic.pixel_center_positions(H, W)
+                points = np.stack([X, Y, np.full_like(X, 0.02)], axis=2)
+                seg = np.where(scene['occupancy'][a] == 1, K.SEG_VALUES['obstacle'], K.SEG_VALUES['floor'])
+                m.global_occupancy_map.update(points, seg, K.SEG_VALUES['obstacle'])
+                pos = scene['robots'][a]['position']
+                for q in range(12):
+                    src = pos if q < 6 else (float(rs.uniform(-rl / 2, rl / 2)), float(rs.uniform(-rw / 2, rw / 2)), 0)
+                    # half of the targets on the other side of x = 0 (around the divider, if any)
+                    tx = float(rs.uniform(0.05, rl / 2)) * (-np.sign(src[0]) if q % 2 == 0 else 1.0)
+                    tgt = (tx if q % 2 == 0 else float(rs.uniform(-rl / 2, rl / 2)), float(rs.uniform(-rw / 2, rw / 2)), 0)
+                    path = m.shortest_path(src, tgt)
+                    key = '%s_e%d_a%d_q%d' % (cfg, e, a, q)
+                    out[key + '_src'] = np.array(src[:2], dtype=np.float64)
+                    out[key + '_tgt'] = np.array(tgt[:2], dtype=np.float64)
+                    out[key + '_path'] = np.array([p[:2] for p in path], dtype=np.float64)
+    cs = np.load(os.path.join(REF, 'shortest_paths', 'sample-configuration-space.npy'), allow_pickle=False).astype(np.uint8)
+    g = sp.GridGraph(np.ascontiguousarray(cs))
+    for q, (s_, t_) in enumerate([((75, 156), (131, 112)), ((131, 112), (75, 156)), ((60, 60), (140, 170))]):
+        out['demo_%d_src' % q] = np.array(s_, dtype=np.int32)
+        out['demo_%d_tgt' % q] = np.array(t_, dtype=np.int32)
+        out['demo_%d_path' % q] = np.array(g.shortest_path(s_, t_), dtype=np.int32).reshape(-1, 2)
+    np.savez_compressed(os.path.join(HERE, 'paths.npz'), **out)
+    print('wrote paths goldens')
+
+
 def main():
     envs, sp = import_reference()
     which = sys.argv[1:] or ['micro', 'scenes']
@@ -332,6 +371,8 @@ def main():
         gen_scenes(envs)
     if 'sp_distance' in which or not sys.argv[1:]:
         gen_sp_distance(envs)
+    if 'paths' in which or not sys.argv[1:]:
+        gen_paths(envs, sp)
 
 
 if __name__ == '__main__':

@@ -128,3 +128,33 @@ def test_distance_to_receptacle_dropin(V):
         for a in range(len(s['robots'])):
             ao = O.AgentOracle(s, a)
             assert got[e][a] == [ao.shortest_path_distance(s['receptacle_position'], p) for p in pos[e][a]]
+
+
+def test_shortest_path_reference_goldens(V):
+    """Movement paths through simaps_shortest_path vs the reference's own
+    OccupancyMap.shortest_path outputs (straight-line test, EDT snap, exact SPFA parents,
+    approximate_polygon, line-of-sight pruning)."""
+    synthetic, vector_env = V
+    from simaps import batch
+    z = G.load('paths.npz')
+    groups = {}
+    for k in z.files:
+        if not k.endswith('_path') or k.startswith('demo'):
+            continue
+        key = k[:-len('_path')]
+        head, q = key.rsplit('_q', 1)
+        cfg, rest = head.rsplit('_e', 1)
+        e, a = (int(x) for x in rest.split('_a'))
+        groups.setdefault(cfg, []).append((e, a, key))
+    nontrivial = 0
+    for cfg, items in groups.items():
+        scenes = [synthetic.make_scene(cfg, 60 + e) for e in range(2)]
+        b = batch.StateBatch(scenes)
+        slots = [b.agents.index((e, a)) for e, a, _ in items]
+        got = b.shortest_paths(np.stack([z[k + '_src'] for _, _, k in items]),
+                               np.stack([z[k + '_tgt'] for _, _, k in items]), slots=slots)
+        for (e, a, key), path in zip(items, got):
+            want = z[key + '_path']
+            nontrivial += len(want) > 2
+            assert np.array_equal(np.array([p[:2] for p in path]), want), key
+    assert nontrivial >= 40

@@ -141,3 +141,23 @@ def test_oracle_shortest_path_distance_vs_reference():
         src = z[key + '_src']
         got = [ao.shortest_path_distance((src[0], src[1]), (x, y)) for x, y in z[key + '_queries']]
         assert got == list(z[key + '_dist']), key
+
+
+def test_oracle_shortest_path_vs_reference():
+    """Movement paths: OccupancyMap.shortest_path / GridGraph.shortest_path
+    (envs.py:2478-2505, pyx:121-154) from the reference itself, exactly."""
+    from simaps import synthetic
+    z = G.load('paths.npz')
+    keys = sorted(k[:-len('_path')] for k in z.files if k.endswith('_path') and not k.startswith('demo'))
+    cache = {}
+    for key in keys:
+        head, q = key.rsplit('_q', 1)
+        cfg, rest = head.rsplit('_e', 1)
+        e, a = (int(x) for x in rest.split('_a'))
+        if (cfg, e, a) not in cache:
+            cache[(cfg, e, a)] = O.AgentOracle(synthetic.make_scene(cfg, 60 + e), a)
+        got = np.array(cache[(cfg, e, a)].shortest_path(z[key + '_src'], z[key + '_tgt']), dtype=np.float64)
+        assert np.array_equal(got, z[key + '_path']), key
+    for q in range(3):
+        got = np.array(O.grid_shortest_path(G.load('sssp.npz')['demo_cspace'], z['demo_%d_src' % q], z['demo_%d_tgt' % q]))
+        assert np.array_equal(got.reshape(-1, 2), z['demo_%d_path' % q]), q
