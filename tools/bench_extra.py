@@ -1,0 +1,95 @@
+"""Throughput of the SURVEY.md 8(f) rows built so far, GPU vs the CPU oracle (1 core):
+
+  sp_distance    OccupancyMap.shortest_path_distance (reward lookups): queries/s
+  shortest_path  OccupancyMap.shortest_path (movement paths): paths/s
+
+    python tools/bench_extra.py [--config lifting_4-small_divider] [--envs 64] [--queries 8]
+
+Prints one JSON line per row.  Inputs resident in HBM; timing with torch.cuda events around K
+launches after warm-up.  The CPU leg times the oracle (the checker) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'spatial-intention-maps_amd'))
+sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from simaps import batch, synthetic  # noqa: E402
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', default='lifting_4-small_divider')
+    ap.add_argument('--envs', type=int, default=64)
+    ap.add_argument('--queries', type=int, default=8, help='reward-lookup targets per agent')
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--cpu-budget', type=float, default=8.0)
+    args = ap.parse_args()
+    import oracle
+    scenes = [synthetic.make_scene(args.config, e) for e in range(args.envs)]
+    b = batch.StateBatch(scenes)
+    rs = np.random.RandomState(0)
+    s0 = scenes[0]
+    rl, rw = s0['room_length'], s0['room_width']
+    N, Q = b.N, args.queries
+    rec = s0['receptacle_position']
+    src = np.array([rec[:2] if rec is not None else scenes[e]['robots'][a]['position'][:2] for e, a in b.agents])
+    tgt = np.stack([rs.uniform(-rl / 2, rl / 2, (N, Q)), rs.uniform(-rw / 2, rw / 2, (N, Q))], -1)
+    src_d = torch.as_tensor(src).cuda()
+    tgt_d = torch.as_tensor(tgt).cuda()
+    dt = timed(lambda: b.shortest_path_distances(src_d, tgt_d), args.steps, 3)
+    # CPU oracle on a bounded sample
+    n, el = 0, 0.0
+    for (e, a) in b.agents:
+        t0 = time.perf_counter()
+        ao = oracle.AgentOracle(scenes[e], a)
+        k = b.agents.index((e, a))
+        for q in range(Q):
+            ao.shortest_path_distance(src[k], tgt[k, q])
+        el += time.perf_counter() - t0
+        n += Q
+        if el > args.cpu_budget:
+            break
+    print(json.dumps({'row': 'sp_distance', 'config': args.config, 'agents': N, 'queries_per_agent': Q,
+                      'gpu_queries_per_s': N * Q / dt, 'gpu_ms_per_launch': dt * 1e3,
+                      'cpu_oracle_queries_per_s': n / el, 'cpu_cores': 1,
+                      'cpu_sample': '%d queries incl. each agent\'s cspace / EDT / SPFA' % n}), flush=True)
+
+    # movement paths: robot position -> random target (half across x = 0)
+    psrc = np.array([scenes[e]['robots'][a]['position'][:2] for e, a in b.agents])
+    ptgt = np.stack([rs.uniform(0.05, rl / 2, N) * -np.sign(psrc[:, 0]), rs.uniform(-rw / 2, rw / 2, N)], -1)
+    dt = timed(lambda: b.shortest_paths(psrc, ptgt), max(3, args.steps // 4), 1)
+    n, el = 0, 0.0
+    for k, (e, a) in enumerate(b.agents):
+        t0 = time.perf_counter()
+        oracle.AgentOracle(scenes[e], a).shortest_path(psrc[k], ptgt[k])
+        el += time.perf_counter() - t0
+        n += 1
+        if el > args.cpu_budget:
+            break
+    print(json.dumps({'row': 'shortest_path', 'config': args.config, 'paths_per_launch': N,
+                      'gpu_paths_per_s': N / dt, 'gpu_ms_per_launch_incl_d2h': dt * 1e3,
+                      'cpu_oracle_paths_per_s': n / el, 'cpu_cores': 1,
+                      'cpu_sample': '%d paths incl. each agent\'s cspace / EDT / SPFA' % n}), flush=True)
+
+
+if __name__ == '__main__':
+    main()
