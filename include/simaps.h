@@ -21,6 +21,9 @@
  *   simaps_shortest_path <- OccupancyMap.shortest_path (envs.py:2478-2505) + GridGraph.shortest_path
  *                          (shortest_paths.pyx:121-154): the movement path of Robot.store_new_action
  *                          (envs.py:875-876), batched, exact SPFA parents.
+ *   simaps_ingest       <- Robot.update_map minus the simulator: Camera.capture_image on a given depth /
+ *                          segmentation frame (envs.py:1927-1955), Mapper.update (2056-2062) and the
+ *                          obstacle scatter of OccupancyMap.update (2447-2450), in place, batched.
  *   simaps_robot_mask   <- Mapper._create_robot_mask (envs.py:2218-2242) (host helper).
  *   simaps_num_channels <- the channel list of Mapper.get_state (envs.py:2071-2113).
  */
@@ -117,6 +120,19 @@ typedef struct simaps_config {
     double intention_channel_nonspatial_scale;
 } simaps_config;
 
+/* A robot camera (Camera subclasses, envs.py:1876-2008): image size and projection constants. */
+typedef struct simaps_camera {
+    int32_t height_px, width_px; /* int(1.63 * 96), int(ASPECT * height) (envs.py:1895-1896) */
+    double near_m, far_m;        /* Camera.NEAR, Camera.FAR */
+    double cx2, cy2;             /* 2 * limit_x, 2 * limit_y, limit_y = tan(radians(FOV / 2)) (1944-1947) */
+} simaps_camera;
+
+/* Segmentation body ids of one env (Camera._ensure_initialized, envs.py:1907-1917). */
+typedef struct simaps_seg_ids {
+    int32_t min_obstacle, max_obstacle, receptacle, min_cube, max_cube;
+    int32_t has_receptacle;      /* receptacle_id is not None */
+} simaps_seg_ids;
+
 /* Optional per-agent intermediates (device pointers, any may be NULL), for parity tests. */
 typedef struct simaps_debug {
     uint8_t *cspace;   /* [N, room_h, room_w] OccupancyMap.configuration_space inside the room rect */
@@ -166,6 +182,16 @@ int simaps_sp_distance(const simaps_config *cfg, int N, const simaps_agent *agen
 int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
                          const simaps_robot *robots, const uint8_t *occupancy, const double *sources,
                          const double *targets, int max_points, double *out_xy, int32_t *out_count, void *stream);
+
+/* Batched observation ingest into the per-agent maps (occupancy / overhead [M, H, W], slot
+ *   agents[n].map_slot), from depth [N][Hc][Wc] float32 (pybullet depth buffer) and seg_raw
+ *   [N][Hc][Wc] int32 (body ids), cam_params [N][9] fp64 = _get_camera_params(robot pose)
+ *   (position, target, up; envs.py:1962-2008), seg_ids [E] per env.  keys: uint64 [M, H, W] scratch,
+ *   all zero on entry and left zero.  All DEVICE.  Points with equal z on one pixel: the later
+ *   camera pixel wins (the reference's np.argsort leaves that order unspecified). */
+int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, const simaps_agent *agents,
+                  const simaps_seg_ids *seg_ids, const double *cam_params, const float *depth, const int32_t *seg_raw,
+                  float *overhead, uint8_t *occupancy, uint64_t *keys, void *stream);
 
 /* Batched GridGraph(grid).shortest_path_image(source):
  *   grids [B, H, W] uint8 (nonzero = free), sources [B, 2] int32 (row, col), out dists [B, H, W]

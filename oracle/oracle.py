@@ -150,6 +150,52 @@ def grid_shortest_path(grid_u8, source, target):
     return path[::-1]
 
 
+def ingest(overhead, occupancy, depth_buffer, seg_raw, cam_params, spec, seg_ids, has_receptacle):
+    """Robot.update_map minus the simulator: Camera.capture_image (envs.py:1927-1955) on a given
+    (depth buffer, segmentation) frame, then Mapper.update (2056-2062) and the obstacle scatter of
+    OccupancyMap.update (2447-2450), in place on (overhead f32 [H, W], occupancy u8 [H, W]).
+    numpy float32 throughout, op for op (np.dot / np.linalg.norm of float32 3-vectors: float32
+    products summed in double -- OpenBLAS sdot -- which is what numpy does here)."""
+    FAR, NEAR = spec.far, spec.near
+    Hc, Wc = depth_buffer.shape
+    depth = FAR * NEAR / (FAR - (FAR - NEAR) * depth_buffer)
+    camera_position = np.array(cam_params[0:3], dtype=np.float32)
+    principal = np.array(cam_params[3:6], dtype=np.float32) - camera_position
+    principal = principal / np.linalg.norm(principal)
+    camera_up = np.array(cam_params[6:9], dtype=np.float32)
+    up = camera_up - np.dot(camera_up, principal) * principal
+    up = up / np.linalg.norm(up)
+    right = np.cross(principal, up)
+    right = right / np.linalg.norm(right)
+    limit_y = math.tan(math.radians(60 / 2))
+    limit_x = limit_y * spec.aspect
+    pixel_x = (2 * limit_x) * (np.arange(Wc, dtype=np.float32) / Wc - 0.5)
+    pixel_y = (2 * limit_y) * (0.5 - (np.arange(Hc, dtype=np.float32) + 1) / Hc)
+    pixel_xv, pixel_yv = np.meshgrid(pixel_x, pixel_y)
+    points = camera_position + depth[:, :, np.newaxis] * (principal + pixel_xv[:, :, np.newaxis] * right
+                                                          + pixel_yv[:, :, np.newaxis] * up)
+    seg = 0.125 * (seg_raw == 0).astype(np.float32)
+    seg += 0.25 * np.logical_and(seg_raw >= seg_ids['min_obstacle'], seg_raw <= seg_ids['max_obstacle']).astype(np.float32)
+    if has_receptacle:
+        seg += 0.375 * (seg_raw == seg_ids['receptacle']).astype(np.float32)
+    seg += 0.5 * np.logical_and(seg_raw >= seg_ids['min_cube'], seg_raw <= seg_ids['max_cube']).astype(np.float32)
+    shape = overhead.shape
+
+    def pix(px, py):  # Mapper.position_to_pixel_indices on float32 arrays (envs.py:2391-2397)
+        i = np.floor(shape[0] / 2 - py * PPM).astype(np.int32)
+        j = np.floor(shape[1] / 2 + px * PPM).astype(np.int32)
+        return np.clip(i, 0, shape[0] - 1), np.clip(j, 0, shape[1] - 1)
+
+    aug = np.concatenate((points, seg[:, :, np.newaxis]), axis=2).reshape(-1, 4)
+    aug = aug[np.argsort(aug[:, 2], kind='stable')]  # ties: later camera pixel wins (see ingest docs)
+    i, j = pix(aug[:, 0], aug[:, 1])
+    overhead[i, j] = aug[:, 3]
+    aug = np.concatenate([points, np.isclose(seg[:, :, np.newaxis], 0.25)], axis=2).reshape(-1, 4)
+    obs = aug[np.isclose(aug[:, 3], 1)]
+    i, j = pix(obs[:, 0], obs[:, 1])
+    occupancy[i, j] = 1
+
+
 def edt_indices(img):
     """scipy.ndimage.distance_transform_edt(img, return_distances=False, return_indices=True)."""
     a = np.ascontiguousarray(img != 0, dtype=np.uint8)

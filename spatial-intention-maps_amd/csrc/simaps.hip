@@ -1640,6 +1640,122 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Observation ingest: Robot.update_map minus the simulator (envs.py:925, 2056-2066): the camera frame
+// -> point cloud (Camera.capture_image, envs.py:1927-1955) -> overhead map (highest point per pixel:
+// argsort by z + last write) and occupancy map (obstacle points, OccupancyMap.update 2447-2450).
+// numpy float32 semantics op for op; np.dot / np.linalg.norm of float32 3-vectors = float32 products
+// summed in double (OpenBLAS sdot), np.cross = (a1 b2 - a2 b1, ...).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float dot3f(const float *a, const float *b)
+{
+    return (float)((((double)(a[0] * b[0])) + (double)(a[1] * b[1])) + (double)(a[2] * b[2]));
+}
+
+// numpy float32 -> int32 cast (x86 cvttss2si): NaN / out of range -> INT_MIN
+__device__ __forceinline__ int np_f32_to_i32(float v)
+{
+    return (v >= -2147483648.0f && v < 2147483648.0f) ? (int)v : INT32_MIN;
+}
+
+__global__ void __launch_bounds__(NT) ingest_kernel(simaps_config cfg, simaps_camera cam,
+                                                    const simaps_agent *__restrict__ agents,
+                                                    const simaps_seg_ids *__restrict__ seg_ids,
+                                                    const double *__restrict__ cam_params,
+                                                    const float *__restrict__ depth, const int32_t *__restrict__ seg_raw,
+                                                    float *__restrict__ overhead, uint8_t *__restrict__ occupancy,
+                                                    unsigned long long *__restrict__ keys)
+{
+    __shared__ float F[12];  // camera position, principal, up, right (float32)
+    const int n = blockIdx.x, tid = threadIdx.x;
+    const int H = cfg.H, W = cfg.W, Hc = cam.height_px, Wc = cam.width_px, NP = Hc * Wc;
+    const simaps_agent ag = agents[n];
+    const simaps_seg_ids ids = seg_ids[ag.env];
+    if (tid == 0) {
+        const double *P = cam_params + 9 * (size_t)n;
+        float cp[3], pr[3], cu[3], up[3], rt[3];
+        for (int c = 0; c < 3; c++) {
+            cp[c] = (float)P[c];
+            pr[c] = (float)P[3 + c] - cp[c];
+            cu[c] = (float)P[6 + c];
+        }
+        const float n1 = sqrtf(dot3f(pr, pr));
+        for (int c = 0; c < 3; c++) pr[c] = pr[c] / n1;
+        const float d = dot3f(cu, pr);
+        for (int c = 0; c < 3; c++) up[c] = cu[c] - d * pr[c];
+        const float n2 = sqrtf(dot3f(up, up));
+        for (int c = 0; c < 3; c++) up[c] = up[c] / n2;
+        rt[0] = pr[1] * up[2] - pr[2] * up[1];
+        rt[1] = pr[2] * up[0] - pr[0] * up[2];
+        rt[2] = pr[0] * up[1] - pr[1] * up[0];
+        const float n3 = sqrtf(dot3f(rt, rt));
+        for (int c = 0; c < 3; c++) {
+            F[c] = cp[c];
+            F[3 + c] = pr[c];
+            F[6 + c] = up[c];
+            F[9 + c] = rt[c] / n3;
+        }
+    }
+    __syncthreads();
+    const float c1 = (float)(cam.far_m * cam.near_m), cfar = (float)cam.far_m, cfn = (float)(cam.far_m - cam.near_m);
+    const float cx2 = (float)cam.cx2, cy2 = (float)cam.cy2;
+    const float h2 = (float)((double)H / 2), w2 = (float)((double)W / 2);
+    const float *db = depth + (size_t)n * NP;
+    const int32_t *raw = seg_raw + (size_t)n * NP;
+    const size_t base = (size_t)ag.map_slot * H * W;
+    // point k -> (map pixel, z key, seg); the same float32 expression in every pass
+    auto point = [&](int k, int &pix, unsigned long long &key, float &seg) {
+        const int i = k / Wc, j = k - i * Wc;
+        const float dep = c1 / (cfar - cfn * db[k]);
+        const float px = cx2 * ((float)j / (float)Wc - 0.5f);
+        const float py = cy2 * (0.5f - ((float)i + 1.0f) / (float)Hc);
+        float p[3];
+        for (int c = 0; c < 3; c++) {
+            float t = F[3 + c] + px * F[9 + c];
+            t = t + py * F[6 + c];
+            p[c] = F[c] + dep * t;
+        }
+        const int r = raw[k];
+        seg = 0.125f * (r == 0 ? 1.0f : 0.0f);
+        seg += 0.25f * ((r >= ids.min_obstacle && r <= ids.max_obstacle) ? 1.0f : 0.0f);
+        if (ids.has_receptacle) seg += 0.375f * (r == ids.receptacle ? 1.0f : 0.0f);
+        seg += 0.5f * ((r >= ids.min_cube && r <= ids.max_cube) ? 1.0f : 0.0f);
+        int pi = np_f32_to_i32(floorf(h2 - p[1] * 96.0f)), pj = np_f32_to_i32(floorf(w2 + p[0] * 96.0f));
+        pi = pi < 0 ? 0 : (pi > H - 1 ? H - 1 : pi);
+        pj = pj < 0 ? 0 : (pj > W - 1 ? W - 1 : pj);
+        pix = pi * W + pj;
+        // np.argsort order by z: float bits made unsigned-monotone, NaN last; equal z -> later pixel
+        const unsigned zb = __float_as_uint(p[2]);
+        const unsigned zk = p[2] != p[2] ? 0xffffffffu : ((zb & 0x80000000u) ? ~zb : (zb | 0x80000000u));
+        key = ((unsigned long long)zk << 32) | (unsigned)(k + 1);
+    };
+    for (int k = tid; k < NP; k += NT) {
+        int pix;
+        unsigned long long key;
+        float seg;
+        point(k, pix, key, seg);
+        if (seg == 0.25f) occupancy[base + pix] = 1;  // np.isclose(seg, obstacle) (seg values are exact)
+        atomicMax(&keys[base + pix], key);
+    }
+    __syncthreads();
+    for (int k = tid; k < NP; k += NT) {  // the highest point of each pixel writes its seg value
+        int pix;
+        unsigned long long key;
+        float seg;
+        point(k, pix, key, seg);
+        if (__hip_atomic_load(&keys[base + pix], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key)
+            overhead[base + pix] = seg;
+    }
+    __syncthreads();
+    for (int k = tid; k < NP; k += NT) {  // leave the scratch zeroed for the next frame
+        int pix;
+        unsigned long long key;
+        float seg;
+        point(k, pix, key, seg);
+        keys[base + pix] = 0ull;
+    }
+}
+
 }  // namespace
 
 // =================================================================================================
@@ -1811,6 +1927,25 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
                        occupancy, sources, targets, max_points, out_xy, out_count);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "shortest_path launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, const simaps_agent *agents,
+                  const simaps_seg_ids *seg_ids, const double *cam_params, const float *depth, const int32_t *seg_raw,
+                  float *overhead, uint8_t *occupancy, uint64_t *keys, void *stream)
+{
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (!cam || cam->height_px <= 0 || cam->width_px <= 0 || !(cam->far_m > cam->near_m) || !(cam->near_m > 0))
+        return fail(SIMAPS_EINVAL, "bad camera");
+    if (N < 0) return fail(SIMAPS_EINVAL, "N < 0");
+    if (N == 0) return 0;
+    if (!agents || !seg_ids || !cam_params || !depth || !seg_raw || !overhead || !occupancy || !keys)
+        return fail(SIMAPS_EINVAL, "NULL buffer");
+    hipLaunchKernelGGL(ingest_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids, cam_params,
+                       depth, seg_raw, overhead, occupancy, reinterpret_cast<unsigned long long *>(keys));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "ingest launch: %s", hipGetErrorString(e));
     return 0;
 }
 

@@ -32,6 +32,16 @@ AGENT_DTYPE = np.dtype([('env', '<i4'), ('robot', '<i4'), ('map_slot', '<i4')], 
 assert ROBOT_DTYPE.itemsize == 72 and ENV_DTYPE.itemsize == 32 and AGENT_DTYPE.itemsize == 12
 
 
+SEG_IDS_DTYPE = np.dtype([('min_obstacle', '<i4'), ('max_obstacle', '<i4'), ('receptacle', '<i4'),
+                          ('min_cube', '<i4'), ('max_cube', '<i4'), ('has_receptacle', '<i4')], align=True)
+
+
+class Camera(ctypes.Structure):
+    """simaps_camera (include/simaps.h)."""
+    _fields_ = [('height_px', ctypes.c_int32), ('width_px', ctypes.c_int32), ('near_m', ctypes.c_double),
+                ('far_m', ctypes.c_double), ('cx2', ctypes.c_double), ('cy2', ctypes.c_double)]
+
+
 class Config(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         'H', 'W', 'room_i0', 'room_j0', 'room_h', 'room_w', 'use_robot_map', 'use_distance_to_receptacle_map',
@@ -70,6 +80,8 @@ def _load():
     L.simaps_sp_distance.restype = i32
     L.simaps_shortest_path.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.simaps_shortest_path.restype = i32
+    L.simaps_ingest.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(Camera), i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.simaps_ingest.restype = i32
     L.simaps_sssp_grid.argtypes = [i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp]
     L.simaps_sssp_grid.restype = i32
     if L.simaps_abi_version() != ABI_VERSION:
@@ -80,7 +92,7 @@ def _load():
 lib = _load()
 
 EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_num_channels', 'simaps_robot_mask',
-            'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_sssp_grid')
+            'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest', 'simaps_sssp_grid')
 
 
 def check(rc):

@@ -237,6 +237,7 @@ class StateBatch:
         out = torch.empty((n, Q), dtype=torch.float64, device=self.device)
         if n == 0 or Q == 0:
             return out
+        self._inflight = (src, tgt)  # alive until the next call (async launch)
         _lib.check(_lib.lib.simaps_sp_distance(
             self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d), _lib.ptr(self.occupancy),
             _lib.ptr(src), _lib.ptr(tgt), Q, _lib.ptr(out), _lib.stream_handle(stream)))
@@ -264,6 +265,43 @@ class StateBatch:
         if (cnt < 0).any():
             raise RuntimeError('a path has %d waypoints > max_points=%d' % (-cnt.min(), max_points))
         return [[(float(x), float(y), 0) for x, y in xy[k, :cnt[k]]] for k in range(n)]
+
+
+    def ingest(self, depth, seg_raw, camera='forward', slots=None, seg_ids=None, stream=None):
+        """Robot.update_map minus the simulator (envs.py:925, 2056-2066) for map slots `slots` (all
+        agents if None): each robot's camera frame -- depth buffer [n, Hc, Wc] float32 and
+        segmentation body ids [n, Hc, Wc] int32, as pybullet getCameraImage returns them -- becomes a
+        point cloud that updates the robot's overhead and occupancy maps in place on the device.
+        camera: 'forward' (use_partial_observations) or 'overhead'; seg_ids: per-env dict of body ids
+        (default: the synthetic scenes' ids).  The camera pose comes from the current descriptor."""
+        from . import camera as cam_mod, synthetic
+        spec = cam_mod.CAMERAS[camera]
+        agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
+        idx = list(range(self.N)) if slots is None else [int(k) for k in slots]
+        dep = torch.as_tensor(depth).to(device=self.device, dtype=torch.float32).contiguous()
+        seg = torch.as_tensor(seg_raw).to(device=self.device, dtype=torch.int32).contiguous()
+        want = (n, spec.height_px, spec.width_px)
+        if tuple(dep.shape) != want or tuple(seg.shape) != want:
+            raise ValueError('depth and seg_raw must be %s' % (want,))
+        params = np.array([spec.params(self.scenes[e]['robots'][a]['position'][0], self.scenes[e]['robots'][a]['position'][1],
+                                       self.scenes[e]['robots'][a]['heading']) for e, a in (self.agents[k] for k in idx)],
+                          dtype=np.float64).reshape(n, 9)
+        ids = np.zeros(len(self.scenes), dtype=_lib.SEG_IDS_DTYPE)
+        for e, sc in enumerate(self.scenes):
+            d = (seg_ids[e] if seg_ids is not None else synthetic.SEG_IDS)
+            for f in ('min_obstacle', 'max_obstacle', 'receptacle', 'min_cube', 'max_cube'):
+                ids[e][f] = d[f]
+            ids[e]['has_receptacle'] = sc['receptacle_position'] is not None
+        if getattr(self, '_keys', None) is None:
+            self._keys = torch.zeros((self.N, self.H, self.W), dtype=torch.int64, device=self.device)
+        cam = _lib.Camera(spec.height_px, spec.width_px, spec.near, spec.far, spec.cx2, spec.cy2)
+        if n == 0:
+            return
+        ids_d, params_d = _to_dev(ids, self.device), torch.from_numpy(params).to(self.device)
+        self._inflight = (ids_d, params_d, dep, seg)  # alive until the next call (async launch)
+        _lib.check(_lib.lib.simaps_ingest(
+            self.cfg, cam, n, _lib.ptr(agents_d), _lib.ptr(ids_d), _lib.ptr(params_d), _lib.ptr(dep), _lib.ptr(seg),
+            _lib.ptr(self.overhead), _lib.ptr(self.occupancy), _lib.ptr(self._keys), _lib.stream_handle(stream)))
 
 
 def sssp_grid(grids, sources, window=None, stream=None):

@@ -242,3 +242,63 @@ def history_path(robot):
     """RobotController.get_history_path (envs.py:1478-1479)."""
     idx = robot['waypoint_index']
     return list(robot['waypoint_positions'][:idx]) + [robot['position']]
+
+
+# Body ids of the synthetic scenes' segmentation masks (pybullet getCameraImage seg buffer):
+# 0 = floor plane, obstacles 1..2, cubes 3..4, receptacle 99, robot k = 10 + k, -1 = background.
+SEG_IDS = {'min_obstacle': 1, 'max_obstacle': 2, 'min_cube': 3, 'max_cube': 4, 'receptacle': 99}
+
+
+def camera_images(scene, agent, kind='forward', seed=0):
+    """A synthetic pybullet-like frame of robot `agent`'s camera (Camera.capture_image input,
+    envs.py:1927-1930): (depth_buffer float32 [Hc, Wc] in [0, 1], seg_raw int32 [Hc, Wc]).
+
+    Rays of the camera model hit a floor whose pixels carry the scene's classes at class heights
+    (walls 0.1 m, cubes 0.044 m, robots 0.07 m), plus tiny depth noise so that no two points share
+    a z value (the reference's argsort breaks z ties in an unspecified order)."""
+    from .camera import CAMERAS
+    spec = CAMERAS[kind]
+    rs = np.random.RandomState(seed)
+    r = scene['robots'][agent]
+    pos, tgt, up = np.array(spec.params(r['position'][0], r['position'][1], r['heading'])).reshape(3, 3)
+    principal = tgt - pos
+    principal /= np.linalg.norm(principal)
+    up = up - np.dot(up, principal) * principal
+    up /= np.linalg.norm(up)
+    right = np.cross(principal, up)
+    right /= np.linalg.norm(right)
+    Hc, Wc = spec.height_px, spec.width_px
+    px = spec.cx2 * (np.arange(Wc) / Wc - 0.5)
+    py = spec.cy2 * (0.5 - (np.arange(Hc) + 1) / Hc)
+    d = principal[None, None, :] + px[None, :, None] * right[None, None, :] + py[:, None, None] * up[None, None, :]
+    H, W = scene['H'], scene['W']
+    seg_truth = scene['seg_truth']
+
+    def classify(x, y):
+        pi = np.clip(np.floor(H / 2 - y * K.LOCAL_MAP_PIXELS_PER_METER).astype(np.int64), 0, H - 1)
+        pj = np.clip(np.floor(W / 2 + x * K.LOCAL_MAP_PIXELS_PER_METER).astype(np.int64), 0, W - 1)
+        s = seg_truth[pi, pj]
+        raw = np.full(x.shape, -1, dtype=np.int32)
+        raw[s == K.SEG_VALUES['floor']] = 0
+        raw[s == K.SEG_VALUES['obstacle']] = 1 + (pi[s == K.SEG_VALUES['obstacle']] % 2)
+        raw[s == K.SEG_VALUES['receptacle']] = SEG_IDS['receptacle']
+        raw[s == K.SEG_VALUES['cube']] = 3 + (pj[s == K.SEG_VALUES['cube']] % 2)
+        for k, o in enumerate(scene['robots']):
+            if k != agent:
+                raw[(x - o['position'][0]) ** 2 + (y - o['position'][1]) ** 2 <= 0.05 ** 2] = 10 + k
+        return raw
+
+    height = {-1: 0.0, 0: 0.0, 1: 0.1, 2: 0.1, 3: 0.044, 4: 0.044, SEG_IDS['receptacle']: 0.001}
+    down = d[..., 2] < -1e-9
+    depth = np.full((Hc, Wc), float(spec.far))
+    t0 = np.where(down, -pos[2] / np.where(down, d[..., 2], -1.0), np.inf)
+    raw = classify(pos[0] + t0 * d[..., 0], pos[1] + t0 * d[..., 1])
+    h = np.vectorize(lambda v: height.get(int(v), 0.07))(raw)
+    t = np.where(down, (h - pos[2]) / np.where(down, d[..., 2], -1.0), np.inf)
+    t = np.where(t > 0, t, t0)
+    depth = np.where(down, np.minimum(t, spec.far), spec.far)
+    raw = np.where(down & (t <= spec.far), raw, -1).astype(np.int32)
+    depth = np.maximum(depth, spec.near)
+    db = (spec.far - spec.far * spec.near / depth) / (spec.far - spec.near)
+    db = np.clip(db + rs.uniform(-2e-6, 2e-6, db.shape), 0.0, 1.0).astype(np.float32)
+    return db, raw

@@ -362,6 +362,70 @@ def gen_paths(envs, sp):
     print('wrote paths goldens')
 
 
+class _FakeCameraP(_FakeP):
+    """env.p for Camera.capture_image: getCameraImage returns a given (depth, seg) frame."""
+    frame = None
+
+    def computeViewMatrix(self, *a, **k):
+        return None
+
+    def getCameraImage(self, w, h, view, proj):
+        db, raw = self.frame
+        assert db.shape == (h, w)
+        return w, h, None, db.copy(), raw.copy()
+
+
+def gen_ingest(envs):
+    """Observation ingest: Robot.update_map -> Mapper.update (envs.py:
+    2056-2066) = Camera.capture_image point cloud (1927-1955), overhead scatter (argsort by z),
+    OccupancyMap.update obstacle scatter (2447-2450), from given depth / segmentation frames."""
+    out = {}
+    for cfg, partial in (('lifting_4-small_divider', True), ('pushing_4-large_empty', False)):
+        scene = synthetic.make_scene(cfg, 80)
+        env = build_env(envs, scene)
+        env.use_partial_observations = partial
+        env.p = _FakeCameraP()
+        for a in range(2):
+            m = envs.Mapper(env, env.robots[a])
+            m.global_overhead_map_without_robots[:] = scene['overhead'][a]
+            m.global_occupancy_map.occupancy_map[:] = scene['occupancy'][a]
+            db, raw = synthetic.camera_images(scene, a, 'forward' if partial else 'overhead', seed=100 + a)
+            # no two points with equal z may land on one map pixel with different seg values (the
+            # reference's argsort breaks z ties in an unspecified order): nudge such depths by a
+            # random number of float32 ulps until none is left
+            for it in range(100):
+                env.p.frame = (db, raw)
+                pts, sg = m.camera.capture_image(env.robots[a].get_position(), env.robots[a].get_heading())
+                pts = pts.reshape(-1, 3)
+                pi, pj = envs.Mapper.position_to_pixel_indices(pts[:, 0], pts[:, 1], m.global_overhead_map_without_robots.shape)
+                key = np.stack([pi, pj, pts[:, 2].view(np.int32)], 1)
+                order = np.lexsort(key.T[::-1])
+                ks, sgs = key[order], sg.ravel()[order]
+                same = np.all(ks[1:] == ks[:-1], axis=1) & (sgs[1:] != sgs[:-1])
+                dup = np.zeros(len(order), bool)
+                dup[order[1:][same]] = True
+                if not dup.any():
+                    break
+                flat = db.ravel().copy()
+                step = np.random.RandomState(it).randint(1, 64, int(dup.sum()))
+                for _ in range(int(step.max())):
+                    mv = dup.copy()
+                    mv[dup] = step > 0
+                    flat[mv] = np.nextafter(flat[mv], np.float32(0))
+                    step -= 1
+                db = flat.reshape(db.shape)
+            assert not dup.any(), 'could not break the z ties'
+            env.p.frame = (db, raw)
+            m.update()
+            key = '%s_a%d' % (cfg, a)
+            out[key + '_depth'] = db
+            out[key + '_seg'] = raw.astype(np.int8)
+            out[key + '_overhead'] = m.global_overhead_map_without_robots.astype(np.float32)
+            out[key + '_occupancy'] = m.global_occupancy_map.occupancy_map.astype(np.uint8)
+    np.savez_compressed(os.path.join(HERE, 'ingest.npz'), **out)
+    print('wrote ingest goldens')
+
+
 def main():
     envs, sp = import_reference()
     which = sys.argv[1:] or ['micro', 'scenes']
@@ -373,6 +437,8 @@ def main():
         gen_sp_distance(envs)
     if 'paths' in which or not sys.argv[1:]:
         gen_paths(envs, sp)
+    if 'ingest' in which or not sys.argv[1:]:
+        gen_ingest(envs)
 
 
 if __name__ == '__main__':

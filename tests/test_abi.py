@@ -18,7 +18,7 @@ def declared_symbols():
 
 
 def test_header_declares_the_abi():
-    assert declared_symbols() == sorted(['simaps_abi_version', 'simaps_last_error', 'simaps_num_channels', 'simaps_sp_distance', 'simaps_shortest_path',
+    assert declared_symbols() == sorted(['simaps_abi_version', 'simaps_last_error', 'simaps_num_channels', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest',
                                          'simaps_robot_mask', 'simaps_get_state', 'simaps_sssp_grid'])
 
 

@@ -158,3 +158,46 @@ def test_shortest_path_reference_goldens(V):
             nontrivial += len(want) > 2
             assert np.array_equal(np.array([p[:2] for p in path]), want), key
     assert nontrivial >= 40
+
+
+def test_ingest_reference_goldens(V):
+    """Observation ingest through simaps_ingest vs the reference's own
+    Mapper.update on the committed frames (forward-facing and overhead cameras)."""
+    synthetic, vector_env = V
+    from simaps import batch
+    z = G.load('ingest.npz')
+    for cfg, kind in (('lifting_4-small_divider', 'forward'), ('pushing_4-large_empty', 'overhead')):
+        s = synthetic.make_scene(cfg, 80)
+        b = batch.StateBatch([s])
+        keys = ['%s_a%d' % (cfg, a) for a in range(2)]
+        b.ingest(np.stack([z[k + '_depth'] for k in keys]), np.stack([z[k + '_seg'].astype(np.int32) for k in keys]),
+                 camera=kind, slots=[0, 1])
+        ov, oc = b.overhead.cpu().numpy(), b.occupancy.cpu().numpy()
+        for a, k in enumerate(keys):
+            assert _bitwise(ov[a], z[k + '_overhead']), k
+            assert np.array_equal(oc[a], z[k + '_occupancy']), k
+        assert int(b._keys.abs().sum()) == 0          # scratch left zeroed
+
+
+@pytest.mark.parametrize('kind', ['forward', 'overhead'])
+def test_ingest_then_get_state_vs_oracle(V, kind):
+    """update_map + get_state end to end on the device vs the oracle (fresh frames; z ties resolved
+    as 'later camera pixel wins' on both sides)."""
+    synthetic, vector_env = V
+    from simaps import batch
+    scenes = [synthetic.make_scene('lifting_2_throwing_2-large_empty', 210 + e) for e in range(3)]
+    b = batch.StateBatch(scenes)
+    frames = [synthetic.camera_images(scenes[e], a, kind, seed=7 * e + a) for e, a in b.agents]
+    b.ingest(np.stack([f[0] for f in frames]), np.stack([f[1] for f in frames]), camera=kind)
+    st = b.as_hwc(b.render()).cpu().numpy()
+    from simaps import camera
+    spec = camera.CAMERAS[kind]
+    ov, oc = b.overhead.cpu().numpy(), b.occupancy.cpu().numpy()
+    for n, (e, a) in enumerate(b.agents):
+        s = scenes[e]
+        r = s['robots'][a]
+        O.ingest(s['overhead'][a], s['occupancy'][a], frames[n][0], frames[n][1],
+                 spec.params(r['position'][0], r['position'][1], r['heading']), spec, synthetic.SEG_IDS,
+                 s['receptacle_position'] is not None)
+        assert _bitwise(ov[n], s['overhead'][a]) and np.array_equal(oc[n], s['occupancy'][a]), (e, a)
+        assert _bitwise(st[n], O.agent_state(s, a)), (e, a)

@@ -161,3 +161,22 @@ def test_oracle_shortest_path_vs_reference():
     for q in range(3):
         got = np.array(O.grid_shortest_path(G.load('sssp.npz')['demo_cspace'], z['demo_%d_src' % q], z['demo_%d_tgt' % q]))
         assert np.array_equal(got.reshape(-1, 2), z['demo_%d_path' % q]), q
+
+
+def test_oracle_ingest_vs_reference():
+    """Observation ingest: Mapper.update with the reference's own
+    Camera.capture_image on the committed depth / segmentation frames, exactly."""
+    from simaps import camera, synthetic
+    z = G.load('ingest.npz')
+    for cfg, kind in (('lifting_4-small_divider', 'forward'), ('pushing_4-large_empty', 'overhead')):
+        s = synthetic.make_scene(cfg, 80)
+        for a in range(2):
+            k = '%s_a%d' % (cfg, a)
+            ov, oc = s['overhead'][a].copy(), s['occupancy'][a].copy()
+            r = s['robots'][a]
+            spec = camera.CAMERAS[kind]
+            O.ingest(ov, oc, z[k + '_depth'], z[k + '_seg'].astype(np.int32),
+                     spec.params(r['position'][0], r['position'][1], r['heading']), spec, synthetic.SEG_IDS,
+                     s['receptacle_position'] is not None)
+            assert np.array_equal(ov.view(np.int32), z[k + '_overhead'].view(np.int32)), k
+            assert np.array_equal(oc, z[k + '_occupancy']), k

@@ -2,6 +2,7 @@
 
   sp_distance    OccupancyMap.shortest_path_distance (reward lookups): queries/s
   shortest_path  OccupancyMap.shortest_path (movement paths): paths/s
+  ingest         Robot.update_map minus the simulator (camera frame -> overhead / occupancy maps): frames/s
 
     python tools/bench_extra.py [--config lifting_4-small_divider] [--envs 64] [--queries 8]
 
@@ -91,5 +92,36 @@ def main():
                       'cpu_sample': '%d paths incl. each agent\'s cspace / EDT / SPFA' % n}), flush=True)
 
 
+def bench_ingest(args):
+    import oracle
+    from simaps import camera
+    scenes = [synthetic.make_scene(args.config, e) for e in range(args.envs)]
+    b = batch.StateBatch(scenes)
+    kind = 'forward'
+    frames = [synthetic.camera_images(scenes[e], a, kind, seed=e * 8 + a) for e, a in b.agents]
+    dep = torch.as_tensor(np.stack([f[0] for f in frames])).cuda()
+    seg = torch.as_tensor(np.stack([f[1] for f in frames])).cuda()
+    dt = timed(lambda: b.ingest(dep, seg, camera=kind), args.steps, 3)
+    spec = camera.CAMERAS[kind]
+    n, el = 0, 0.0
+    for k, (e, a) in enumerate(b.agents):
+        s = scenes[e]
+        r = s['robots'][a]
+        ov, oc = s['overhead'][a].copy(), s['occupancy'][a].copy()
+        t0 = time.perf_counter()
+        oracle.ingest(ov, oc, frames[k][0], frames[k][1], spec.params(r['position'][0], r['position'][1], r['heading']),
+                      spec, synthetic.SEG_IDS, s['receptacle_position'] is not None)
+        el += time.perf_counter() - t0
+        n += 1
+        if el > args.cpu_budget:
+            break
+    print(json.dumps({'row': 'ingest', 'config': args.config, 'camera': kind, 'frames_per_launch': b.N,
+                      'points_per_frame': spec.height_px * spec.width_px, 'gpu_frames_per_s': b.N / dt,
+                      'gpu_ms_per_launch': dt * 1e3, 'cpu_oracle_frames_per_s': n / el, 'cpu_cores': 1,
+                      'cpu_sample': '%d frames: capture_image points + argsort scatter + obstacle scatter' % n}),
+          flush=True)
+
+
 if __name__ == '__main__':
     main()
+    bench_ingest(argparse.Namespace(config='lifting_4-small_divider', envs=64, steps=10, cpu_budget=8.0))
