@@ -91,8 +91,8 @@ def max_over_ranks(values, world, device='cpu'):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=50)
-    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument('--config', default='lifting_4-small_divider')
     ap.add_argument('--envs', type=int, default=64, help='envs per GPU (BASELINE configs[1]: 64)')
     ap.add_argument('--layout', default='chw', choices=['hwc', 'chw'])
@@ -117,18 +117,20 @@ def main():
     out = b.alloc_state()
     stream = torch.cuda.current_stream()
 
-    # HIP events on the launch stream bracket every timed launch (kernel time for the roofline).
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events on the launch stream bracket the K timed launches (per-launch events would add
+    # ~6 us of marker overhead to every step); kernel_ms = their elapsed time / K, i.e. the average
+    # launch duration including the launch-to-launch gaps (conservative for the roofline).
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def step(k):
-        if k >= 0:
-            ev[k][0].record(stream)
+        if k == 0:
+            ev0.record(stream)
         b.render(out, stream=stream)
-        if k >= 0:
-            ev[k][1].record(stream)
+        if k == args.steps - 1:
+            ev1.record(stream)
 
     elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, 'cuda')
-    kern_ms = max_over_ranks([float(np.mean([s.elapsed_time(e) for s, e in ev]))], world, 'cuda')[0]
+    kern_ms = max_over_ranks([ev0.elapsed_time(ev1) / args.steps], world, 'cuda')[0]
 
     stacks_per_step = b.N * world
     value = stacks_per_step * args.steps / elapsed
