@@ -393,15 +393,18 @@ struct Group {
             return;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        // relaxed LDS atomics, ordered by the local-only fences around them: acquire / release
+        // orderings on the atomics themselves would also wait for every outstanding GLOBAL access
+        // of the wave (vmcnt(0)), exposing the render group's gather / store latency at each sync
         if ((threadIdx.x & 63) == 0) {
             const unsigned g = __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const unsigned arrived = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const unsigned arrived = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (arrived == (unsigned)nw - 1) {
                 __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_store(&bar[1], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(&bar[1], g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else {
                 unsigned spins = 0;
-                while (__hip_atomic_load(&bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == g) {
+                while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == g) {
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > (1u << 22)) {  // ~0.1 s: never in a correct run; flag and fall through
                         __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -892,7 +895,11 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         STAMP_NB(14);
     }
 #endif
+#ifndef SIMAPS_ABL_NOROBOTMAP
     for (int item = g.t; item < nr * 1024; item += g.n) {
+#else
+    for (int item = g.t; item < 0; item += g.n) {
+#endif
         const int q = item >> 10, bi = (item >> 5) & 31, bj = item & 31;
         const RobotP &P = sh.rob[q];
         if (bi > P.bi1 - P.bi0 || bj > P.bj1 - P.bj0) continue;
@@ -922,8 +929,12 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
             vrob = (mr & 2u) ? 1.0f : ((mr & 1u) ? 0.5f : 0.0f);
             vov = vseg > 0.0f ? vseg : ovv[k];
         }
+#ifdef SIMAPS_ABL_NOSTORE01
+        asm volatile("" ::"v"(vov), "v"(vrob));
+#else
         rc.put(0, p, vov);
         if (cfg.use_robot_map) rc.put(1, p, vrob);
+#endif
     }
     g.sync();  // the raster below reuses the robot-map region
     if (g.t == 0) STAMP_NB(11);
@@ -935,7 +946,9 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     for (int pass = 0; pass < 2; pass++) {
         const bool on = pass == 0 ? cfg.use_history_map : cfg.use_intention_map;
         if (!on) continue;
+#ifndef SIMAPS_ABL_NORASTER
         raster_lines(sh, tile, cfg, rb, paths, pass == 0 ? 4 : cfg.intention_map_encoding, g);
+#endif
         if (g.t == 0) STAMP_NB(12);
 #pragma unroll
         for (int k = 0; k < MAXPG; k++) {
