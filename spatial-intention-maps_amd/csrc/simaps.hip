@@ -73,6 +73,8 @@ __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
     } while (0)
 #endif
 constexpr int MAX_SEG = 128;     // intention / history segments per agent
+constexpr int RBLK = (CROP + 7) / 8;  // 8 x 8 blocks per crop side (robot sets, render_maps)
+constexpr int RBLK_PITCH = 32;        // row pitch of the block table: 0xff >> 3 = 31 is a row / column no robot touches
 constexpr int SEG_PER_ROBOT = SIMAPS_MAX_PATH - 1;
 constexpr int MAX_ROWS = 112;    // room rect rows (bit-row arrays)
 constexpr int WIN_WORDS = 3;     // occupancy window row: up to 192 bits
@@ -138,9 +140,10 @@ struct RobotP {
     double x, y, tx, ty;
     int S0, S1, st_i, st_j;  // stamp shape, placement (pixel - S // 2, envs.py:2272)
     int type, lifting, idle, group;
+    int bi0, bi1, bj0, bj1;  // global-pixel box outside which the rotated mask is surely 0 (16-B aligned)
     int tpi, tpj;            // target end-effector pixel
-    int bi0, bi1, bj0, bj1;  // global-pixel box outside which the rotated mask is surely 0
-    float seg_val, pad;
+    unsigned code0;          // robot-code bits of a class-mask pixel (robot_bits)
+    float seg_val;
     uint32_t sbits[2][32];   // rotated stamp inside the box: [0] class mask, [1] lifted-cube mask
 };
 
@@ -159,8 +162,7 @@ struct Shared {
     int src_q[2][2], src_s[2][2], src_ok[2];
     int sp_slot[2];      // which dist buffer each sp channel uses (-1 = off)
     float dmax[2];
-    float unreach[2];    // scaled value of unreachable / outside cells when dist_scaled
-    int dist_scaled;     // dist[] already holds the channel values (sp / 96 * scale)
+    float unreach[2];    // scaled value of unreachable / outside cells
     int flag[2];
     int rounds;          // SSSP rounds to convergence (-1: cap hit)
     int nseg;
@@ -172,6 +174,7 @@ struct Shared {
     int colbest[2][SIMAPS_MAX_ROOM_W];
     int envg[2][SIMAPS_MAX_ROOM_W];  // Voronoi envelope (rect columns) per source
     unsigned bar[2][4];              // group barriers {count, generation, timeout, -}: [0] sweeps, [1] render
+    uint32_t rblk[RBLK_PITCH * RBLK_PITCH / 4];  // per 8 x 8 crop block: bit q = robot q's stamp box overlaps it
     int changed[3];                  // rotating per-round "some sweep improved a cell" flags
     Seg seg[MAX_SEG];
 };
@@ -189,21 +192,34 @@ constexpr int OFF_UNION = OFF_DIST + align16(2 * DIST_FLOATS * 4);
 constexpr int TILE_BYTES = TILE * TILE * 4;
 constexpr int UNION_BYTES = align16((int)sizeof(SsspScratch) > TILE_BYTES ? (int)sizeof(SsspScratch) : TILE_BYTES);
 constexpr int LDS_BYTES = OFF_UNION + UNION_BYTES;
-constexpr int RMAP_BYTES = align16(CROP * CROP);  // u8 robot-code map over the crop (render_maps)
-static_assert(RMAP_BYTES + 4 * LW * 8 <= UNION_BYTES, "robot map + rotation tables fit the union");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+static_assert(offsetof(RobotP, bi0) % 16 == 0 && sizeof(RobotP) % 16 == 0, "RobotP box loads as one b128");
 
 // ------------------------------------------------------------------------------------------------
 // Block reductions (16 waves)
 // ------------------------------------------------------------------------------------------------
+// DPP within each 16-lane row (quad swaps, half-row and row mirrors), then the 4 row results by
+// readlane: no LDS round trips (ds_bpermute) and a wave-uniform result.  NaN-free inputs only.
+#define WAVE_REDUCE_F32(v, OP)                                                                          \
+    do {                                                                                                \
+        v = OP(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xf, 0xf, false)));  \
+        v = OP(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xf, 0xf, false)));  \
+        v = OP(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xf, 0xf, false))); \
+        v = OP(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xf, 0xf, false))); \
+        const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));                \
+        const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));               \
+        const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));               \
+        const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));               \
+        v = OP(OP(r0, r1), OP(r2, r3));                                                                 \
+    } while (0)
 __device__ __forceinline__ float wave_min(float v)
 {
-    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    WAVE_REDUCE_F32(v, fminf);
     return v;
 }
 __device__ __forceinline__ float wave_max(float v)
 {
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    WAVE_REDUCE_F32(v, fmaxf);
     return v;
 }
 
@@ -632,7 +648,6 @@ __device__ __forceinline__ void sssp_scale(Shared &sh, float *dist, int nsrc, fl
         }
         if (g.t == 0) sh.unreach[s] = un;
     }
-    if (g.t == 0) sh.dist_scaled = 1;
 }
 
 __device__ __forceinline__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
@@ -649,55 +664,80 @@ __device__ __forceinline__ void sssp(Shared &sh, SsspScratch &S, float *dist, in
 // Intention / history raster (Mapper._create_global_intention_or_history_map, envs.py:2302-2347)
 // ------------------------------------------------------------------------------------------------
 // enc: SIMAPS_ENC_* or 4 = history (ramp over the reversed history path)
+// The per-robot segment table of one pass (robot k's lane; path_length accumulates sequentially).
+// The first pass's table is built in the params phase, where its serial fp64 chain (sqrt, divide)
+// overlaps the robot-rotation lanes instead of sitting on the render group's critical path.
+__device__ __forceinline__ void seg_table(Shared &sh, const simaps_config &cfg, const simaps_robot *rb,
+                                          const double *__restrict__ paths, int enc, int k, int me)
+{
+    int cnt = 0;
+    const simaps_robot &r = rb[k];
+    if (k != me && !r.idle && enc != SIMAPS_ENC_CIRCLE) {
+        const double scale = cfg.intention_map_scale;
+        const int off = enc == 4 ? r.history_off : r.intention_off;
+        const int full = enc == 4 ? r.history_len : r.intention_len;
+        const bool as_line = enc == SIMAPS_ENC_LINE && full >= 2;  // [path[0], path[-1]] (envs.py:2315-2316)
+        const int len = as_line ? 2 : full;
+        double L = 0.0;
+        for (int i = 1; i < len && cnt < SEG_PER_ROBOT; i++) {
+            const int ia = i - 1, ib = as_line ? full - 1 : i;
+            const double sx = paths[2 * (off + ia)], sy = paths[2 * (off + ia) + 1];
+            const double tx = paths[2 * (off + ib)], ty = paths[2 * (off + ib) + 1];
+            const double dx = tx - sx, dy = ty - sy;
+            const double seg_len = scale * sqrt(dx * dx + dy * dy);  // envs.py:2324, 2557-2558
+            Seg &G = sh.seg[k * SEG_PER_ROBOT + cnt];
+            pos_to_pix(sx, sy, cfg.H, cfg.W, G.si, G.sj);
+            pos_to_pix(tx, ty, cfg.H, cfg.W, G.ti, G.tj);
+            G.dr = abs(G.ti - G.si);
+            G.dc = abs(G.tj - G.sj);
+            G.n = (G.dr > G.dc ? G.dr : G.dc) + 1;
+            G.last = (i == len - 1);
+            // np.clip(np.linspace(1 - L, 1 - (L + seg), n), 0, 1) (envs.py:2335)
+            G.start = 1 - L;
+            G.stop = 1 - (L + seg_len);
+            G.step = G.n > 1 ? (G.stop - G.start) / (G.n - 1) : 0.0;
+            L += seg_len;
+            cnt++;
+        }
+    }
+    sh.seg_robot_cnt[k] = cnt;
+}
+
+// max(v) into tile cell (a, b) and, for thick lines, its 4-neighbours: the grey dilation with disk(1)
+// (envs.py:2343-2344) applied as a scatter at raster time, so a sample is one read.  The cross is
+// symmetric, so scattering each line pixel into its cross equals dilating the raster; the tile's
+// 1-px halo holds every neighbour of a crop pixel.
+__device__ __forceinline__ void tile_put(unsigned *tu, int a, int b, float v, int thick)
+{
+    const unsigned u = __float_as_uint(v);  // v > 0: the uint order is the float order
+    if ((unsigned)a < (unsigned)TILE && (unsigned)b < (unsigned)TILE) atomicMax(&tu[a * TILE + b], u);
+    if (thick > 1) {
+        if ((unsigned)(a - 1) < (unsigned)TILE && (unsigned)b < (unsigned)TILE) atomicMax(&tu[(a - 1) * TILE + b], u);
+        if ((unsigned)(a + 1) < (unsigned)TILE && (unsigned)b < (unsigned)TILE) atomicMax(&tu[(a + 1) * TILE + b], u);
+        if ((unsigned)a < (unsigned)TILE && (unsigned)(b - 1) < (unsigned)TILE) atomicMax(&tu[a * TILE + b - 1], u);
+        if ((unsigned)a < (unsigned)TILE && (unsigned)(b + 1) < (unsigned)TILE) atomicMax(&tu[a * TILE + b + 1], u);
+    }
+}
+
+// Rasterise one pass into the tile (max of line values per pixel).  Zeroes the tile and, unless
+// the params phase already did, builds the segment table; two group barriers.
 __device__ __forceinline__ void raster_lines(Shared &sh, float *tile, const simaps_config &cfg, const simaps_robot *rb,
-                             const double *__restrict__ paths, int enc, const Group &g)
+                             const double *__restrict__ paths, int enc, bool have_table, const Group &g)
 {
     const int tid = g.t, lane = threadIdx.x & 63, wave = g.t >> 6, nwaves = g.n >> 6;
+    uint4 *tz = reinterpret_cast<uint4 *>(tile);
+    for (int k = tid; k < TILE * TILE / 4; k += g.n) tz[k] = uint4{0u, 0u, 0u, 0u};
+    static_assert(TILE * TILE % 4 == 0, "tile zeroing");
     unsigned *tu = reinterpret_cast<unsigned *>(tile);
-    for (int k = tid; k < TILE * TILE; k += g.n) tu[k] = 0u;
-    const double scale = cfg.intention_map_scale;
-    const float scale_f = (float)scale;
-    // per-robot segment tables (one lane per robot; path_length accumulates sequentially)
-    if (tid < sh.nr) {
-        const int k = tid;
-        int cnt = 0;
-        const RobotP &R = sh.rob[k];
-        if (k != sh.me && !R.idle && enc != SIMAPS_ENC_CIRCLE) {
-            const simaps_robot &r = rb[k];
-            const int off = enc == 4 ? r.history_off : r.intention_off;
-            const int full = enc == 4 ? r.history_len : r.intention_len;
-            const bool as_line = enc == SIMAPS_ENC_LINE && full >= 2;  // [path[0], path[-1]] (envs.py:2315-2316)
-            const int len = as_line ? 2 : full;
-            double L = 0.0;
-            for (int i = 1; i < len && cnt < SEG_PER_ROBOT; i++) {
-                const int ia = i - 1, ib = as_line ? full - 1 : i;
-                const double sx = paths[2 * (off + ia)], sy = paths[2 * (off + ia) + 1];
-                const double tx = paths[2 * (off + ib)], ty = paths[2 * (off + ib) + 1];
-                const double dx = tx - sx, dy = ty - sy;
-                const double seg_len = scale * sqrt(dx * dx + dy * dy);  // envs.py:2324, 2557-2558
-                Seg &G = sh.seg[k * SEG_PER_ROBOT + cnt];
-                pos_to_pix(sx, sy, cfg.H, cfg.W, G.si, G.sj);
-                pos_to_pix(tx, ty, cfg.H, cfg.W, G.ti, G.tj);
-                G.dr = abs(G.ti - G.si);
-                G.dc = abs(G.tj - G.sj);
-                G.n = (G.dr > G.dc ? G.dr : G.dc) + 1;
-                G.last = (i == len - 1);
-                // np.clip(np.linspace(1 - L, 1 - (L + seg), n), 0, 1) (envs.py:2335)
-                G.start = 1 - L;
-                G.stop = 1 - (L + seg_len);
-                G.step = G.n > 1 ? (G.stop - G.start) / (G.n - 1) : 0.0;
-                L += seg_len;
-                cnt++;
-            }
-        }
-        sh.seg_robot_cnt[k] = cnt;
-    }
+    const float scale_f = (float)cfg.intention_map_scale;
+    const int thick = cfg.intention_map_line_thickness;
+    if (!have_table && tid < sh.nr) seg_table(sh, cfg, rb, paths, enc, tid, sh.me);
     g.sync();
     const int ti0 = sh.pi - TILE_HALF, tj0 = sh.pj - TILE_HALF;
     if (enc == SIMAPS_ENC_CIRCLE) {
         if (tid < sh.nr && tid != sh.me && !sh.rob[tid].idle) {
             const int a = sh.rob[tid].tpi - ti0, b = sh.rob[tid].tpj - tj0;
-            if (a >= 0 && a < TILE && b >= 0 && b < TILE) atomicMax(&tu[a * TILE + b], __float_as_uint(scale_f));
+            tile_put(tu, a, b, scale_f, thick);
         }
     } else {
         // one wave per segment, lanes stride over its pixels
@@ -730,24 +770,16 @@ __device__ __forceinline__ void raster_lines(Shared &sh, float *tile, const sima
                     v = (float)y;
                 }
                 const int a = pr - ti0, b = pc - tj0;
-                if (v > 0.0f && a >= 0 && a < TILE && b >= 0 && b < TILE) atomicMax(&tu[a * TILE + b], __float_as_uint(v));
+                if (v > 0.0f) tile_put(tu, a, b, v, thick);
             }
         }
     }
     g.sync();
 }
 
-__device__ __forceinline__ float tile_sample(const float *tile, int thick, int gi, int gj, int pi, int pj)
+__device__ __forceinline__ float tile_sample(const float *tile, int gi, int gj, int pi, int pj)
 {
-    const int a = gi - pi + TILE_HALF, b = gj - pj + TILE_HALF;
-    float v = tile[a * TILE + b];
-    if (thick > 1) {
-        v = fmaxf(v, tile[(a - 1) * TILE + b]);
-        v = fmaxf(v, tile[(a + 1) * TILE + b]);
-        v = fmaxf(v, tile[a * TILE + b - 1]);
-        v = fmaxf(v, tile[a * TILE + b + 1]);
-    }
-    return v;
+    return tile[(gi - pi + TILE_HALF) * TILE + (gj - pj + TILE_HALF)];  // dilated at raster time (tile_put)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -761,32 +793,10 @@ struct RenderCtx {
     int C, n;
     __device__ __forceinline__ void put(int ch, int p, float v) const
     {
-        int idx = cfg.layout_chw ? ch * LW * LW + p : p * C + ch;  // < 96 * 96 * C: 32-bit
+        unsigned idx = cfg.layout_chw ? ch * LW * LW + p : p * C + ch;  // < 96 * 96 * C: 32-bit
         asm volatile("" : "+v"(idx));  // computed at the store: no per-pixel offsets hoisted across passes
-        out[idx] = v;
-    }
-    // global pixel sampled by output pixel p (Mapper._get_local_map, envs.py:2200-2211), packed
-    // gi << 16 | gj, or -1 where the scipy rotate falls outside the crop (cval 0)
-    // gpix from the per-agent product tables T (render_maps): the same fp64 operations, 4 products fewer
-    __device__ __forceinline__ int gpix_tab(const double *T, int p) const
-    {
-        const Rot &R = sh.rot;
-        const int a = p / LW, b = p % LW;
-        const double s0 = (T[a] + T[LW + b]) + R.f0;
-        const double s1 = (T[2 * LW + a] + T[3 * LW + b]) + R.f1;
-        const double hi = CROP - 1;
-        if (!(s0 >= 0.0 && s0 <= hi && s1 >= 0.0 && s1 <= hi)) return -1;
-        const int gi = sh.pi - HALF_CROP + (int)floor(s0 + 0.5), gj = sh.pj - HALF_CROP + (int)floor(s1 + 0.5);
-        return (gi >= 0 && gi < cfg.H && gj >= 0 && gj < cfg.W) ? (gi << 16) | gj : -1;
-    }
-    __device__ __forceinline__ int gpix(int p) const
-    {
-        const Rot &R = sh.rot;
-        const int a = p / LW, b = p % LW;
-        int k0, k1;
-        if (!rot_src(R, CROP, a + R.S0 / 2 - LW / 2, b + R.S1 / 2 - LW / 2, k0, k1)) return -1;
-        const int gi = sh.pi - HALF_CROP + k0, gj = sh.pj - HALF_CROP + k1;
-        return (gi >= 0 && gi < cfg.H && gj >= 0 && gj < cfg.W) ? (gi << 16) | gj : -1;
+        // 32-bit byte offset from an SGPR base: one VGPR per address (saddr form), no 64-bit adds
+        *reinterpret_cast<float *>(reinterpret_cast<char *>(out) + idx * 4u) = v;
     }
 };
 
@@ -827,66 +837,125 @@ __device__ __forceinline__ void intention_channel_order(Shared &sh, const simaps
 
 // Channels that do not need the shortest-path maps, rendered by group g:
 // overhead (0), robot (1), history / intention maps, baseline intention channels.
+//
+// Sample indices (Mapper._get_local_map, envs.py:2200-2211; rot_src): each output pixel's source
+// index in the crop is computed once per pixel and reused by every channel and the distance phase.
+// Fast path in fp32: |s_f32 - s_f64| < 1e-4 for every term range here (|o| <= 144, |f| <= 200,
+// five roundings of <= 2^-24 relative), so wherever s_f32 + 0.5 lies more than SAMPLE_EPS from an
+// integer and s_f32 more than SAMPLE_EPS from the crop bounds, floor(s + 0.5) and the in-crop test
+// equal the fp64 ones.  The few pixels inside that band (~0.2%) take the exact fp64 rot_src.
+constexpr float SAMPLE_EPS = 4e-4f;
+
+// robot r's stamp bit tiles -> the overhead seg bits / robot-map code of global pixel (gi, gj)
+// (Mapper._create_global_robot_map, envs.py:2251-2276): bit g = seg value (g + 5) / 8
+// (SEG_VALUES robot_group_{g+1}), bit 4 = 0.5, bit 5 = 1.0; the max over robots is the highest bit
+__device__ __forceinline__ unsigned robot_bits(const RobotP &P, int gi, int gj)
+{
+    const int a = gi - P.bi0, b = gj - P.bj0;
+    unsigned bits = 0;
+    if ((unsigned)a <= (unsigned)(P.bi1 - P.bi0) && (unsigned)b <= (unsigned)(P.bj1 - P.bj0)) {
+        if ((P.sbits[0][a] >> b) & 1u) bits |= P.code0;
+        if ((P.sbits[1][a] >> b) & 1u) bits |= 1u << 5;  // lifted-cube mask, value 1.0
+    }
+    return bits;
+}
+
 __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry &geo, const float *__restrict__ ovh,
                             const simaps_robot *rb, const double *__restrict__ paths, float *tile)
 {
     const simaps_config &cfg = rc.cfg;
     Shared &sh = rc.sh;
-    const int nr = sh.nr, W = cfg.W;
+    const int nr = sh.nr, W = cfg.W, H = cfg.H;
     constexpr int NP = LW * LW;
-    // overhead / robot channels.  The robots' rotated stamps (per-robot bit tiles, built once per
-    // workgroup) are first OR-ed into a 136 x 136 map over the agent's crop, in the raster-tile
-    // region: bit (g + 5) = seg value (g + 5) / 8 (SEG_VALUES robot_group_{g+1}), bit 16 = 0.5,
-    // bit 17 = 1.0 (non-seg values).  A pixel is then one LDS read; the highest bit of each field is
-    // the np.maximum over robots of _create_global_robot_map (envs.py:2251-2276).
-    uint8_t *rmap = reinterpret_cast<uint8_t *>(tile);
-    unsigned *rmapw = reinterpret_cast<unsigned *>(tile);
-    // products of the local rotation (fp64, exactly the terms of rot_src): T[0][a] = o0 * c,
-    // T[1][b] = o1 * s, T[2][a] = o0 * -s, T[3][b] = o1 * c for output row a / column b
-    double *T = reinterpret_cast<double *>(reinterpret_cast<char *>(tile) + RMAP_BYTES);
-    const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
+    const int ci0 = __builtin_amdgcn_readfirstlane(sh.pi - HALF_CROP);
+    const int cj0 = __builtin_amdgcn_readfirstlane(sh.pj - HALF_CROP);
+    // the sample index of each of this thread's output pixels (fast fp32 path, exact fp64 fallback),
+    // packed 2 per register: crop-relative (row << 8 | col), 0xffff = outside (cval)
+    constexpr int MAXPG = 18;  // output pixels per render thread (>= 8 render waves)
+    uint32_t gqp[MAXPG / 2];
     {
-        uint4 *z = reinterpret_cast<uint4 *>(rmap);
-        for (int k = g.t; k < RMAP_BYTES / 16; k += g.n) z[k] = uint4{0u, 0u, 0u, 0u};
-        const Rot &R = sh.rot;
-        for (int k = g.t; k < 4 * LW; k += g.n) {
-            const int which = k / LW, i = k % LW;
-            const double o = (which & 1) ? (double)(i + R.S1 / 2 - LW / 2) : (double)(i + R.S0 / 2 - LW / 2);
-            T[k] = which == 0 ? o * R.c : which == 1 ? o * R.s : which == 2 ? o * (-R.s) : o * R.c;
+        const Rot R = sh.rot;
+        const float c = (float)R.c, sn = (float)R.s, f0 = (float)R.f0, f1 = (float)R.f1;
+        const int oa = R.S0 / 2 - LW / 2, ob = R.S1 / 2 - LW / 2;
+        const float hi = CROP - 1;
+        int a = g.t / LW, b = g.t % LW;  // pixel p = g.t + k * g.n, walked incrementally
+        const int da = g.n / LW, db = g.n % LW;
+#pragma unroll
+        for (int k = 0; k < MAXPG; k++) {
+            uint32_t v = 0xffffu;
+            if (a < LW) {
+#if defined(SIMAPS_ABL_NOGPIX)
+                v = ((uint32_t)(a + 20) << 8) | (uint32_t)(b + 20);
+#else
+                const float o0 = (float)(a + oa), o1 = (float)(b + ob);
+                const float s0 = (o0 * c + o1 * sn) + f0, s1 = (o0 * (-sn) + o1 * c) + f1;
+                const float u0 = s0 + 0.5f, u1 = s1 + 0.5f;
+                const float k0 = floorf(u0), k1 = floorf(u1);
+                // distances to the crop bounds and to the rounding boundaries, branch-free
+                const float m_in = fmaxf(fabsf(s0 - 0.5f * hi), fabsf(s1 - 0.5f * hi));
+                const float m_fr = fmaxf(fabsf(u0 - k0 - 0.5f), fabsf(u1 - k1 - 0.5f));
+                const int out = m_in > 0.5f * hi + SAMPLE_EPS;
+                const int sure = out | ((m_in < 0.5f * hi - SAMPLE_EPS) & (m_fr < 0.5f - SAMPLE_EPS));
+                const int i0 = (int)k0, i1 = (int)k1;
+                const int inmap = ((unsigned)(ci0 + i0) < (unsigned)H) & ((unsigned)(cj0 + i1) < (unsigned)W);
+                const uint32_t vin = (!out & inmap) ? (((uint32_t)i0 << 8) | (uint32_t)i1) : 0xffffu;
+                v = sure ? vin : 0xfffeu;  // 0xfffe: exact fp64 below
+#endif
+            }
+            if (k & 1) gqp[k >> 1] |= v << 16;
+            else gqp[k >> 1] = v;
+            a += da;
+            b += db;
+            if (b >= LW) { b -= LW; a++; }
+        }
+        // the pixels in the rounding band: exact fp64 rot_src (a separate pass keeps the fp64
+        // temporaries out of the fast loop's register budget)
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < MAXPG / 2; k++) any |= ((gqp[k] & 0xffffu) == 0xfffeu) | ((gqp[k] >> 16) == 0xfffeu);
+        if (any) {
+#pragma unroll
+            for (int k = 0; k < MAXPG; k++) {
+                const uint32_t cur = (gqp[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
+                if (cur == 0xfffeu) {
+                    const int p = g.t + k * g.n;
+                    int i0, i1;
+                    uint32_t v = 0xffffu;
+                    if (rot_src(R, CROP, p / LW + oa, p % LW + ob, i0, i1)) {
+                        const int gi = ci0 + i0, gj = cj0 + i1;
+                        if (gi >= 0 && gi < H && gj >= 0 && gj < W) v = ((uint32_t)i0 << 8) | (uint32_t)i1;
+                    }
+                    gqp[k >> 1] ^= (v ^ 0xfffeu) << ((k & 1) * 16);
+                }
+            }
         }
     }
-    g.sync();
-    // the sample index of each of this thread's output pixels, computed once (fp64 scipy rule) and
-    // reused by every channel of the group, then handed to the distance phase through LDS
-    constexpr int MAXPG = 18;  // output pixels per render thread (>= 8 render waves)
-    // packed 2 per register: crop-relative (row << 8 | col), 0xffff = outside (cval)
-    uint32_t gqp[MAXPG / 2];
-#pragma unroll
-    for (int k = 0; k < MAXPG; k++) {
-        const int p = g.t + k * g.n;
-#if defined(SIMAPS_ABL_NOGPIX)
-        const int q = p < NP ? ((sh.pi - 48 + p / LW) << 16) | (sh.pj - 48 + p % LW) : -1;
-#else
-        const int q = p < NP ? rc.gpix_tab(T, p) : -1;
+    auto gq_v = [&](int k) -> uint32_t { return (gqp[k >> 1] >> ((k & 1) * 16)) & 0xffffu; };
+    // channel index after overhead / robot / distance channels (envs.py:2071-2113 order)
+    int ch = 1 + !!cfg.use_robot_map + !!cfg.use_distance_to_receptacle_map + !!cfg.use_shortest_path_to_receptacle_map +
+             !!cfg.use_shortest_path_map;
+    // history / intention passes, rasterised into the LDS tile (the first pass's segment table was
+    // built in the params phase)
+    int encs[2], npass = 0;
+    if (cfg.use_history_map) encs[npass++] = 4;
+    if (cfg.use_intention_map) encs[npass++] = cfg.intention_map_encoding;
+    const int thick = cfg.intention_map_line_thickness;
+#ifndef SIMAPS_ABL_NORASTER
+    if (npass > 0) raster_lines(sh, tile, cfg, rb, paths, encs[0], true, g);
 #endif
-        const uint32_t v = q >= 0 ? (uint32_t)((((q >> 16) - ci0) << 8) | ((q & 0xffff) - cj0)) : 0xffffu;
-        if (k & 1) gqp[k >> 1] |= v << 16;
-        else gqp[k >> 1] = v;
-    }
-    // global (gi << 16 | gj) of pixel slot k, or -1
-    auto gq_at = [&](int k) -> int {
-        const uint32_t v = (gqp[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
-        return v == 0xffffu ? -1 : ((ci0 + (int)(v >> 8)) << 16) | (cj0 + (int)(v & 0xffu));
-    };
-    // every overhead gather of the thread in flight at once; the robot map is built meanwhile
+    // every overhead gather of the thread in flight at once, issued after the first raster (whose
+    // integer divisions and fp64 need the registers); the intention samples and stores run meanwhile
     float ovv[MAXPG];
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
-        const int q = gq_at(k);
+        uint32_t v = gq_v(k);
+        asm volatile("" : "+v"(v));  // nothing computed here is shared with (kept alive for) later passes
 #ifdef SIMAPS_ABL_NOGATHER
-        ovv[k] = q >= 0 ? 0.125f : 0.0f;
+        ovv[k] = v != 0xffffu ? 0.125f : 0.0f;
 #else
-        ovv[k] = q >= 0 ? ovh[(size_t)(q >> 16) * W + (q & 0xffff)] : 0.0f;
+        // branch-free, 32-bit offsets (SGPR base): pixels outside the crop load cell 0, ignored later
+        const int idx = (ci0 + (int)(v >> 8)) * W + (cj0 + (int)(v & 0xffu));
+        ovv[k] = *reinterpret_cast<const float *>(reinterpret_cast<const char *>(ovh) + (unsigned)(v != 0xffffu ? idx : 0) * 4u);
 #endif
     }
 #ifdef SIMAPS_PHASE_STAMPS
@@ -895,40 +964,45 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         STAMP_NB(14);
     }
 #endif
-#ifndef SIMAPS_ABL_NOROBOTMAP
-    for (int item = g.t; item < nr * 1024; item += g.n) {
-#else
-    for (int item = g.t; item < 0; item += g.n) {
-#endif
-        const int q = item >> 10, bi = (item >> 5) & 31, bj = item & 31;
-        const RobotP &P = sh.rob[q];
-        if (bi > P.bi1 - P.bi0 || bj > P.bj1 - P.bj0) continue;
-        const int a = P.bi0 + bi - ci0, b = P.bj0 + bj - cj0;
-        if (a < 0 || a >= CROP || b < 0 || b >= CROP) continue;
-        unsigned bits = 0;  // byte code: bit g = seg value (g + 5) / 8, bit 4 = 0.5, bit 5 = 1.0
-        if ((P.sbits[0][bi] >> bj) & 1u) {
-            bits |= 1u << P.group;
-            if (P.type != SIMAPS_LIFTING) bits |= 1u << 5;
-            else if (!P.lifting) bits |= 1u << 4;
+    // sample one rasterised pass into channel c (then the tile may be reused)
+    auto sample_pass = [&](int c) {
+        if (g.t == 0) STAMP_NB(12);
+#pragma unroll
+        for (int k = 0; k < MAXPG; k++) {
+            const int p = g.t + k * g.n;
+            uint32_t v = gq_v(k);
+            asm volatile("" : "+v"(v));
+            if (p < NP)
+                rc.put(c, p, v != 0xffffu ? tile_sample(tile, ci0 + (int)(v >> 8), cj0 + (int)(v & 0xffu), sh.pi, sh.pj) : 0.0f);
         }
-        if ((P.sbits[1][bi] >> bj) & 1u) bits |= 1u << 5;  // lifted-cube mask, value 1.0
-        const int idx = a * CROP + b;
-        if (bits) atomicOr(&rmapw[idx >> 2], bits << (8 * (idx & 3)));
-    }
-    g.sync();
+        g.sync();
+    };
+    if (npass > 0) sample_pass(ch);
     if (g.t == 0) STAMP_NB(13);
+    // overhead / robot channels: per pixel, the 8 x 8 crop block's robot set (sh.rblk, built in the
+    // stamps phase) selects the few robots whose stamp box can contain it
+    const uint8_t *rblk = reinterpret_cast<const uint8_t *>(sh.rblk);
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
-        const int p = g.t + k * g.n, q = gq_at(k);
+        const int p = g.t + k * g.n;
         if (p >= NP) break;
-        float vseg = 0.0f, vrob = 0.0f, vov = 0.0f;
-        if (q >= 0) {
-            const unsigned m = rmap[((q >> 16) - ci0) * CROP + (q & 0xffff) - cj0];
-            const unsigned ms = m & 0xfu, mr = m >> 4;
-            vseg = ms ? (float)(31 - __builtin_clz(ms) + 5) * 0.125f : 0.0f;
-            vrob = (mr & 2u) ? 1.0f : ((mr & 1u) ? 0.5f : 0.0f);
-            vov = vseg > 0.0f ? vseg : ovv[k];
+        // an outside pixel (0xffff) reads block (31, 31), which no robot touches.  (The asm keeps the
+        // per-pixel index math and validity test here instead of hoisted above the gathers, where 18
+        // pixels' worth of it would not fit the register budget.)
+        uint32_t v = gq_v(k);
+        asm volatile("" : "+v"(v));
+        const int a = (int)(v >> 8), b = (int)(v & 0xffu);
+        unsigned rs = rblk[(a >> 3) * RBLK_PITCH + (b >> 3)];
+        unsigned m = 0;
+        while (rs) {
+            const int q = __builtin_ctz(rs);
+            rs &= rs - 1;
+            m |= robot_bits(sh.rob[q], ci0 + a, cj0 + b);
         }
+        const unsigned ms = m & 0xfu, mr = m >> 4;
+        const float vseg = ms ? (float)(31 - __builtin_clz(ms) + 5) * 0.125f : 0.0f;
+        const float vrob = (mr & 2u) ? 1.0f : ((mr & 1u) ? 0.5f : 0.0f);
+        const float vov = vseg > 0.0f ? vseg : (v != 0xffffu ? ovv[k] : 0.0f);
 #ifdef SIMAPS_ABL_NOSTORE01
         asm volatile("" ::"v"(vov), "v"(vrob));
 #else
@@ -936,28 +1010,16 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         if (cfg.use_robot_map) rc.put(1, p, vrob);
 #endif
     }
-    g.sync();  // the raster below reuses the robot-map region
     if (g.t == 0) STAMP_NB(11);
-    // channel index after overhead / robot / distance channels (envs.py:2071-2113 order)
-    int ch = 1 + !!cfg.use_robot_map + !!cfg.use_distance_to_receptacle_map + !!cfg.use_shortest_path_to_receptacle_map +
-             !!cfg.use_shortest_path_map;
-    // history / intention maps, rasterised into the LDS tile
-    const int thick = cfg.intention_map_line_thickness;
-    for (int pass = 0; pass < 2; pass++) {
-        const bool on = pass == 0 ? cfg.use_history_map : cfg.use_intention_map;
-        if (!on) continue;
+    // the second history / intention pass (history + intention configs), after the overhead values
+    // are consumed: its raster needs the registers the gathers held
+    if (npass > 1) {
 #ifndef SIMAPS_ABL_NORASTER
-        raster_lines(sh, tile, cfg, rb, paths, pass == 0 ? 4 : cfg.intention_map_encoding, g);
+        raster_lines(sh, tile, cfg, rb, paths, encs[1], false, g);
 #endif
-        if (g.t == 0) STAMP_NB(12);
-#pragma unroll
-        for (int k = 0; k < MAXPG; k++) {
-            const int p = g.t + k * g.n, q = gq_at(k);
-            if (p < NP) rc.put(ch, p, q >= 0 ? tile_sample(tile, thick, q >> 16, q & 0xffff, sh.pi, sh.pj) : 0.0f);
-        }
-        ch++;
-        g.sync();
+        sample_pass(ch + 1);
     }
+    ch += npass;
     // baseline intention channels (Mapper._get_intention_channels, envs.py:2349-2378)
     if (cfg.use_intention_channels) {  // sh.order / sh.nonsp: intention_channel_order (params phase)
         int c2 = 0;
@@ -969,15 +1031,16 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
                 const RobotP &R = sh.rob[kq];
 #pragma unroll
                 for (int k = 0; k < MAXPG; k++) {
-                    const int p = g.t + k * g.n, q = gq_at(k);
+                    const int p = g.t + k * g.n;
                     if (p >= NP) continue;
-                    float v = 0.0f;
-                    if (q >= 0 && !R.idle) {
-                        const int di = abs((q >> 16) - R.tpi), dj = abs((q & 0xffff) - R.tpj);
+                    const uint32_t v = gq_v(k);
+                    float val = 0.0f;
+                    if (v != 0xffffu && !R.idle) {
+                        const int di = abs(ci0 + (int)(v >> 8) - R.tpi), dj = abs(cj0 + (int)(v & 0xffu) - R.tpj);
                         const bool hit = thick > 1 ? (di + dj <= 1) : (di == 0 && dj == 0);
-                        v = hit ? scale_f : 0.0f;
+                        val = hit ? scale_f : 0.0f;
                     }
-                    rc.put(ch, p, v);
+                    rc.put(ch, p, val);
                 }
                 ch++;
             } else {
@@ -987,12 +1050,12 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         }
     }
     // hand the sample indices to the distance phase: crop-relative (row << 8 | col), 0xffff = cval
-    g.sync();  // the tile region is dead
+    // (the tile region is free: every raster pass ended with a group barrier)
     uint16_t *tab = reinterpret_cast<uint16_t *>(tile);
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
         const int p = g.t + k * g.n;
-        if (p < NP) tab[p] = (uint16_t)((gqp[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
+        if (p < NP) tab[p] = (uint16_t)gq_v(k);
     }
 }
 
@@ -1001,6 +1064,10 @@ static_assert(PPT * NT == LW * LW, "pixel split");
 
 // Distance channels (all 16 waves): Euclidean map, then shortest-path maps; local -= local.min()
 // (envs.py:2213-2216), so every value is kept in registers until the block minimum is known.
+// The sweep group has already turned dist[] into channel values (sssp_scale), border cells
+// included: cell 0 of each array holds the "unreachable" value, which is also the value of every
+// global pixel outside the room rect, so an out-of-rect pixel just reads cell 0.  Everything the
+// per-pixel loop needs from `sh` is read once into registers: the loop is straight-line code.
 __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, const simaps_env &ev, const float *dist, int nsrc,
                                          const uint16_t *tab)
 {
@@ -1011,51 +1078,56 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
     const int nd = has_eu + nsrc;
     if (nd == 0) return;
     const int ch = 1 + !!cfg.use_robot_map;
-    int gpix[PPT];  // from the render group's table (render_maps), not recomputed
-    const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
+    const int ci0 = __builtin_amdgcn_readfirstlane(sh.pi - HALF_CROP);
+    const int cj0 = __builtin_amdgcn_readfirstlane(sh.pj - HALF_CROP);
+    const int ri0 = __builtin_amdgcn_readfirstlane(ci0 - sh.i0), rj0 = __builtin_amdgcn_readfirstlane(cj0 - sh.j0);
+    const unsigned h = __builtin_amdgcn_readfirstlane(sh.h), w = __builtin_amdgcn_readfirstlane(sh.w);
+    const int pw = sssp_pitch(w);
+    // per pixel: the rect cell index (0 = outside the rect), or -1 outside the rotated crop
+    int cell[PPT];
+    unsigned gpx[PPT];  // (gi << 16) | gj for the Euclidean map
+    unsigned tv[PPT];
 #pragma unroll
-    for (int k = 0; k < PPT; k++) {
-        const unsigned v = tab[tid + k * NT];
-        gpix[k] = v == 0xffffu ? -1 : ((ci0 + (int)(v >> 8)) << 16) | (cj0 + (int)(v & 0xffu));
+    for (int k = 0; k < PPT; k++) tv[k] = tab[tid + k * NT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {  // selects as arithmetic: no exec-mask blocks between the loads
+        const unsigned v = tv[k];
+        const int r = ri0 + (int)(v >> 8), c = rj0 + (int)(v & 0xffu);
+        const int in = (int)((unsigned)r < h) & (int)((unsigned)c < w);
+        cell[k] = (((r + 1) * pw + c + 1) & -in) | -(int)(v == 0xffffu);
+        gpx[k] = ((unsigned)(ci0 + (int)(v >> 8)) << 16) | (unsigned)(cj0 + (int)(v & 0xffu));
     }
+    // vals[0]: Euclidean map (first, envs.py:2083-2084) if present; vals[1 + s]: source s.  Each
+    // branch is wave-uniform and outside the pixel loop, so a channel's loads issue back to back.
     float vals[3][PPT];
-    float mins[3];
-    const float sps = (float)cfg.shortest_path_map_scale;
-    const bool scaled = sh.dist_scaled;
-    const float eus = (float)cfg.distance_to_receptacle_map_scale;
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-        mins[q] = INFINITY;
-        if (q >= nd) continue;
-        const bool eu = q < has_eu;  // Euclidean map first (envs.py:2083-2084)
-        const int s = q - has_eu;
-        const float *D = dist + (eu ? 0 : s) * DIST_FLOATS;
-        const float unreach = eu ? 0.0f : scaled ? sh.unreach[s] : (sh.dmax[s] / 96.0f) * sps;
+    float mins[3] = {INFINITY, INFINITY, INFINITY};
+    if (has_eu) {  // envs.py:2278-2286
+        const float eus = (float)cfg.distance_to_receptacle_map_scale;
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
-            float v = 0.0f;
-            if (gpix[k] >= 0) {
-                const int gi = gpix[k] >> 16, gj = gpix[k] & 0xffff;
-                if (eu) {  // envs.py:2278-2286
-                    const double px = ((gj + 0.5) - (double)W / 2) / PPM, py = ((double)H / 2 - (gi + 0.5)) / PPM;
-                    const double dx = ev.receptacle_x - px, dy = ev.receptacle_y - py;
-                    v = (float)sqrt(dx * dx + dy * dy) * eus;
-                } else {  // envs.py:2288-2300, 2514-2517
-                    const int r = gi - sh.i0, c = gj - sh.j0;
-                    const bool in = r >= 0 && r < sh.h && c >= 0 && c < sh.w;
-                    const float dd = in ? D[(r + 1) * sssp_pitch(sh.w) + c + 1] : __int_as_float(INF_BITS);
-                    if (scaled) v = in ? dd : unreach;
-                    else v = dd != __int_as_float(INF_BITS) ? (dd / 96.0f) * sps : unreach;
-                }
-            }
-            vals[q][k] = v;
-            mins[q] = fminf(mins[q], v);
+            const int gi = gpx[k] >> 16, gj = gpx[k] & 0xffff;
+            const double px = ((gj + 0.5) - (double)W / 2) / PPM, py = ((double)H / 2 - (gi + 0.5)) / PPM;
+            const double dx = ev.receptacle_x - px, dy = ev.receptacle_y - py;
+            const float v = cell[k] < 0 ? 0.0f : (float)sqrt(dx * dx + dy * dy) * eus;
+            vals[0][k] = v;
+            mins[0] = fminf(mins[0], v);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; s++) {  // envs.py:2288-2300, 2514-2517 (scaled in place by sssp_scale)
+        if (s >= nsrc) continue;
+        const lds_float *D = (const lds_float *)(dist + s * DIST_FLOATS);
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const float v = D[max(cell[k], 0)];
+            vals[1 + s][k] = cell[k] < 0 ? 0.0f : v;
+            mins[1 + s] = fminf(mins[1 + s], vals[1 + s][k]);
         }
     }
     if (tid == 0) STAMP_NB(16);
 #pragma unroll
     for (int q = 0; q < 3; q++) {
-        if (q >= nd) continue;
+        if (q == 0 ? !has_eu : q > nsrc) continue;
         const float m = wave_min(mins[q]);
         if ((tid & 63) == 0) sh.red[q][tid >> 6] = m;
     }
@@ -1063,16 +1135,34 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
     if (tid == 0) STAMP_NB(17);
 #pragma unroll
     for (int q = 0; q < 3; q++) {
-        if (q >= nd) continue;
+        if (q == 0 ? !has_eu : q > nsrc) continue;
         float mm = sh.red[q][0];
         for (int k = 1; k < NT / 64; k++) mm = fminf(mm, sh.red[q][k]);
         mins[q] = mm;
     }
 #pragma unroll
     for (int q = 0; q < 3; q++) {
-        if (q >= nd) continue;
+        if (q == 0 ? !has_eu : q > nsrc) continue;
+        const int c = ch + q - 1 + has_eu;
 #pragma unroll
-        for (int k = 0; k < PPT; k++) rc.put(ch + q, tid + k * NT, vals[q][k] - mins[q]);
+        for (int k = 0; k < PPT; k++) rc.put(c, tid + k * NT, vals[q][k] - mins[q]);
+    }
+}
+
+// group g, after sssp_finish and before sssp_scale (debug only): the raw distances of both sources,
+// unreachable / blocked -> -1 (GridGraph.shortest_path_image)
+__device__ __forceinline__ void dump_dist(const Shared &sh, const float *dist, float *out, const Group &g)
+{
+    const int hw = sh.h * sh.w;
+    for (int k = g.t; k < 2 * hw; k += g.n) {
+        const int which = k / hw, rem = k % hw;
+        const int s = sh.sp_slot[which];
+        float v = -1.0f;
+        if (s >= 0) {
+            v = dist[s * DIST_FLOATS + (rem / sh.w + 1) * sssp_pitch(sh.w) + rem % sh.w + 1];
+            if (v == __int_as_float(INF_BITS)) v = -1.0f;
+        }
+        out[k] = v;
     }
 }
 
@@ -1090,6 +1180,11 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const int n = blockIdx.x;
     const int tid = threadIdx.x;
     const int H = cfg.H, W = cfg.W;
+#ifdef SIMAPS_REPEAT  // diagnostic: run the body SIMAPS_REPEAT times (stamps keep the last, warm-cache pass)
+#pragma clang loop unroll(disable)
+    for (int rep = 0; rep < SIMAPS_REPEAT + (int)(n >> 30); rep++) {
+    lds_barrier();
+#endif
     const simaps_agent ag = agents[n];
     // the occupancy window loads first: they depend on the map slot only
     const bool need_cspace = cfg.use_shortest_path_to_receptacle_map || cfg.use_shortest_path_map || dbg.cspace;
@@ -1123,7 +1218,6 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             sh.sp_slot[1] = ns++;
         }
         sh.nsrc = ns;
-        sh.dist_scaled = 0;
     }
     if (tid == 64) {
         const simaps_robot &me = rb[ag.robot];
@@ -1161,11 +1255,29 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             P.bj1 = min(P.bj1, P.bj0 + 31);
         }
         P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
+        P.code0 = (1u << r.group_index) | (r.type != SIMAPS_LIFTING ? 1u << 5 : (!r.lifting ? 1u << 4 : 0u));
     }
+    if (tid >= 512 && tid < 512 + RBLK_PITCH * RBLK_PITCH / 4) sh.rblk[tid - 512] = 0u;
+    // the first history / intention pass's segment table, one lane per robot (raster_lines)
+    if ((cfg.use_history_map || cfg.use_intention_map) && tid >= 320 && tid < 320 + ev.num_robots)
+        seg_table(sh, cfg, rb, paths, cfg.use_history_map ? 4 : cfg.intention_map_encoding, tid - 320, ag.robot);
     lds_barrier();
     if (tid == 0) STAMP_NB(9);
 
     if (cfg.use_intention_channels && tid == 256) intention_channel_order(sh, cfg, rb);
+    // robot sets of the 8 x 8 crop blocks: a stamp box (<= 32 x 32) overlaps <= 5 x 5 blocks
+    if (tid >= 512 && tid < 512 + 25 * ev.num_robots) {
+        const int q = (tid - 512) / 25, d = (tid - 512) % 25;
+        const RobotP &P = sh.rob[q];
+        const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
+        const int a0 = max(P.bi0 - ci0, 0), a1 = min(P.bi1 - ci0, CROP - 1);
+        const int b0 = max(P.bj0 - cj0, 0), b1 = min(P.bj1 - cj0, CROP - 1);
+        const int ba = (a0 >> 3) + d / 5, bb = (b0 >> 3) + d % 5;
+        if (a0 <= a1 && b0 <= b1 && ba <= (a1 >> 3) && bb <= (b1 >> 3)) {
+            const int blk = ba * RBLK_PITCH + bb;
+            atomicOr(&sh.rblk[blk >> 2], (1u << q) << (8 * (blk & 3)));
+        }
+    }
 
     // ---- rotated robot stamps (Mapper._create_global_robot_map, envs.py:2251-2276): each robot's
     // scipy-rotated mask, evaluated once per workgroup into a <= 32 x 32 bit tile at its global box.
@@ -1233,7 +1345,8 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         sssp_rounds(sh, dist, nsrc, g);
 #endif
         sssp_finish(sh, dist, nsrc, g);  // while the render waves finish
-        if (!dbg.dist) sssp_scale(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);
+        if (dbg.dist) dump_dist(sh, dist, dbg.dist + (size_t)n * 2 * sh.h * sh.w, g);
+        sssp_scale(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);
         STAMP_NB(7);
     } else {
         const int nw = NT / 64 - sweep_waves;
@@ -1259,18 +1372,6 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             if (s >= 0) { o[0] = sh.src_q[s][0]; o[1] = sh.src_q[s][1]; o[2] = sh.src_s[s][0]; o[3] = sh.src_s[s][1]; }
             else { o[0] = o[1] = o[2] = o[3] = -1; }
         }
-        if (dbg.dist) {
-            for (int k = tid; k < 2 * sh.h * sh.w; k += NT) {
-                const int which = k / (sh.h * sh.w), rem = k % (sh.h * sh.w);
-                const int s = sh.sp_slot[which];
-                float v = -1.0f;
-                if (s >= 0) {
-                    v = dist[s * DIST_FLOATS + (rem / sh.w + 1) * sssp_pitch(sh.w) + rem % sh.w + 1];
-                    if (v == __int_as_float(INF_BITS)) v = -1.0f;
-                }
-                dbg.dist[(size_t)n * 2 * sh.h * sh.w + k] = v;
-            }
-        }
     }
     if (dbg.status && tid == 0) {
         int st = 0;
@@ -1281,6 +1382,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     }
 #ifdef SIMAPS_PHASE_STAMPS
     if (tid == 0 && blockIdx.x < MAX_STAMP_WG) g_stamps[blockIdx.x * NSTAMP + 10] = (unsigned long long)sh.rounds;
+#endif
+#ifdef SIMAPS_REPEAT
+    }
 #endif
 }
 

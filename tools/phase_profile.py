@@ -47,12 +47,10 @@ def main():
     res = {'config': args.config, 'layout': args.layout, 'N': b.N, 'total_us_median': float(np.median((t[:, 6] - t[:, 0]) / 100.0)),
            'span_us': float((t[:, 6].max() - t[:, 0].min()) / 100.0),
            'split_groups_us': {'sweeps_median': float(np.median(sweeps)), 'render_maps_median': float(np.median(maps)),
-                               'maps_ch01': float(np.median((st[:, 11] - st[:, 3]) / 100.0)),
-                               'ch01_tables_sampleidx_issue': float(np.median((st[:, 14] - st[:, 3]) / 100.0)),
-                               'ch01_robotmap': float(np.median((st[:, 13] - st[:, 14]) / 100.0)),
-                               'ch01_consume_store': float(np.median((st[:, 11] - st[:, 13]) / 100.0)),
-                               'maps_raster': float(np.median((st[:, 12] - st[:, 11]) / 100.0)),
-                               'maps_sample': float(np.median((st[:, 8] - st[:, 12]) / 100.0))},
+                               'sampleidx_raster_gathers': float(np.median((st[:, 14] - st[:, 3]) / 100.0)),
+                               'intention_sample': float(np.median((st[:, 13] - st[:, 14]) / 100.0)),
+                               'overhead_robot_consume': float(np.median((st[:, 11] - st[:, 13]) / 100.0)),
+                               'rest': float(np.median((st[:, 8] - st[:, 11]) / 100.0))},
            'pre_split_us': {'robot_params': float(np.median((st[:, 9] - st[:, 0]) / 100.0)),
                             'stamp_tiles': float(np.median((st[:, 1] - st[:, 9]) / 100.0)),
                             'cspace_stage': float(np.median((st[:, 15] - st[:, 1]) / 100.0)),
