@@ -50,7 +50,7 @@ namespace {
 constexpr int NT = 1024;
 #ifdef SIMAPS_PHASE_STAMPS
 // Diagnostic build only (libsimaps_prof.so): per-workgroup s_memrealtime (100 MHz) stamps.
-constexpr int MAX_STAMP_WG = 8192, NSTAMP = 24;
+constexpr int MAX_STAMP_WG = 8192, NSTAMP = 40;
 __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
 // (a barrier first, so a stamp marks the moment the SLOWEST wave finished the previous phase)
 #define STAMP(k)                                                                                 \
@@ -456,13 +456,15 @@ struct Group {
 // Rotations (no invalid source lanes, no `old` operand): lane 0 / lane 63 receive lane 63 / lane 0,
 // which never own a cell (spans are <= 63 cells for 1 cell per lane, <= 120 for 2), so they carry
 // +inf.
+// (bound_ctrl set: a full-wave rotation has no invalid source lane, and it lets the compiler fold the
+// move into its consumer -- v_add_f32_dpp with the |.| source modifier)
 __device__ __forceinline__ float from_prev_lane(float v)  // lane i <- lane i-1
 {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x13c, 0xf, 0xf, false));  // wave_ror:1
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x13c, 0xf, 0xf, true));  // wave_ror:1
 }
 __device__ __forceinline__ float from_next_lane(float v)  // lane i <- lane i+1
 {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x134, 0xf, 0xf, false));  // wave_rol:1
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x134, 0xf, 0xf, true));  // wave_rol:1
 }
 
 __device__ __forceinline__ int sssp_pitch(int w) { return (w + 2) | 1; }
@@ -471,22 +473,15 @@ constexpr unsigned NINF_BITS = 0xff800000u;  // blocked / border cells
 
 typedef __attribute__((address_space(3))) float lds_float;
 
-// ds_min_f32 for the lanes with `on` set, as ONE inline-asm block: an `if (on) atomicMin(...)` makes
-// the compiler split the sweep step into exec-masked basic blocks, which no instruction scheduling
-// crosses, so each step's latency chain would be fully exposed.  The asm's LDS op is invisible to
-// the compiler's lgkmcnt bookkeeping; an extra in-order op AFTER a load only makes its waits more
-// conservative, and every barrier waits lgkmcnt(0).
-__device__ __forceinline__ void lds_min_masked(lds_float *p, float v, bool on)
+// Unconditional ds_min_f32 of every lane, visible to the compiler.  (An `if (on) atomicMin` splits the
+// step into exec-masked basic blocks no scheduling crosses; a masked inline-asm ds_min is invisible
+// to the compiler's lgkmcnt bookkeeping, so each prefetch wait also drained the previous steps'
+// atomics -- an LDS atomic round trip on every step of the chain.)  min(cell, m) with a real
+// candidate m is a valid relaxation whether or not it improves the cell, and idle lanes write +inf
+// to their own scratch cell, so no lane's write has to be masked.
+__device__ __forceinline__ void lds_min(lds_float *p, float v)
 {
-    const uint64_t m = __ballot(on);
-    uint64_t save;
-    asm volatile(
-        "s_and_saveexec_b64 %0, %1\n\t"
-        "ds_min_f32 %2, %3\n\t"
-        "s_mov_b64 exec, %0"
-        : "=&s"(save)
-        : "s"(m), "v"((unsigned)(uintptr_t)p), "v"(v)
-        : "memory");
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // One sweep of one wave.  DIR: 0 down, 1 up (lines = rows), 2 right, 3 left (lines = columns);
@@ -504,33 +499,40 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw)
     const int a0 = 1 + CPL * lane;
     const bool act = a0 <= span;              // cell 1 of the last lane may be the border
     const int st = act ? (FWD ? sl : -sl) : 0;
-    int cur = act ? (FWD ? 1 : len) * sl + a0 * sa : 0;
-    int pf = cur;
+    // idle lanes: prefetch the -inf corner cell, write +inf to cells of their own (no conflicts)
+    int pf = act ? (FWD ? 1 : len) * sl + a0 * sa : 0;
+    int cur = act ? pf : CPL * lane;
     const float NI = -INFINITY;
     float A0 = D[pf], A1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
     float B0 = D[pf], B1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
     float C0 = D[pf], C1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
     float E0 = D[pf], E1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
+    // p0 / p1: the previous line's values, -inf on blocked cells; consumers take |p| (a free source
+    // modifier, also on the DPP-folded adds), so a blocked cell passes on +inf
     float p0 = INFINITY, p1 = INFINITY;       // the line before the first one: nothing
+    float s2 = SQRT2F;
+    asm volatile("" : "+v"(s2));              // in a VGPR: a DPP-folded add takes no literal / SGPR
     bool chg = false;
 #define SWEEP_STEP(R0, R1, LIVE)                                                                        \
     do {                                                                                                \
         float m0, m1 = INFINITY;                                                                        \
         if (CPL == 2) {                                                                                 \
             const float pm = from_prev_lane(p1), pp = from_next_lane(p0);                               \
-            m0 = fminf(fminf(p0 + 1.0f, pm + SQRT2F), p1 + SQRT2F);                                     \
-            m1 = fminf(fminf(p1 + 1.0f, p0 + SQRT2F), pp + SQRT2F);                                     \
+            m0 = fminf(fminf(fabsf(p0) + 1.0f, fabsf(pm) + s2), fabsf(p1) + s2);                        \
+            m1 = fminf(fminf(fabsf(p1) + 1.0f, fabsf(p0) + s2), fabsf(pp) + s2);                        \
         } else {                                                                                        \
             const float pm = from_prev_lane(p0), pp = from_next_lane(p0);                               \
-            m0 = fminf(fminf(p0 + 1.0f, pm + SQRT2F), pp + SQRT2F);                                     \
+            m0 = fminf(fminf(fabsf(p0) + 1.0f, fabsf(pm) + s2), fabsf(pp) + s2);                        \
         }                                                                                               \
         const bool u0 = (LIVE) && m0 < R0;                                                              \
         const bool u1 = CPL == 2 && (LIVE) && m1 < R1;                                                  \
-        lds_min_masked(&D[cur], m0, u0);                                                                \
-        if (CPL == 2) lds_min_masked(&D[cur + sa], m1, u1);                                             \
+        if (LIVE) { /* wave-uniform: steps past the last line write nothing */                          \
+            lds_min(&D[cur], act ? m0 : INFINITY);                                                      \
+            if (CPL == 2) lds_min(&D[cur + sa], act ? m1 : INFINITY);                                   \
+        }                                                                                               \
         chg |= u0 | u1;                                                                                 \
-        p0 = fabsf(__builtin_elementwise_minimum(m0, R0));                                              \
-        if (CPL == 2) p1 = fabsf(__builtin_elementwise_minimum(m1, R1));                                \
+        p0 = __builtin_elementwise_minimum(m0, R0);                                                     \
+        if (CPL == 2) p1 = __builtin_elementwise_minimum(m1, R1);                                       \
         R0 = D[pf];                                                                                     \
         if (CPL == 2) R1 = D[pf + sa];                                                                  \
         cur += st;                                                                                      \
@@ -597,11 +599,34 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
     const int tid = threadIdx.x, wave = tid >> 6;
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
     const int max_rounds = h * w + 16;  // a converged round changes nothing; the cap guards a bug
+#ifdef SIMAPS_SWEEP_PRIO
+    {   // issue priority: the longer sweeps first (VALU arbitration is priority, then age)
+        const int s = wave >> 2, dir = (wave + 2 * s) & 3;
+        if ((dir >= 2) == (w >= h)) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(2);
+    }
+#endif
     for (int round = 0;; round++) {
         if (tid == 0) sh.changed[(round + 1) % 3] = 0;
         const int s = wave >> 2;
-        if (sh.src_ok[s] && sweep(dist + s * DIST_FLOATS, h, w, pw, wave & 3) && (tid & 63) == 0)
+#ifdef SIMAPS_PHASE_STAMPS
+        if (tid == 0 && round < 4) STAMP_NB(18 + round);
+        if (round == 0) STAMP_NB(32 + wave);
+#endif
+        // waves go to SIMD (wave % 4): source 1's directions are rotated by 2 so that every SIMD
+        // hosts one row sweep and one column sweep (the long ones would otherwise share two SIMDs)
+#ifdef SIMAPS_DIAG_SWAP_ARRAYS  // diagnostic: waves 0-3 sweep array 1, waves 4-7 array 0
+        const int arr = nsrc == 2 ? 1 - s : s;
+#else
+        const int arr = s;
+#endif
+        if (sh.src_ok[arr] && sweep(dist + arr * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3) && (tid & 63) == 0)
             sh.changed[round % 3] = 1;
+#ifdef SIMAPS_PHASE_STAMPS
+        if (round == 0 && wave == 0) STAMP_NB(22);
+        if (round == 0 && wave == 2) STAMP_NB(23);
+        if (round == 0) STAMP_NB(24 + wave);
+#endif
         g.sync();
         if (!sh.changed[round % 3] || round >= max_rounds) {
             if (tid == 0) sh.rounds = round >= max_rounds ? -1 : round + 1;
@@ -1957,7 +1982,7 @@ extern "C" {
 int simaps_abi_version(void) { return SIMAPS_ABI_VERSION; }
 
 #ifdef SIMAPS_PHASE_STAMPS
-// Diagnostic build only: copy the stamp table (uint64 [8192][24]) to host memory.
+// Diagnostic build only: copy the stamp table (uint64 [8192][NSTAMP]) to host memory.
 int simaps_debug_read_stamps(unsigned long long *host_out)
 {
     return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : SIMAPS_EHIP;

@@ -35,7 +35,7 @@ def main():
     for _ in range(3):
         b.render(out)
     torch.cuda.synchronize()
-    st = np.zeros((8192, 24), dtype=np.uint64)
+    st = np.zeros((8192, 40), dtype=np.uint64)
     b.render(out)
     torch.cuda.synchronize()
     assert L.simaps_debug_read_stamps(st.ctypes.data) == 0
@@ -58,6 +58,11 @@ def main():
            'distance_us': {'values': float(np.median((st[:, 16] - st[:, 5]) / 100.0)),
                            'block_min': float(np.median((st[:, 17] - st[:, 16]) / 100.0)),
                            'stores': float(np.median((st[:, 6] - st[:, 17]) / 100.0))},
+           'sweep_rounds_us': {'round_%d' % r: float(np.median((st[:, 19 + r] - st[:, 18 + r]) / 100.0)) for r in range(3)},
+           'first_sweep_us': {'down(w0)': float(np.median((st[:, 22] - st[:, 18]) / 100.0)),
+                              'right(w2)': float(np.median((st[:, 23] - st[:, 18]) / 100.0))},
+           'wave_sweep_r0_us': {'start': [float(np.median((st[:, 32 + w] - st[:, 18]) / 100.0)) for w in range(8)],
+                                'end': [float(np.median((st[:, 24 + w] - st[:, 18]) / 100.0)) for w in range(8)]},
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())},
            'phases_us': {p: {'median': float(np.median(d[:, i])), 'max': float(d[:, i].max())}
                          for i, p in enumerate(PHASES)}}
