@@ -50,7 +50,7 @@ namespace {
 constexpr int NT = 1024;
 #ifdef SIMAPS_PHASE_STAMPS
 // Diagnostic build only (libsimaps_prof.so): per-workgroup s_memrealtime (100 MHz) stamps.
-constexpr int MAX_STAMP_WG = 8192, NSTAMP = 40;
+constexpr int MAX_STAMP_WG = 8192, NSTAMP = 48;
 __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
 // (a barrier first, so a stamp marks the moment the SLOWEST wave finished the previous phase)
 #define STAMP(k)                                                                                 \
@@ -885,6 +885,9 @@ __device__ __forceinline__ unsigned robot_bits(const RobotP &P, int gi, int gj)
     return bits;
 }
 
+// NPT: output pixels per render thread (18 / 12 / 9 for 8 / 12 / 16 render waves), a compile-time
+// constant so every pixel loop is exact (no bounds tests) and its index math folds.
+template <int NPT>
 __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry &geo, const float *__restrict__ ovh,
                             const simaps_robot *rb, const double *__restrict__ paths, float *tile)
 {
@@ -896,19 +899,21 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     const int cj0 = __builtin_amdgcn_readfirstlane(sh.pj - HALF_CROP);
     // the sample index of each of this thread's output pixels (fast fp32 path, exact fp64 fallback),
     // packed 2 per register: crop-relative (row << 8 | col), 0xffff = outside (cval)
-    constexpr int MAXPG = 18;  // output pixels per render thread (>= 8 render waves)
-    uint32_t gqp[MAXPG / 2];
+    constexpr int MAXPG = NPT;
+    constexpr int GN = NP / NPT;  // == g.n
+    static_assert(GN * NPT == NP && GN % 64 == 0, "render group split");
+    uint32_t gqp[(MAXPG + 1) / 2];
     {
         const Rot R = sh.rot;
         const float c = (float)R.c, sn = (float)R.s, f0 = (float)R.f0, f1 = (float)R.f1;
         const int oa = R.S0 / 2 - LW / 2, ob = R.S1 / 2 - LW / 2;
         const float hi = CROP - 1;
-        int a = g.t / LW, b = g.t % LW;  // pixel p = g.t + k * g.n, walked incrementally
-        const int da = g.n / LW, db = g.n % LW;
+        int a = g.t / LW, b = g.t % LW;  // pixel p = g.t + k * GN, walked incrementally
+        constexpr int da = GN / LW, db = GN % LW;
 #pragma unroll
         for (int k = 0; k < MAXPG; k++) {
             uint32_t v = 0xffffu;
-            if (a < LW) {
+            {
 #if defined(SIMAPS_ABL_NOGPIX)
                 v = ((uint32_t)(a + 20) << 8) | (uint32_t)(b + 20);
 #else
@@ -928,22 +933,28 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
 #endif
             }
             if (k & 1) gqp[k >> 1] |= v << 16;
-            else gqp[k >> 1] = v;
+            else gqp[k >> 1] = v | (k == MAXPG - 1 ? 0xffff0000u : 0u);
             a += da;
             b += db;
-            if (b >= LW) { b -= LW; a++; }
+            if (db && b >= LW) { b -= LW; a++; }
         }
+#ifdef SIMAPS_PHASE_STAMPS
+        if (g.t == 0) {
+            asm volatile("" ::"v"(gqp[0]), "v"(gqp[8]));
+            STAMP_NB(40);
+        }
+#endif
         // the pixels in the rounding band: exact fp64 rot_src (a separate pass keeps the fp64
         // temporaries out of the fast loop's register budget)
         bool any = false;
 #pragma unroll
-        for (int k = 0; k < MAXPG / 2; k++) any |= ((gqp[k] & 0xffffu) == 0xfffeu) | ((gqp[k] >> 16) == 0xfffeu);
+        for (int k = 0; k < (MAXPG + 1) / 2; k++) any |= ((gqp[k] & 0xffffu) == 0xfffeu) | ((gqp[k] >> 16) == 0xfffeu);
         if (any) {
 #pragma unroll
             for (int k = 0; k < MAXPG; k++) {
                 const uint32_t cur = (gqp[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
                 if (cur == 0xfffeu) {
-                    const int p = g.t + k * g.n;
+                    const int p = g.t + k * GN;
                     int i0, i1;
                     uint32_t v = 0xffffu;
                     if (rot_src(R, CROP, p / LW + oa, p % LW + ob, i0, i1)) {
@@ -965,9 +976,16 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     if (cfg.use_history_map) encs[npass++] = 4;
     if (cfg.use_intention_map) encs[npass++] = cfg.intention_map_encoding;
     const int thick = cfg.intention_map_line_thickness;
+#ifdef SIMAPS_PHASE_STAMPS
+    if (g.t == 0) {
+        asm volatile("" ::"v"(gqp[0]), "v"(gqp[8]));
+        STAMP_NB(41);
+    }
+#endif
 #ifndef SIMAPS_ABL_NORASTER
     if (npass > 0) raster_lines(sh, tile, cfg, rb, paths, encs[0], true, g);
 #endif
+    if (g.t == 0) STAMP_NB(42);
     // every overhead gather of the thread in flight at once, issued after the first raster (whose
     // integer divisions and fp64 need the registers); the intention samples and stores run meanwhile
     float ovv[MAXPG];
@@ -994,11 +1012,10 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         if (g.t == 0) STAMP_NB(12);
 #pragma unroll
         for (int k = 0; k < MAXPG; k++) {
-            const int p = g.t + k * g.n;
+            const int p = g.t + k * GN;
             uint32_t v = gq_v(k);
             asm volatile("" : "+v"(v));
-            if (p < NP)
-                rc.put(c, p, v != 0xffffu ? tile_sample(tile, ci0 + (int)(v >> 8), cj0 + (int)(v & 0xffu), sh.pi, sh.pj) : 0.0f);
+            rc.put(c, p, v != 0xffffu ? tile_sample(tile, ci0 + (int)(v >> 8), cj0 + (int)(v & 0xffu), sh.pi, sh.pj) : 0.0f);
         }
         g.sync();
     };
@@ -1009,8 +1026,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     const uint8_t *rblk = reinterpret_cast<const uint8_t *>(sh.rblk);
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
-        const int p = g.t + k * g.n;
-        if (p >= NP) break;
+        const int p = g.t + k * GN;
         // an outside pixel (0xffff) reads block (31, 31), which no robot touches.  (The asm keeps the
         // per-pixel index math and validity test here instead of hoisted above the gathers, where 18
         // pixels' worth of it would not fit the register budget.)
@@ -1056,8 +1072,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
                 const RobotP &R = sh.rob[kq];
 #pragma unroll
                 for (int k = 0; k < MAXPG; k++) {
-                    const int p = g.t + k * g.n;
-                    if (p >= NP) continue;
+                    const int p = g.t + k * GN;
                     const uint32_t v = gq_v(k);
                     float val = 0.0f;
                     if (v != 0xffffu && !R.idle) {
@@ -1070,7 +1085,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
                 ch++;
             } else {
                 for (int e = 0; e < 2; e++, ch++, c2++)
-                    for (int p = g.t; p < NP; p += g.n) rc.put(ch, p, sh.nonsp[c2]);
+                    for (int k = 0; k < MAXPG; k++) rc.put(ch, g.t + k * GN, sh.nonsp[c2]);
             }
         }
     }
@@ -1079,8 +1094,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     uint16_t *tab = reinterpret_cast<uint16_t *>(tile);
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
-        const int p = g.t + k * g.n;
-        if (p < NP) tab[p] = (uint16_t)gq_v(k);
+        tab[g.t + k * GN] = (uint16_t)gq_v(k);
     }
 }
 
@@ -1377,7 +1391,10 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         const int nw = NT / 64 - sweep_waves;
         const Group g{tid - 64 * sweep_waves, 64 * nw, sweep_waves ? sh.bar[1] : nullptr, nw};
 #ifndef SIMAPS_ABL_NORENDER  // diagnostic: sweeps alone (output channels 0.. left unwritten)
-        render_maps(rc, g, geo, overhead + (size_t)ag.map_slot * H * W, rb, paths, tile);
+        const float *ovh = overhead + (size_t)ag.map_slot * H * W;
+        if (nw == 8) render_maps<18>(rc, g, geo, ovh, rb, paths, tile);
+        else if (nw == 12) render_maps<12>(rc, g, geo, ovh, rb, paths, tile);
+        else render_maps<9>(rc, g, geo, ovh, rb, paths, tile);
 #endif
         if (g.t == 0) STAMP_NB(8);
     }

@@ -35,7 +35,7 @@ def main():
     for _ in range(3):
         b.render(out)
     torch.cuda.synchronize()
-    st = np.zeros((8192, 40), dtype=np.uint64)
+    st = np.zeros((8192, 48), dtype=np.uint64)
     b.render(out)
     torch.cuda.synchronize()
     assert L.simaps_debug_read_stamps(st.ctypes.data) == 0
@@ -63,6 +63,10 @@ def main():
                               'right(w2)': float(np.median((st[:, 23] - st[:, 18]) / 100.0))},
            'wave_sweep_r0_us': {'start': [float(np.median((st[:, 32 + w] - st[:, 18]) / 100.0)) for w in range(8)],
                                 'end': [float(np.median((st[:, 24 + w] - st[:, 18]) / 100.0)) for w in range(8)]},
+           'render_front_us': {'sampleidx_fast': float(np.median((st[:, 40] - st[:, 3]) / 100.0)),
+                               'sampleidx_fp64': float(np.median((st[:, 41] - st[:, 40]) / 100.0)),
+                               'raster1': float(np.median((st[:, 42] - st[:, 41]) / 100.0)),
+                               'gather_issue': float(np.median((st[:, 14] - st[:, 42]) / 100.0))},
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())},
            'phases_us': {p: {'median': float(np.median(d[:, i])), 'max': float(d[:, i].max())}
                          for i, p in enumerate(PHASES)}}
