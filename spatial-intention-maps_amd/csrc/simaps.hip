@@ -133,6 +133,48 @@ __device__ __forceinline__ void lds_barrier()
 }
 
 // ------------------------------------------------------------------------------------------------
+// Wave groups: the workgroup splits into SSSP-sweep waves and render waves that run concurrently.
+// A group of fewer than 16 waves synchronises through an LDS barrier (lane 0 of each wave arrives
+// on a counter; the last one bumps a generation word the others poll with s_sleep; bounded spin).
+// ------------------------------------------------------------------------------------------------
+struct Group {
+    int t, n;           // thread index within the group, threads in the group
+    unsigned *bar;      // nullptr: the whole workgroup (__syncthreads)
+    int nw;             // waves in the group
+    __device__ void sync() const
+    {
+        if (!bar) {
+            lds_barrier();
+            return;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        // relaxed LDS atomics, ordered by the local-only fences around them: acquire / release
+        // orderings on the atomics themselves would also wait for every outstanding GLOBAL access
+        // of the wave (vmcnt(0)), exposing the render group's gather / store latency at each sync
+        if ((threadIdx.x & 63) == 0) {
+            const unsigned g = __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const unsigned arrived = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (arrived == (unsigned)nw - 1) {
+                __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(&bar[1], g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                unsigned spins = 0;
+                while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == g) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 22)) {  // ~0.1 s: never in a correct run; flag and fall through
+                        __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        break;
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    }
+};
+
+__device__ __forceinline__ Group whole_wg() { return Group{(int)threadIdx.x, 1024, nullptr, 16}; }
+
+// ------------------------------------------------------------------------------------------------
 // LDS layout
 // ------------------------------------------------------------------------------------------------
 struct RobotP {
@@ -176,6 +218,8 @@ struct Shared {
     unsigned bar[2][4];              // group barriers {count, generation, timeout, -}: [0] sweeps, [1] render
     uint32_t rblk[RBLK_PITCH * RBLK_PITCH / 4];  // per 8 x 8 crop block: bit q = robot q's stamp box overlaps it
     int changed[3];                  // rotating per-round "some sweep improved a cell" flags
+    int scratch_free;                // the cspace scratch may be reused as the raster tile
+    uint32_t mwin[5 * 24 + 20];      // robot mask windows: [5][24] bit rows + [5][4] ints (stamp tiles)
     Seg seg[MAX_SEG];
 };
 
@@ -227,29 +271,33 @@ __device__ __forceinline__ float wave_max(float v)
 // Phase: occupancy window -> free-cell bit rows (cspace inside the room rect)
 // ------------------------------------------------------------------------------------------------
 // occ: the agent's occupancy map [H, W] (nonzero = obstacle).  r = disk radius (<= RMAX).
-// The window loads are issued at kernel start (cspace_load, for the largest radius, so they do not
-// wait for the robot descriptor) and land in registers while the params phase runs.
+// The window loads are issued first thing by the group that builds the cspace (cspace_load, for the
+// largest radius, so they need no robot descriptor) and land in registers.
 constexpr int RMAX = 7;  // floor(RADIUS * 96) <= 6 for every robot class (envs.py:2421)
+// G threads cover the window: words 0-1 of a row (columns 0..127): thread -> (row t / 128 + (G / 128) q,
+// column t % 128), so every wave holds 64 consecutive columns of one row (one ballot per row word);
+// word 2 (columns 128..133): thread -> (row 8 * wave + lane / 8 + (G / 8) u, column 128 + lane % 8).
+template <int G>
 struct OccLoad {
-    uint8_t v[16], v2;
+    static constexpr int NQ = 16384 / G, NU = 1024 / G;  // 128 rows x 128 columns, 128 rows x 8 columns
+    uint8_t v[NQ], v2[NU];
 };
-// Words 0-1 of a window row: thread -> (row tid / 128 + 8q, column tid % 128), so every wave holds
-// 64 consecutive columns of one row (one ballot per row word).  Word 2 (columns 128..133): thread ->
-// (row 8 * wave + lane / 8, column 128 + lane % 8).
-__device__ __forceinline__ void cspace_load(OccLoad &L, const uint8_t *__restrict__ occ, int H, int W, int i0, int j0,
-                                            int h, int w)
+template <int G>
+__device__ __forceinline__ void cspace_load(OccLoad<G> &L, const uint8_t *__restrict__ occ, int H, int W, int i0, int j0,
+                                            int h, int w, int t)
 {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lane = t & 63, wave = t >> 6;
     const int wh = h + 2 * RMAX, ww = w + 2 * RMAX;  // <= 126 x 134
-    const int c = tid & 127, r0 = tid >> 7;
+    const int c = t & 127, r0 = t >> 7;
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
-        const int rr = r0 + 8 * q, gi = i0 - RMAX + rr, gj = j0 - RMAX + c;
+    for (int q = 0; q < OccLoad<G>::NQ; q++) {
+        const int rr = r0 + (G / 128) * q, gi = i0 - RMAX + rr, gj = j0 - RMAX + c;
         L.v[q] = (rr < wh && c < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
     }
-    {
-        const int rr = 8 * wave + (lane >> 3), cc = 128 + (lane & 7), gi = i0 - RMAX + rr, gj = j0 - RMAX + cc;
-        L.v2 = (rr < wh && cc < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
+#pragma unroll
+    for (int u = 0; u < OccLoad<G>::NU; u++) {
+        const int rr = 8 * wave + (lane >> 3) + (G / 8) * u, cc = 128 + (lane & 7), gi = i0 - RMAX + rr, gj = j0 - RMAX + cc;
+        L.v2[u] = (rr < wh && cc < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
     }
 }
 
@@ -266,31 +314,36 @@ __device__ __forceinline__ unsigned row16_or(unsigned x)
 // S.win rows (RMAX-window coordinates) -> S.freeb: 1 - max(1 - room_mask, binary_dilation(occ, disk(r)))
 // inside the room rect (envs.py:2453).  No LDS staging, no atomics: window words come straight from
 // the loaded registers by ballots; each 16-lane DPP row computes one output row, lane = disk row dy.
-__device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad &L, int h, int w, int r)
+// Group g (g.n == G threads) -- the whole workgroup, or the sweep group while the render group works.
+template <int G>
+__device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L, int h, int w, int r, const Group &g)
 {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = g.t, lane = t & 63, wave = t >> 6;
     const int whM = h + 2 * RMAX, wwM = w + 2 * RMAX;
     {
-        const int c = tid & 127, r0 = tid >> 7;
+        const int c = t & 127, r0 = t >> 7;
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const int rr = r0 + 8 * q;
+        for (int q = 0; q < OccLoad<G>::NQ; q++) {
+            const int rr = r0 + (G / 128) * q;
             const uint64_t m = __ballot(rr < whM && c < wwM && L.v[q] != 0);
             if (lane == 0 && rr < whM) S.win[rr][wave & 1] = m;
         }
-        const int rr = 8 * wave + (lane >> 3), cc = 128 + (lane & 7);
-        const uint64_t m = __ballot(rr < whM && cc < wwM && L.v2 != 0);
-        if (lane < 8 && 8 * wave + lane < whM) S.win[8 * wave + lane][2] = (m >> (8 * lane)) & 0xffu;
+#pragma unroll
+        for (int u = 0; u < OccLoad<G>::NU; u++) {
+            const int rb = 8 * wave + (G / 8) * u, rr = rb + (lane >> 3), cc = 128 + (lane & 7);
+            const uint64_t m = __ballot(rr < whM && cc < wwM && L.v2[u] != 0);
+            if (lane < 8 && rb + lane < whM) S.win[rb + lane][2] = (m >> (8 * lane)) & 0xffu;
+        }
     }
-    lds_barrier();
-    if (threadIdx.x == 0) STAMP_NB(15);
+    g.sync();
+    if (t == 0) STAMP_NB(15);
     const B128 fm = b_mask(w);
-    const int dy = (tid & 15) - r;
+    const int dy = (t & 15) - r;
     int hw = -1;  // disk(r) half-width of row dy (skimage disk: dx^2 + dy^2 <= r^2)
     if (dy <= r)
         while ((hw + 1) * (hw + 1) + dy * dy <= r * r) hw++;
-    for (int base = 0; base < h; base += NT / 16) {  // uniform: every lane takes part in the DPP ORs
-        const int row = base + (tid >> 4);
+    for (int base = 0; base < h; base += G / 16) {  // uniform: every lane takes part in the DPP ORs
+        const int row = base + (t >> 4);
         B128 acc = {0, 0};
         if (row < h && hw >= 0) {
             const uint64_t *wrow = S.win[row + RMAX + dy];
@@ -298,20 +351,20 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad &L, i
         }
         const unsigned a0 = row16_or((unsigned)acc.lo), a1 = row16_or((unsigned)(acc.lo >> 32));
         const unsigned a2 = row16_or((unsigned)acc.hi), a3 = row16_or((unsigned)(acc.hi >> 32));
-        if ((tid & 15) == 0 && row < h) {
+        if ((t & 15) == 0 && row < h) {
             const uint64_t lo = ((uint64_t)a1 << 32) | a0, hi = ((uint64_t)a3 << 32) | a2;
             S.freeb[row] = {~lo & fm.lo, ~hi & fm.hi};
         }
     }
-    lds_barrier();
+    g.sync();
 }
 
 // ------------------------------------------------------------------------------------------------
 // Phase: snap the query pixels to the closest free cell (scipy EDT feature transform at q)
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc)
+__device__ __forceinline__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc, const Group &g)
 {
-    const int tid = threadIdx.x;
+    const int tid = g.t;
     const int h = sh.h, w = sh.w, i0 = sh.i0, j0 = sh.j0;
     // fast path (the common case): a free query pixel is its own nearest free cell (EDT distance 0)
     if (tid < nsrc) {
@@ -323,12 +376,12 @@ __device__ __forceinline__ void snap_sources(Shared &sh, SsspScratch &S, int nsr
             sh.src_s[tid][1] = sh.src_q[tid][1];
         }
     }
-    lds_barrier();
+    g.sync();
     bool slow = false;
     for (int s = 0; s < nsrc; s++) slow |= !sh.src_ok[s];
     if (!slow) return;
     // pass 1 (scipy: per column along axis 0): nearest free row of each rect column, ties low
-    for (int item = tid; item < nsrc * 128; item += NT) {  // w <= 120 columns per source
+    for (int item = tid; item < nsrc * 128; item += g.n) {  // w <= 120 columns per source
         const int s = item >> 7, c = item & 127;
         if (c >= w || sh.src_ok[s]) continue;
         const int qi = sh.src_q[s][0];
@@ -341,7 +394,7 @@ __device__ __forceinline__ void snap_sources(Shared &sh, SsspScratch &S, int nsr
         }
         sh.colbest[s][c] = best;
     }
-    lds_barrier();
+    g.sync();
     // pass 2 (scipy _VoronoiFT along axis 1), one lane per source
     if ((tid & 63) == 0 && (tid >> 6) < nsrc && !sh.src_ok[tid >> 6]) {
         const int s = tid >> 6;
@@ -390,48 +443,8 @@ __device__ __forceinline__ void snap_sources(Shared &sh, SsspScratch &S, int nsr
             }
         }
     }
-    lds_barrier();
+    g.sync();
 }
-
-// ------------------------------------------------------------------------------------------------
-// Wave groups: the workgroup splits into SSSP-sweep waves and render waves that run concurrently.
-// A group of fewer than 16 waves synchronises through an LDS barrier (lane 0 of each wave arrives
-// on a counter; the last one bumps a generation word the others poll with s_sleep; bounded spin).
-// ------------------------------------------------------------------------------------------------
-struct Group {
-    int t, n;           // thread index within the group, threads in the group
-    unsigned *bar;      // nullptr: the whole workgroup (__syncthreads)
-    int nw;             // waves in the group
-    __device__ void sync() const
-    {
-        if (!bar) {
-            lds_barrier();
-            return;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        // relaxed LDS atomics, ordered by the local-only fences around them: acquire / release
-        // orderings on the atomics themselves would also wait for every outstanding GLOBAL access
-        // of the wave (vmcnt(0)), exposing the render group's gather / store latency at each sync
-        if ((threadIdx.x & 63) == 0) {
-            const unsigned g = __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const unsigned arrived = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (arrived == (unsigned)nw - 1) {
-                __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_store(&bar[1], g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-                unsigned spins = 0;
-                while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == g) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 22)) {  // ~0.1 s: never in a correct run; flag and fall through
-                        __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        break;
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    }
-};
 
 // ------------------------------------------------------------------------------------------------
 // Phase: single-source shortest paths for nsrc sources over the free cells of the rect
@@ -485,73 +498,90 @@ __device__ __forceinline__ void lds_min(lds_float *p, float v)
 }
 
 // One sweep of one wave.  DIR: 0 down, 1 up (lines = rows), 2 right, 3 left (lines = columns);
-// CPL: cells per lane across the line (1: span <= 63, 2: span <= 120).  Returns true if a lane
-// found an improvement.  Lines are prefetched P steps ahead into a ring of named registers;
-// lanes past the span sit on the -inf corner cell.
-template <int DIR, int CPL>
-__device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw)
+// CPL: cells per lane across the line (1: span <= 63, 2: span <= 120); PWC: the pitch when known at
+// compile time (0: runtime).  Returns true if a lane found an improvement.  Lines are prefetched P
+// steps ahead into a ring of named registers.
+// Every lane strides through memory the same way (one base per group of P steps, immediate offsets,
+// no per-lane address arithmetic): lanes past the span alias the cells of active lanes and are made
+// inert by per-lane constants instead of selects -- their edge weights are +inf (candidates +inf:
+// the atomic min leaves the aliased cell alone and `candidate < cell` is false) and their passed-on
+// value is minimum(., -inf) = -inf (|.| = +inf reaches the neighbouring lanes).
+template <int DIR, int CPL, int PWC>
+__device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw_rt)
 {
     constexpr bool VERT = DIR < 2, FWD = (DIR & 1) == 0;
     constexpr int P = 4;
+    const int pw = PWC ? PWC : pw_rt;
     const int lane = threadIdx.x & 63;
     const int sl = VERT ? pw : 1;             // address stride along the sweep (line to line)
     const int sa = VERT ? 1 : pw;             // across the line (cell 0 -> cell 1 of a lane)
-    const int a0 = 1 + CPL * lane;
-    const bool act = a0 <= span;              // cell 1 of the last lane may be the border
-    const int st = act ? (FWD ? sl : -sl) : 0;
-    // idle lanes: prefetch the -inf corner cell, write +inf to cells of their own (no conflicts)
-    int pf = act ? (FWD ? 1 : len) * sl + a0 * sa : 0;
-    int cur = act ? pf : CPL * lane;
+    const int nact = (span + CPL - 1) / CPL;  // lanes owning a cell (>= 1)
+    const bool act = lane < nact;
+    const int own = act ? lane : lane & ((1 << (31 - __clz(nact))) - 1);
+    lds_float *Dl = D + (1 + CPL * own) * sa;
+    // line of step t: FWD 1 + t, else len - t.  Group base at step t0: lines t0 .. t0 + 2P - 1 at
+    // non-negative offsets (ds offsets are unsigned)
+    auto gbase = [&](int t0) { return FWD ? Dl + (1 + t0) * sl : Dl + (len - t0 - (2 * P - 1)) * sl; };
+    auto goff = [&](int j) { return FWD ? j * sl : (2 * P - 1 - j) * sl; };
+    float one = act ? 1.0f : INFINITY, s2 = act ? SQRT2F : INFINITY, X = act ? INFINITY : -INFINITY;
+    asm volatile("" : "+v"(one), "+v"(s2), "+v"(X));  // VGPR operands (DPP-folded adds take no literal)
     const float NI = -INFINITY;
-    float A0 = D[pf], A1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
-    float B0 = D[pf], B1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
-    float C0 = D[pf], C1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
-    float E0 = D[pf], E1 = CPL == 2 ? D[pf + sa] : NI; pf += st;
+    lds_float *G = gbase(0);
+    float A0 = G[goff(0)], A1 = CPL == 2 ? G[goff(0) + sa] : NI;
+    float B0 = G[goff(1)], B1 = CPL == 2 ? G[goff(1) + sa] : NI;
+    float C0 = G[goff(2)], C1 = CPL == 2 ? G[goff(2) + sa] : NI;
+    float E0 = G[goff(3)], E1 = CPL == 2 ? G[goff(3) + sa] : NI;
     // p0 / p1: the previous line's values, -inf on blocked cells; consumers take |p| (a free source
     // modifier, also on the DPP-folded adds), so a blocked cell passes on +inf
     float p0 = INFINITY, p1 = INFINITY;       // the line before the first one: nothing
-    float s2 = SQRT2F;
-    asm volatile("" : "+v"(s2));              // in a VGPR: a DPP-folded add takes no literal / SGPR
-    bool chg = false;
-#define SWEEP_STEP(R0, R1, LIVE)                                                                        \
+    uint64_t chg = 0;
+#define SWEEP_STEP(R0, R1, J, LIVE)                                                                     \
     do {                                                                                                \
         float m0, m1 = INFINITY;                                                                        \
         if (CPL == 2) {                                                                                 \
             const float pm = from_prev_lane(p1), pp = from_next_lane(p0);                               \
-            m0 = fminf(fminf(fabsf(p0) + 1.0f, fabsf(pm) + s2), fabsf(p1) + s2);                        \
-            m1 = fminf(fminf(fabsf(p1) + 1.0f, fabsf(p0) + s2), fabsf(pp) + s2);                        \
+            m0 = fminf(fminf(fabsf(p0) + one, fabsf(pm) + s2), fabsf(p1) + s2);                         \
+            m1 = fminf(fminf(fabsf(p1) + one, fabsf(p0) + s2), fabsf(pp) + s2);                         \
         } else {                                                                                        \
             const float pm = from_prev_lane(p0), pp = from_next_lane(p0);                               \
-            m0 = fminf(fminf(fabsf(p0) + 1.0f, fabsf(pm) + s2), fabsf(pp) + s2);                        \
+            m0 = fminf(fminf(fabsf(p0) + one, fabsf(pm) + s2), fabsf(pp) + s2);                         \
         }                                                                                               \
-        const bool u0 = (LIVE) && m0 < R0;                                                              \
-        const bool u1 = CPL == 2 && (LIVE) && m1 < R1;                                                  \
+        /* improvements as wave masks (v_cmp -> SGPRs, s_or): no per-lane flag arithmetic */            \
+        const uint64_t u0 = (LIVE) ? __builtin_amdgcn_ballot_w64(m0 < R0) : 0;                          \
+        const uint64_t u1 = CPL == 2 && (LIVE) ? __builtin_amdgcn_ballot_w64(m1 < R1) : 0;              \
         if (LIVE) { /* wave-uniform: steps past the last line write nothing */                          \
-            lds_min(&D[cur], act ? m0 : INFINITY);                                                      \
-            if (CPL == 2) lds_min(&D[cur + sa], act ? m1 : INFINITY);                                   \
+            SWEEP_WRITE(&G[goff(J)], m0, R0);                                                           \
+            if (CPL == 2) SWEEP_WRITE(&G[goff(J) + sa], m1, R1);                                        \
         }                                                                                               \
         chg |= u0 | u1;                                                                                 \
-        p0 = __builtin_elementwise_minimum(m0, R0);                                                     \
-        if (CPL == 2) p1 = __builtin_elementwise_minimum(m1, R1);                                       \
-        R0 = D[pf];                                                                                     \
-        if (CPL == 2) R1 = D[pf + sa];                                                                  \
-        cur += st;                                                                                      \
-        pf += st;                                                                                       \
+        p0 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m0, R0), X);                   \
+        if (CPL == 2) p1 = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m1, R1), X);     \
+        R0 = G[goff((J) + P)];                                                                          \
+        if (CPL == 2) R1 = G[goff((J) + P) + sa];                                                       \
     } while (0)
+#ifdef SIMAPS_DIAG_PLAINSTORE  // diagnostic (wrong results): plain stores instead of LDS atomic min
+#define SWEEP_WRITE(P_, V_, R_) (*(P_) = fminf((V_), (R_)))
+#else
+#define SWEEP_WRITE(P_, V_, R_) lds_min((P_), (V_))
+#endif
     int t = 0;
+#pragma unroll 4
     for (; t + P <= len; t += P) {
-        SWEEP_STEP(A0, A1, true);
-        SWEEP_STEP(B0, B1, true);
-        SWEEP_STEP(C0, C1, true);
-        SWEEP_STEP(E0, E1, true);
+        G = gbase(t);
+        SWEEP_STEP(A0, A1, 0, true);
+        SWEEP_STEP(B0, B1, 1, true);
+        SWEEP_STEP(C0, C1, 2, true);
+        SWEEP_STEP(E0, E1, 3, true);
     }
     if (t < len) {  // 1..3 remaining lines; steps past the end store nothing
-        SWEEP_STEP(A0, A1, t < len);
-        SWEEP_STEP(B0, B1, t + 1 < len);
-        SWEEP_STEP(C0, C1, t + 2 < len);
+        G = gbase(t);
+        SWEEP_STEP(A0, A1, 0, t < len);
+        SWEEP_STEP(B0, B1, 1, t + 1 < len);
+        SWEEP_STEP(C0, C1, 2, t + 2 < len);
     }
 #undef SWEEP_STEP
-    return __ballot(chg) != 0;
+#undef SWEEP_WRITE
+    return chg != 0;
 }
 
 __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_in)
@@ -562,25 +592,34 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
     h = __builtin_amdgcn_readfirstlane(h);
     w = __builtin_amdgcn_readfirstlane(w);
     pw = __builtin_amdgcn_readfirstlane(pw);
+    // every BASELINE room is 92 columns wide (pitch 95): its sweeps get immediate-offset addressing
+    if (pw == 95) {
+        switch (dir) {
+        case 0: return sweep_t<0, 2, 95>(D, h, w, pw);
+        case 1: return sweep_t<1, 2, 95>(D, h, w, pw);
+        case 2: return h <= 63 ? sweep_t<2, 1, 95>(D, w, h, pw) : sweep_t<2, 2, 95>(D, w, h, pw);
+        default: return h <= 63 ? sweep_t<3, 1, 95>(D, w, h, pw) : sweep_t<3, 2, 95>(D, w, h, pw);
+        }
+    }
     switch (dir) {
-    case 0: return w <= 63 ? sweep_t<0, 1>(D, h, w, pw) : sweep_t<0, 2>(D, h, w, pw);
-    case 1: return w <= 63 ? sweep_t<1, 1>(D, h, w, pw) : sweep_t<1, 2>(D, h, w, pw);
-    case 2: return h <= 63 ? sweep_t<2, 1>(D, w, h, pw) : sweep_t<2, 2>(D, w, h, pw);
-    default: return h <= 63 ? sweep_t<3, 1>(D, w, h, pw) : sweep_t<3, 2>(D, w, h, pw);
+    case 0: return w <= 63 ? sweep_t<0, 1, 0>(D, h, w, pw) : sweep_t<0, 2, 0>(D, h, w, pw);
+    case 1: return w <= 63 ? sweep_t<1, 1, 0>(D, h, w, pw) : sweep_t<1, 2, 0>(D, h, w, pw);
+    case 2: return h <= 63 ? sweep_t<2, 1, 0>(D, w, h, pw) : sweep_t<2, 2, 0>(D, w, h, pw);
+    default: return h <= 63 ? sweep_t<3, 1, 0>(D, w, h, pw) : sweep_t<3, 2, 0>(D, w, h, pw);
     }
 }
 
-// all threads: free cells +inf, blocked / border -inf, sources 0 (one pass over the rect rows)
-__device__ __forceinline__ void sssp_init(Shared &sh, const SsspScratch &S, float *dist, int nsrc)
+// group g: free cells +inf, blocked / border -inf, sources 0 (one pass over the rect rows)
+__device__ __forceinline__ void sssp_init(Shared &sh, const SsspScratch &S, float *dist, int nsrc, const Group &g)
 {
-    const int tid = threadIdx.x;
+    const int tid = g.t;
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
     const float NI = -INFINITY;
     int sidx[2];  // flat index of each (snapped, free) source, -1 if none
     for (int s = 0; s < 2; s++)
         sidx[s] = (s < nsrc && sh.src_ok[s]) ? (sh.src_s[s][0] - sh.i0 + 1) * pw + (sh.src_s[s][1] - sh.j0 + 1) : -1;
     // (row, column) walk instead of k / pitch: integer division by a runtime value costs ~40 ops
-    for (int rr = tid >> 7; rr < h + 2; rr += NT >> 7) {
+    for (int rr = tid >> 7; rr < h + 2; rr += g.n >> 7) {
         const B128 fb = (rr >= 1 && rr <= h) ? S.freeb[rr - 1] : B128{0, 0};
         for (int c = tid & 127; c < pw; c += 128) {
             const int k = rr * pw + c;
@@ -589,8 +628,7 @@ __device__ __forceinline__ void sssp_init(Shared &sh, const SsspScratch &S, floa
         }
     }
     if (tid < 3) sh.changed[tid] = 0;
-    if (tid < 8) (&sh.bar[0][0])[tid] = 0u;
-    lds_barrier();
+    g.sync();
 }
 
 // the sweep group (waves 0 .. 4*nsrc-1): rounds of concurrent sweeps until one changes nothing
@@ -619,6 +657,9 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
         const int arr = nsrc == 2 ? 1 - s : s;
 #else
         const int arr = s;
+#endif
+#ifdef SIMAPS_DIAG_ONESRC  // diagnostic (wrong results): only source 0 sweeps
+        if (arr == 1) {} else
 #endif
         if (sh.src_ok[arr] && sweep(dist + arr * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3) && (tid & 63) == 0)
             sh.changed[round % 3] = 1;
@@ -675,9 +716,11 @@ __device__ __forceinline__ void sssp_scale(Shared &sh, float *dist, int nsrc, fl
     }
 }
 
+// all threads (single-kernel users: sssp_grid_kernel, sp_distance_kernel)
 __device__ __forceinline__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
 {
-    sssp_init(sh, S, dist, nsrc);
+    if (threadIdx.x < 8) (&sh.bar[0][0])[threadIdx.x] = 0u;
+    sssp_init(sh, S, dist, nsrc, Group{(int)threadIdx.x, NT, nullptr, NT / 64});
     const int wave = threadIdx.x >> 6;
     if (wave < 4 * nsrc) sssp_rounds(sh, dist, nsrc, Group{(int)threadIdx.x, 256 * nsrc, sh.bar[0], 4 * nsrc});
     lds_barrier();
@@ -800,6 +843,24 @@ __device__ __forceinline__ void raster_lines(Shared &sh, float *tile, const sima
         }
     }
     g.sync();
+}
+
+// The raster tile aliases the cspace scratch: the render group waits until the sweep group has
+// released it (sweep_track; set from the start when no group builds a cspace).  Lane 0 of each wave
+// polls; the acquire fence orders the wave's later tile accesses after the release.
+__device__ __forceinline__ void wait_scratch(Shared &sh)
+{
+    if ((threadIdx.x & 63) == 0) {
+        unsigned spins = 0;
+        while (!__hip_atomic_load(&sh.scratch_free, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 22)) {  // never in a correct run: flag (status bit 4) and fall through
+                __hip_atomic_store(&sh.bar[1][2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                break;
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 __device__ __forceinline__ float tile_sample(const float *tile, int gi, int gj, int pi, int pj)
@@ -928,7 +989,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
                 const int sure = out | ((m_in < 0.5f * hi - SAMPLE_EPS) & (m_fr < 0.5f - SAMPLE_EPS));
                 const int i0 = (int)k0, i1 = (int)k1;
                 const int inmap = ((unsigned)(ci0 + i0) < (unsigned)H) & ((unsigned)(cj0 + i1) < (unsigned)W);
-                const uint32_t vin = (!out & inmap) ? (((uint32_t)i0 << 8) | (uint32_t)i1) : 0xffffu;
+                const uint32_t vin = ((out ^ 1) & inmap) ? (((uint32_t)i0 << 8) | (uint32_t)i1) : 0xffffu;
                 v = sure ? vin : 0xfffeu;  // 0xfffe: exact fp64 below
 #endif
             }
@@ -982,6 +1043,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         STAMP_NB(41);
     }
 #endif
+    wait_scratch(sh);
 #ifndef SIMAPS_ABL_NORASTER
     if (npass > 0) raster_lines(sh, tile, cfg, rb, paths, encs[0], true, g);
 #endif
@@ -1205,6 +1267,64 @@ __device__ __forceinline__ void dump_dist(const Shared &sh, const float *dist, f
     }
 }
 
+// The cspace / SSSP track of get_state_kernel (group g = waves [0, 64 * G)): occupancy window ->
+// cspace (OccupancyMap.update, envs.py:2453-2454) -> snapped sources (envs.py:2514-2517, 2523-2524)
+// -> distance arrays; then the cspace scratch is released to the render group's raster tile and
+// the sweeps run to the fixpoint (GridGraph._spfa, pyx:69-114), finish and scale in place.
+template <int G>
+__device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *dist, const simaps_config &cfg,
+                                            const Geometry &geo, const simaps_agent &ag, const simaps_env &ev,
+                                            const simaps_robot *__restrict__ robots,
+                                            const uint8_t *__restrict__ occupancy, int nsrc, const simaps_debug &dbg,
+                                            int n, const Group &g)
+{
+    const int t = g.t, H = cfg.H, W = cfg.W;
+    const int h = cfg.room_h, w = cfg.room_w;
+    OccLoad<G> occ_regs;  // issued first: they depend on the map slot only
+    cspace_load<G>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, h, w, t);
+    const simaps_robot *rb = robots + ev.robot_off;
+    if (t == 0) {
+        sh.h = h;
+        sh.w = w;
+        sh.i0 = cfg.room_i0;
+        sh.j0 = cfg.room_j0;
+        int ns = 0;
+        sh.sp_slot[0] = sh.sp_slot[1] = -1;
+        if (cfg.use_shortest_path_to_receptacle_map) {
+            pos_to_pix(ev.receptacle_x, ev.receptacle_y, H, W, sh.src_q[ns][0], sh.src_q[ns][1]);
+            sh.sp_slot[0] = ns++;
+        }
+        if (cfg.use_shortest_path_map) {
+            pos_to_pix(rb[ag.robot].x, rb[ag.robot].y, H, W, sh.src_q[ns][0], sh.src_q[ns][1]);
+            sh.sp_slot[1] = ns++;
+        }
+        sh.nsrc = ns;
+    }
+    build_cspace<G>(S, occ_regs, h, w, geo.cspace_r[rb[ag.robot].type], g);  // (its first sync publishes sh)
+    if (t == 0) STAMP_NB(2);
+    if (dbg.cspace) {
+        for (int k = t; k < h * w; k += g.n) dbg.cspace[(size_t)n * h * w + k] = b_test(S.freeb[k / w], k % w) ? 1 : 0;
+    }
+    if (nsrc > 0) {
+        snap_sources(sh, S, nsrc, g);
+        sssp_init(sh, S, dist, nsrc, g);
+    }
+    // every read of the cspace scratch is done (sssp_init ended with a group sync): the render
+    // group may now overwrite it with its raster tile
+    if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __hip_atomic_store(&sh.scratch_free, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        STAMP_NB(3);
+    }
+    if (nsrc == 0) return;
+#ifndef SIMAPS_ABL_NOSWEEP  // diagnostic: render alone (distance channels wrong)
+    sssp_rounds(sh, dist, nsrc, g);
+#endif
+    sssp_finish(sh, dist, nsrc, g);  // while the render waves finish
+    if (dbg.dist) dump_dist(sh, dist, dbg.dist + (size_t)n * 2 * h * w, g);
+    sssp_scale(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);
+}
+
 __global__ void __launch_bounds__(NT) get_state_kernel(
     simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents, const simaps_env *__restrict__ envs,
     const simaps_robot *__restrict__ robots, const double *__restrict__ paths, const uint8_t *__restrict__ occupancy,
@@ -1225,178 +1345,137 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     lds_barrier();
 #endif
     const simaps_agent ag = agents[n];
-    // the occupancy window loads first: they depend on the map slot only
-    const bool need_cspace = cfg.use_shortest_path_to_receptacle_map || cfg.use_shortest_path_map || dbg.cspace;
-    OccLoad occ_regs;
-    if (need_cspace)
-        cspace_load(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
-                    cfg.room_w);
+    // Sources of the shortest-path maps (envs.py:2071-2113 order): receptacle, then the robot.
+    const int nsrc = (cfg.use_shortest_path_to_receptacle_map ? 1 : 0) + (cfg.use_shortest_path_map ? 1 : 0);
+    // Two tracks run concurrently from the start: waves [0, cs_waves) build the cspace, snap the
+    // sources and sweep the distance arrays (4 waves per source); the other waves compute the robot
+    // parameters and stamp tiles and render every channel that does not need distances.
+    const int cs_waves = nsrc > 0 ? 4 * nsrc : (dbg.cspace ? 4 : 0);
+    if (tid < 8) (&sh.bar[0][0])[tid] = 0u;
+    if (tid == 8) sh.scratch_free = cs_waves == 0;
     const simaps_env ev = envs[ag.env];
-    const simaps_robot *rb = robots + ev.robot_off;
-    STAMP(0);
-
-    // ---- parameters (one lane per robot; the agent's own local rotation on another wave)
-    if (tid == 0) {
-        sh.nr = ev.num_robots;
-        sh.me = ag.robot;
-        sh.env = ag.env;
-        sh.has_rec = ev.has_receptacle;
-        sh.h = cfg.room_h;
-        sh.w = cfg.room_w;
-        sh.i0 = cfg.room_i0;
-        sh.j0 = cfg.room_j0;
-        sh.r = geo.cspace_r[rb[ag.robot].type];
-        int ns = 0;
-        sh.sp_slot[0] = sh.sp_slot[1] = -1;
-        if (cfg.use_shortest_path_to_receptacle_map) {
-            pos_to_pix(ev.receptacle_x, ev.receptacle_y, H, W, sh.src_q[ns][0], sh.src_q[ns][1]);
-            sh.sp_slot[0] = ns++;
-        }
-        if (cfg.use_shortest_path_map) {
-            pos_to_pix(rb[ag.robot].x, rb[ag.robot].y, H, W, sh.src_q[ns][0], sh.src_q[ns][1]);
-            sh.sp_slot[1] = ns++;
-        }
-        sh.nsrc = ns;
-    }
-    if (tid == 64) {
-        const simaps_robot &me = rb[ag.robot];
-        sh.rot = rot_params(CROP, 90.0 - me.heading * RAD_TO_DEG);
-        pos_to_pix(me.x, me.y, H, W, sh.pi, sh.pj);
-    }
-    if (tid >= 128 && tid < 128 + ev.num_robots) {
-        const int k = tid - 128;
-        const simaps_robot &r = rb[k];
-        RobotP &P = sh.rob[k];
-        const Rot R = rot_params(LW, r.heading * RAD_TO_DEG - 90.0);
-        P.c = R.c; P.s = R.s; P.f0 = R.f0; P.f1 = R.f1; P.S0 = R.S0; P.S1 = R.S1;
-        int pi, pj;
-        pos_to_pix(r.x, r.y, H, W, pi, pj);
-        P.st_i = pi - R.S0 / 2;
-        P.st_j = pj - R.S1 / 2;
-        P.type = r.type; P.lifting = r.lifting; P.idle = r.idle; P.group = r.group_index;
-        P.x = r.x; P.y = r.y; P.tx = r.target_x; P.ty = r.target_y;
-        pos_to_pix(r.target_x, r.target_y, H, W, P.tpi, P.tpj);
-        {   // conservative prefilter box: inverse-rotate the mask's nonzero window (+-2 px)
-            const int st = geo.mask_start[r.type], wd = geo.mask_width[r.type];
-            const double lo0 = st - (r.type == SIMAPS_LIFTING ? geo.cube_w : 0) - 1.0, hi0 = st + wd + 1.0;
-            const double lo1 = st - 1.0, hi1 = st + wd + 1.0;
-            double mn0 = 1e30, mx0 = -1e30, mn1 = 1e30, mx1 = -1e30;
-            for (int q = 0; q < 4; q++) {
-                const double a = ((q & 1) ? hi0 : lo0) - R.f0, b = ((q & 2) ? hi1 : lo1) - R.f1;
-                const double o0 = R.c * a - R.s * b, o1 = R.s * a + R.c * b;
-                mn0 = fmin(mn0, o0); mx0 = fmax(mx0, o0); mn1 = fmin(mn1, o1); mx1 = fmax(mx1, o1);
-            }
-            P.bi0 = max(P.st_i, P.st_i + (int)floor(mn0) - 2);
-            P.bi1 = min(P.st_i + R.S0 - 1, P.st_i + (int)ceil(mx0) + 2);
-            P.bj0 = max(P.st_j, P.st_j + (int)floor(mn1) - 2);
-            P.bj1 = min(P.st_j + R.S1 - 1, P.st_j + (int)ceil(mx1) + 2);
-            P.bi1 = min(P.bi1, P.bi0 + 31);  // the window is <= 17 x 13 px: its rotated box fits 32 x 32
-            P.bj1 = min(P.bj1, P.bj0 + 31);
-        }
-        P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
-        P.code0 = (1u << r.group_index) | (r.type != SIMAPS_LIFTING ? 1u << 5 : (!r.lifting ? 1u << 4 : 0u));
-    }
-    if (tid >= 512 && tid < 512 + RBLK_PITCH * RBLK_PITCH / 4) sh.rblk[tid - 512] = 0u;
-    // the first history / intention pass's segment table, one lane per robot (raster_lines)
-    if ((cfg.use_history_map || cfg.use_intention_map) && tid >= 320 && tid < 320 + ev.num_robots)
-        seg_table(sh, cfg, rb, paths, cfg.use_history_map ? 4 : cfg.intention_map_encoding, tid - 320, ag.robot);
-    lds_barrier();
-    if (tid == 0) STAMP_NB(9);
-
-    if (cfg.use_intention_channels && tid == 256) intention_channel_order(sh, cfg, rb);
-    // robot sets of the 8 x 8 crop blocks: a stamp box (<= 32 x 32) overlaps <= 5 x 5 blocks
-    if (tid >= 512 && tid < 512 + 25 * ev.num_robots) {
-        const int q = (tid - 512) / 25, d = (tid - 512) % 25;
-        const RobotP &P = sh.rob[q];
-        const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
-        const int a0 = max(P.bi0 - ci0, 0), a1 = min(P.bi1 - ci0, CROP - 1);
-        const int b0 = max(P.bj0 - cj0, 0), b1 = min(P.bj1 - cj0, CROP - 1);
-        const int ba = (a0 >> 3) + d / 5, bb = (b0 >> 3) + d % 5;
-        if (a0 <= a1 && b0 <= b1 && ba <= (a1 >> 3) && bb <= (b1 >> 3)) {
-            const int blk = ba * RBLK_PITCH + bb;
-            atomicOr(&sh.rblk[blk >> 2], (1u << q) << (8 * (blk & 3)));
-        }
-    }
-
-    // ---- rotated robot stamps (Mapper._create_global_robot_map, envs.py:2251-2276): each robot's
-    // scipy-rotated mask, evaluated once per workgroup into a <= 32 x 32 bit tile at its global box.
-    // The 5 host-computed mask windows are staged in the (still unused) union region first.
-    uint32_t *mwin = reinterpret_cast<uint32_t *>(smem + OFF_UNION);  // [5][24] bits + [5][4] ints
-    if (tid < 5 * 24) mwin[tid] = geo.mbits[tid / 24][tid % 24];
-    if (tid >= 128 && tid < 128 + 20) {
-        const int q = tid - 128, m = q >> 2, f = q & 3;
-        mwin[120 + q] = f == 0 ? geo.mrow0[m] : f == 1 ? geo.mcol0[m] : f == 2 ? geo.mnrows[m] : geo.mncols[m];
-    }
-    lds_barrier();
-    // a wave covers tile rows bi, bi + 1 of one robot (64 cells): bits by ballot, no atomics
-    for (int item = tid; item < ev.num_robots * 1024; item += NT) {
-        const int k = item >> 10, cell = item & 1023, bi = cell >> 5, bj = cell & 31;
-        RobotP &P = sh.rob[k];
-        const int gi = P.bi0 + bi, gj = P.bj0 + bj;
-        bool b0 = false, b1 = false;
-        int m0, m1;
-        const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
-        if (gi <= P.bi1 && gj <= P.bj1 && rot_src(R, LW, gi - P.st_i, gj - P.st_j, m0, m1)) {
-            auto bit = [&](int m) {
-                const int *mi = reinterpret_cast<const int *>(mwin + 120 + 4 * m);
-                const int r = m0 - mi[0], c = m1 - mi[1];
-                return r >= 0 && r < mi[2] && c >= 0 && c < mi[3] && ((mwin[m * 24 + r] >> c) & 1u);
-            };
-            b0 = bit(P.type);
-            b1 = P.type == SIMAPS_LIFTING && P.lifting && bit(4);
-        }
-        const uint64_t w0 = __ballot(b0), w1 = __ballot(b1);
-        if ((tid & 63) == 0) {
-            P.sbits[0][bi] = (uint32_t)w0;
-            P.sbits[0][bi + 1] = (uint32_t)(w0 >> 32);
-            P.sbits[1][bi] = (uint32_t)w1;
-            P.sbits[1][bi + 1] = (uint32_t)(w1 >> 32);
-        }
-    }
-    lds_barrier();
-
-    // ---- cspace + snap (all waves)
-    STAMP(1);
-    const int nsrc = sh.nsrc;
-    if (need_cspace) {
-        build_cspace(S, occ_regs, sh.h, sh.w, sh.r);
-        if (dbg.cspace) {
-            for (int k = tid; k < sh.h * sh.w; k += NT)
-                dbg.cspace[(size_t)n * sh.h * sh.w + k] = b_test(S.freeb[k / sh.w], k % sh.w) ? 1 : 0;
-        }
-    }
-    STAMP(2);
-    if (nsrc > 0) {
-        snap_sources(sh, S, nsrc);
-        sssp_init(sh, S, dist, nsrc);
-    }
-    STAMP(3);
-
-    // ---- split: waves [0, 4*nsrc) sweep the distance arrays while the other waves render every
-    // channel that does not need them (overhead, robot, history / intention, intention channels).
-    // The raster tile reuses the cspace scratch, which the sweeps no longer read.
+    lds_barrier();  // the group barriers are zeroed
+    if (tid == 0) STAMP_NB(0);
     float *out = state + (size_t)n * LW * LW * C;
     const RenderCtx rc{cfg, sh, out, C, n};
-    const int sweep_waves = 4 * nsrc;
-    if ((tid >> 6) < sweep_waves) {
-        const Group g{tid, 64 * sweep_waves, sh.bar[0], sweep_waves};
-#ifndef SIMAPS_ABL_NOSWEEP  // diagnostic: render alone (distance channels wrong)
-        sssp_rounds(sh, dist, nsrc, g);
-#endif
-        sssp_finish(sh, dist, nsrc, g);  // while the render waves finish
-        if (dbg.dist) dump_dist(sh, dist, dbg.dist + (size_t)n * 2 * sh.h * sh.w, g);
-        sssp_scale(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);
+    if ((tid >> 6) < cs_waves) {
+        const Group g{tid, 64 * cs_waves, sh.bar[0], cs_waves};
+        if (cs_waves == 8) sweep_track<512>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g);
+        else sweep_track<256>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g);
         STAMP_NB(7);
     } else {
-        const int nw = NT / 64 - sweep_waves;
-        const Group g{tid - 64 * sweep_waves, 64 * nw, sweep_waves ? sh.bar[1] : nullptr, nw};
+        const int nw = NT / 64 - cs_waves;
+        const Group g{tid - 64 * cs_waves, 64 * nw, cs_waves ? sh.bar[1] : nullptr, nw};
+        const int t = g.t;
+        const simaps_robot *rb = robots + ev.robot_off;
+        // ---- parameters (one lane per robot; the agent's own local rotation on another wave)
+        if (t == 0) {
+            sh.nr = ev.num_robots;
+            sh.me = ag.robot;
+            sh.env = ag.env;
+            sh.has_rec = ev.has_receptacle;
+        }
+        if (t == 64) {
+            const simaps_robot &me = rb[ag.robot];
+            sh.rot = rot_params(CROP, 90.0 - me.heading * RAD_TO_DEG);
+            pos_to_pix(me.x, me.y, H, W, sh.pi, sh.pj);
+        }
+        if (t >= 128 && t < 128 + ev.num_robots) {
+            const int k = t - 128;
+            const simaps_robot &r = rb[k];
+            RobotP &P = sh.rob[k];
+            const Rot R = rot_params(LW, r.heading * RAD_TO_DEG - 90.0);
+            P.c = R.c; P.s = R.s; P.f0 = R.f0; P.f1 = R.f1; P.S0 = R.S0; P.S1 = R.S1;
+            int pi, pj;
+            pos_to_pix(r.x, r.y, H, W, pi, pj);
+            P.st_i = pi - R.S0 / 2;
+            P.st_j = pj - R.S1 / 2;
+            P.type = r.type; P.lifting = r.lifting; P.idle = r.idle; P.group = r.group_index;
+            P.x = r.x; P.y = r.y; P.tx = r.target_x; P.ty = r.target_y;
+            pos_to_pix(r.target_x, r.target_y, H, W, P.tpi, P.tpj);
+            {   // conservative prefilter box: inverse-rotate the mask's nonzero window (+-2 px)
+                const int st = geo.mask_start[r.type], wd = geo.mask_width[r.type];
+                const double lo0 = st - (r.type == SIMAPS_LIFTING ? geo.cube_w : 0) - 1.0, hi0 = st + wd + 1.0;
+                const double lo1 = st - 1.0, hi1 = st + wd + 1.0;
+                double mn0 = 1e30, mx0 = -1e30, mn1 = 1e30, mx1 = -1e30;
+                for (int q = 0; q < 4; q++) {
+                    const double a = ((q & 1) ? hi0 : lo0) - R.f0, b = ((q & 2) ? hi1 : lo1) - R.f1;
+                    const double o0 = R.c * a - R.s * b, o1 = R.s * a + R.c * b;
+                    mn0 = fmin(mn0, o0); mx0 = fmax(mx0, o0); mn1 = fmin(mn1, o1); mx1 = fmax(mx1, o1);
+                }
+                P.bi0 = max(P.st_i, P.st_i + (int)floor(mn0) - 2);
+                P.bi1 = min(P.st_i + R.S0 - 1, P.st_i + (int)ceil(mx0) + 2);
+                P.bj0 = max(P.st_j, P.st_j + (int)floor(mn1) - 2);
+                P.bj1 = min(P.st_j + R.S1 - 1, P.st_j + (int)ceil(mx1) + 2);
+                P.bi1 = min(P.bi1, P.bi0 + 31);  // the window is <= 17 x 13 px: its rotated box fits 32 x 32
+                P.bj1 = min(P.bj1, P.bj0 + 31);
+            }
+            P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
+            P.code0 = (1u << r.group_index) | (r.type != SIMAPS_LIFTING ? 1u << 5 : (!r.lifting ? 1u << 4 : 0u));
+        }
+        if (t < RBLK_PITCH * RBLK_PITCH / 4) sh.rblk[t] = 0u;
+        // the first history / intention pass's segment table, one lane per robot (raster_lines)
+        if ((cfg.use_history_map || cfg.use_intention_map) && t >= 320 && t < 320 + ev.num_robots)
+            seg_table(sh, cfg, rb, paths, cfg.use_history_map ? 4 : cfg.intention_map_encoding, t - 320, ag.robot);
+        // the 5 host-computed robot mask windows (stamp tiles below)
+        if (t < 5 * 24) sh.mwin[t] = geo.mbits[t / 24][t % 24];
+        if (t >= 192 && t < 192 + 20) {
+            const int q = t - 192, m = q >> 2, f = q & 3;
+            sh.mwin[120 + q] = f == 0 ? geo.mrow0[m] : f == 1 ? geo.mcol0[m] : f == 2 ? geo.mnrows[m] : geo.mncols[m];
+        }
+        g.sync();
+        if (t == 0) STAMP_NB(9);
+        if (cfg.use_intention_channels && t == 256) intention_channel_order(sh, cfg, rb);
+        // robot sets of the 8 x 8 crop blocks: a stamp box (<= 32 x 32) overlaps <= 5 x 5 blocks
+        if (t < 25 * ev.num_robots) {
+            const int q = t / 25, d = t % 25;
+            const RobotP &P = sh.rob[q];
+            const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
+            const int a0 = max(P.bi0 - ci0, 0), a1 = min(P.bi1 - ci0, CROP - 1);
+            const int b0 = max(P.bj0 - cj0, 0), b1 = min(P.bj1 - cj0, CROP - 1);
+            const int ba = (a0 >> 3) + d / 5, bb = (b0 >> 3) + d % 5;
+            if (a0 <= a1 && b0 <= b1 && ba <= (a1 >> 3) && bb <= (b1 >> 3)) {
+                const int blk = ba * RBLK_PITCH + bb;
+                atomicOr(&sh.rblk[blk >> 2], (1u << q) << (8 * (blk & 3)));
+            }
+        }
+
+        // ---- rotated robot stamps (Mapper._create_global_robot_map, envs.py:2251-2276): each robot's
+        // scipy-rotated mask, evaluated once per workgroup into a <= 32 x 32 bit tile at its global box.
+        // a wave covers tile rows bi, bi + 1 of one robot (64 cells): bits by ballot, no atomics
+        for (int item = t; item < ev.num_robots * 1024; item += g.n) {
+            const int k = item >> 10, cell = item & 1023, bi = cell >> 5, bj = cell & 31;
+            RobotP &P = sh.rob[k];
+            const int gi = P.bi0 + bi, gj = P.bj0 + bj;
+            bool b0 = false, b1 = false;
+            int m0, m1;
+            const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
+            if (gi <= P.bi1 && gj <= P.bj1 && rot_src(R, LW, gi - P.st_i, gj - P.st_j, m0, m1)) {
+                auto bit = [&](int m) {
+                    const int *mi = reinterpret_cast<const int *>(sh.mwin + 120 + 4 * m);
+                    const int r = m0 - mi[0], c = m1 - mi[1];
+                    return r >= 0 && r < mi[2] && c >= 0 && c < mi[3] && ((sh.mwin[m * 24 + r] >> c) & 1u);
+                };
+                b0 = bit(P.type);
+                b1 = P.type == SIMAPS_LIFTING && P.lifting && bit(4);
+            }
+            const uint64_t w0 = __ballot(b0), w1 = __ballot(b1);
+            if ((t & 63) == 0) {
+                P.sbits[0][bi] = (uint32_t)w0;
+                P.sbits[0][bi + 1] = (uint32_t)(w0 >> 32);
+                P.sbits[1][bi] = (uint32_t)w1;
+                P.sbits[1][bi + 1] = (uint32_t)(w1 >> 32);
+            }
+        }
+        g.sync();
+        if (t == 0) STAMP_NB(1);
 #ifndef SIMAPS_ABL_NORENDER  // diagnostic: sweeps alone (output channels 0.. left unwritten)
         const float *ovh = overhead + (size_t)ag.map_slot * H * W;
         if (nw == 8) render_maps<18>(rc, g, geo, ovh, rb, paths, tile);
         else if (nw == 12) render_maps<12>(rc, g, geo, ovh, rb, paths, tile);
         else render_maps<9>(rc, g, geo, ovh, rb, paths, tile);
 #endif
-        if (g.t == 0) STAMP_NB(8);
+        if (t == 0) STAMP_NB(8);
     }
     lds_barrier();
     STAMP(4);
@@ -1491,9 +1570,9 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
     const int n = blockIdx.x, tid = threadIdx.x;
     const int H = cfg.H, W = cfg.W;
     const simaps_agent ag = agents[n];
-    OccLoad occ_regs;
-    cspace_load(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
-                cfg.room_w);
+    OccLoad<NT> occ_regs;
+    cspace_load<NT>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
+                    cfg.room_w, tid);
     if (tid == 0) {
         const simaps_env ev = envs[ag.env];
         sh.h = cfg.room_h;
@@ -1505,8 +1584,8 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
         sh.nsrc = 1;
     }
     lds_barrier();
-    build_cspace(S, occ_regs, sh.h, sh.w, sh.r);
-    snap_sources(sh, S, 1);
+    build_cspace<NT>(S, occ_regs, sh.h, sh.w, sh.r, whole_wg());
+    snap_sources(sh, S, 1, whole_wg());
     const bool src_ok = sh.src_ok[0];
     sssp(sh, S, dist, 1);  // the source's distance image (GridGraph._spfa_with_cache, pyx:116-119)
     const int pw = sssp_pitch(sh.w);
@@ -1517,7 +1596,7 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
             pos_to_pix(t[0], t[1], H, W, sh.src_q[tid][0], sh.src_q[tid][1]);
         }
         lds_barrier();
-        snap_sources(sh, S, nq);
+        snap_sources(sh, S, nq, whole_wg());
         if (tid < nq) {
             float d = -1.0f;  // dists[target] (pyx:156-163); unreachable -> -1 (pyx:110-112)
             if (src_ok && sh.src_ok[tid]) {
@@ -1611,9 +1690,9 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
     const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int H = cfg.H, W = cfg.W;
     const simaps_agent ag = agents[n];
-    OccLoad occ_regs;
-    cspace_load(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
-                cfg.room_w);
+    OccLoad<NT> occ_regs;
+    cspace_load<NT>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
+                    cfg.room_w, tid);
     const double sx = sources[2 * n], sy = sources[2 * n + 1], tx = targets[2 * n], ty = targets[2 * n + 1];
     if (tid == 0) {
         const simaps_env ev = envs[ag.env];
@@ -1627,7 +1706,7 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
         sh.nsrc = 2;
     }
     lds_barrier();
-    build_cspace(S, occ_regs, sh.h, sh.w, sh.r);
+    build_cspace<NT>(S, occ_regs, sh.h, sh.w, sh.r, whole_wg());
     double *o = out_xy + (size_t)n * max_pts * 2;
     // (1) straight line on cspace_thin between the unsnapped pixels (envs.py:2484-2486)
     if (tid < 64) {
@@ -1640,7 +1719,7 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
         return;
     }
     // (2) snap both ends (envs.py:2489-2490)
-    snap_sources(sh, S, 2);
+    snap_sources(sh, S, 2, whole_wg());
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w), cells = (h + 2) * pw;
     // (3) GridGraph._spfa (pyx:69-114) from the snapped source, exactly: one wave, the 8 out-edges of
     // a popped vertex evaluated by lanes 0..7 (distinct heads, so in parallel), then the pushes and
