@@ -64,12 +64,20 @@ __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
         if ((threadIdx.x & 63) == 0 && blockIdx.x < MAX_STAMP_WG)                                \
             g_stamps[blockIdx.x * NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime();              \
     } while (0)
+#define STAMP_CLK(k) /* shader-clock counter (s_memtime): with a realtime stamp, the clock rate */  \
+    do {                                                                                         \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < MAX_STAMP_WG)                                \
+            g_stamps[blockIdx.x * NSTAMP + (k)] = __builtin_amdgcn_s_memtime();                  \
+    } while (0)
 #else
 #define STAMP(k) \
     do {         \
     } while (0)
 #define STAMP_NB(k) \
     do {            \
+    } while (0)
+#define STAMP_CLK(k) \
+    do {             \
     } while (0)
 #endif
 constexpr int MAX_SEG = 128;     // intention / history segments per agent
@@ -565,7 +573,6 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw_rt)
 #define SWEEP_WRITE(P_, V_, R_) lds_min((P_), (V_))
 #endif
     int t = 0;
-#pragma unroll 4
     for (; t + P <= len; t += P) {
         G = gbase(t);
         SWEEP_STEP(A0, A1, 0, true);
@@ -584,6 +591,161 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw_rt)
     return chg != 0;
 }
 
+// The same sweep as one inline-asm loop, for a compile-time pitch.  Measured on gfx950
+// (tools/micro/issue.hip, one wave): every instruction costs the wave ~4.5 (VOP2 / SALU) to ~5.5
+// (VOP3, DPP, v_cmp) cycles of issue, an SALU that consumes a v_cmp's SGPR result stalls ~16 more,
+// ds_min_f32 ~9 alone / ~17 beside other LDS traffic -- dependent VALU latency is hidden.  So the
+// step is minimised in instruction count, not in dependency depth:
+//   - no per-step loop control: full groups of P = 4 steps, the first group and the tail peeled;
+//   - changes are tracked in a VGPR, acc = min3(acc, m0 - R0, m1 - R1) (NaN from inf - inf is
+//     ignored by v_min3), tested once at the end -- no v_cmp -> s_or per cell;
+//   - exact lgkmcnt waits: step j waits only for line j's prefetch (issued P steps earlier);
+//     the compiler's loop-merged bookkeeping drained the last steps' atomics instead.
+// Every LDS operation, wait and register of the loop lives inside the asm, which drains
+// (lgkmcnt(0)) before handing its registers back.  A DPP read of p0 / p1 follows their VALU write
+// by >= 3 VALU instructions.
+// Diagnostic variants (wrong results; per-step cost attribution with the stamp build):
+// SIMAPS_DIAG_SWA_NOMIN (no atomics), SIMAPS_DIAG_SWA_NOREAD (no prefetch reads after the prologue)
+#ifdef SIMAPS_DIAG_SWA_NOMIN
+#define SWA_DSMIN(x) ""
+#else
+#define SWA_DSMIN(x) x
+#endif
+#ifdef SIMAPS_DIAG_SWA_NOREAD
+#define SWA_DSREAD(x) ""
+#define SWA_WAIT(W) ""
+#else
+#define SWA_DSREAD(x) x
+#ifdef SIMAPS_DIAG_SWA_NOMIN
+#define SWA_WAIT(W) "s_waitcnt lgkmcnt(0)\n\t"
+#else
+#define SWA_WAIT(W) "s_waitcnt lgkmcnt(" #W ")\n\t"
+#endif
+#endif
+#define SWA_OFF(J) "((%[k0]+(" #J ")*%[kd])*%[sl4])"
+#define SWA_ROR "wave_ror:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+#define SWA_ROL "wave_rol:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+// CPL 2: m0 = min3(|p0| + 1, prev-lane |p1| + s2, |p1| + s2), m1 = min3(|p1| + 1, |p0| + s2,
+// next-lane |p0| + s2); p' = minimum3(m, R, X)
+#define SWA_STEP2(RA0, RA1, J, W)                                                                  \
+    "v_add_f32_e64 %[a], |%[p0]|, %[one]\n\t"                                                      \
+    "v_add_f32_e64 %[d], |%[p1]|, %[one]\n\t"                                                      \
+    "v_add_f32_e64 %[c], |%[p1]|, %[s2]\n\t"                                                       \
+    "v_add_f32_e64 %[e], |%[p0]|, %[s2]\n\t"                                                       \
+    "v_add_f32_dpp %[b], |%[p1]|, %[s2] " SWA_ROR "\n\t"                                           \
+    "v_add_f32_dpp %[f], |%[p0]|, %[s2] " SWA_ROL "\n\t"                                           \
+    "v_min3_f32 %[a], %[a], %[b], %[c]\n\t"                                                        \
+    "v_min3_f32 %[d], %[d], %[e], %[f]\n\t"                                                        \
+    SWA_DSMIN("ds_min_f32 %[va], %[a] offset:" SWA_OFF(J) "\n\t")                                  \
+    SWA_DSMIN("ds_min_f32 %[va], %[d] offset:(" SWA_OFF(J) "+%[sa4])\n\t")                         \
+    SWA_WAIT(W)                                                                                    \
+    "v_minimum3_f32 %[p0], %[a], %[" #RA0 "], %[X]\n\t"                                            \
+    "v_minimum3_f32 %[p1], %[d], %[" #RA1 "], %[X]\n\t"                                            \
+    "v_sub_f32 %[b], %[a], %[" #RA0 "]\n\t"                                                        \
+    "v_sub_f32 %[e], %[d], %[" #RA1 "]\n\t"                                                        \
+    SWA_DSREAD("ds_read_b32 %[" #RA0 "], %[va] offset:" SWA_OFF(J + 4) "\n\t")                     \
+    SWA_DSREAD("ds_read_b32 %[" #RA1 "], %[va] offset:(" SWA_OFF(J + 4) "+%[sa4])\n\t")            \
+    "v_min3_f32 %[acc], %[acc], %[b], %[e]\n\t"
+// CPL 1: m = min3(|p| + 1, prev-lane |p| + s2, next-lane |p| + s2)
+#define SWA_STEP1(RA0, J, W)                                                                       \
+    "v_add_f32_e64 %[a], |%[p0]|, %[one]\n\t"                                                      \
+    "v_add_f32_dpp %[b], |%[p0]|, %[s2] " SWA_ROR "\n\t"                                           \
+    "v_add_f32_dpp %[c], |%[p0]|, %[s2] " SWA_ROL "\n\t"                                           \
+    "v_min3_f32 %[a], %[a], %[b], %[c]\n\t"                                                        \
+    SWA_DSMIN("ds_min_f32 %[va], %[a] offset:" SWA_OFF(J) "\n\t")                                  \
+    SWA_WAIT(W)                                                                                    \
+    "v_minimum3_f32 %[p0], %[a], %[" #RA0 "], %[X]\n\t"                                            \
+    "v_sub_f32 %[b], %[a], %[" #RA0 "]\n\t"                                                        \
+    SWA_DSREAD("ds_read_b32 %[" #RA0 "], %[va] offset:" SWA_OFF(J + 4) "\n\t")                     \
+    "v_min_f32 %[acc], %[b], %[acc]\n\t"
+#define SWA_IFLEN(J) "s_cmp_le_i32 %[len], " #J "\n\t s_cbranch_scc1 3f\n\t"
+#define SWA_IFREM(J) "s_cmp_le_i32 %[rem], " #J "\n\t s_cbranch_scc1 3f\n\t"
+// lgkmcnt after the 2P prologue / steady-state reads: first group j -> ops issued after line j's read
+#define SWA_BODY(STEP, R0_, R1_, R2_, R3_, W0, W1, W2, W3, WS)                                     \
+    SWA_IFLEN(0) STEP(R0_, 0, W0) SWA_IFLEN(1) STEP(R1_, 1, W1) SWA_IFLEN(2) STEP(R2_, 2, W2)      \
+    SWA_IFLEN(3) STEP(R3_, 3, W3)                                                                  \
+    "v_add_u32_e32 %[va], %[gstep], %[va]\n\t"                                                     \
+    "s_cmp_eq_u32 %[ng], 0\n\t"                                                                    \
+    "s_cbranch_scc1 2f\n"                                                                          \
+    "1:\n\t"                                                                                       \
+    STEP(R0_, 0, WS) STEP(R1_, 1, WS) STEP(R2_, 2, WS) STEP(R3_, 3, WS)                            \
+    "v_add_u32_e32 %[va], %[gstep], %[va]\n\t"                                                     \
+    "s_sub_u32 %[ng], %[ng], 1\n\t"                                                                \
+    "s_cmp_lg_u32 %[ng], 0\n\t"                                                                    \
+    "s_cbranch_scc1 1b\n"                                                                          \
+    "2:\n\t"                                                                                       \
+    SWA_IFREM(0) STEP(R0_, 0, WS) SWA_IFREM(1) STEP(R1_, 1, WS) SWA_IFREM(2) STEP(R2_, 2, WS)      \
+    "3:\n\t"                                                                                       \
+    "s_waitcnt lgkmcnt(0)\n\t"
+#define SWA_S2(RA, J, W) SWA_STEP2(RA##0, RA##1, J, W)
+
+template <int DIR, int CPL, int PWC>
+__device__ bool sweep_asm(lds_float *__restrict__ D, int len, int span)
+{
+    static_assert(PWC > 0, "compile-time pitch");
+    constexpr bool VERT = DIR < 2, FWD = (DIR & 1) == 0;
+    constexpr int P = 4;
+    constexpr int SL = VERT ? PWC : 1, SA = VERT ? 1 : PWC;
+    const int lane = threadIdx.x & 63;
+    const int nact = (span + CPL - 1) / CPL;
+    const bool act = lane < nact;
+    const int own = act ? lane : lane & ((1 << (31 - __clz(nact))) - 1);
+    lds_float *Dl = D + (1 + CPL * own) * SA;
+    // group base at step 0; lines j = 0 .. 2P - 1 of a group at offset (k0 + j kd) * SL * 4 >= 0
+    uint32_t va = (uint32_t)(uintptr_t)(FWD ? Dl + SL : Dl + (len - (2 * P - 1)) * SL);
+    float one = act ? 1.0f : INFINITY, s2 = act ? SQRT2F : INFINITY, X = act ? INFINITY : -INFINITY;
+    float p0 = INFINITY, p1 = INFINITY, acc = 0.0f;
+    float r00, r01, r10, r11, r20, r21, r30, r31, a, b, c, d, e, f;
+    int ng = len > P ? (len - P) / P : 0;   // steady-state groups after the first
+    const int rem = len > P ? (len - P) % P : 0;
+    if constexpr (CPL == 2) {
+        asm volatile(
+            SWA_DSREAD("ds_read_b32 %[r00], %[va] offset:" SWA_OFF(0) "\n\t")
+            SWA_DSREAD("ds_read_b32 %[r01], %[va] offset:(" SWA_OFF(0) "+%[sa4])\n\t")
+            SWA_DSREAD("ds_read_b32 %[r10], %[va] offset:" SWA_OFF(1) "\n\t")
+            SWA_DSREAD("ds_read_b32 %[r11], %[va] offset:(" SWA_OFF(1) "+%[sa4])\n\t")
+            SWA_DSREAD("ds_read_b32 %[r20], %[va] offset:" SWA_OFF(2) "\n\t")
+            SWA_DSREAD("ds_read_b32 %[r21], %[va] offset:(" SWA_OFF(2) "+%[sa4])\n\t")
+            SWA_DSREAD("ds_read_b32 %[r30], %[va] offset:" SWA_OFF(3) "\n\t")
+            SWA_DSREAD("ds_read_b32 %[r31], %[va] offset:(" SWA_OFF(3) "+%[sa4])\n\t")
+            SWA_BODY(SWA_S2, r0, r1, r2, r3, 8, 10, 12, 14, 14)
+            : [p0] "+v"(p0), [p1] "+v"(p1), [acc] "+v"(acc), [va] "+v"(va), [ng] "+s"(ng), [r00] "=&v"(r00),
+              [r01] "=&v"(r01), [r10] "=&v"(r10), [r11] "=&v"(r11), [r20] "=&v"(r20), [r21] "=&v"(r21),
+              [r30] "=&v"(r30), [r31] "=&v"(r31), [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d),
+              [e] "=&v"(e), [f] "=&v"(f)
+            : [one] "v"(one), [s2] "v"(s2), [X] "v"(X), [len] "s"(len), [rem] "s"(rem),
+              [k0] "i"(FWD ? 0 : 2 * P - 1), [kd] "i"(FWD ? 1 : -1), [sl4] "i"(SL * 4), [sa4] "i"(SA * 4),
+              [gstep] "i"((FWD ? P : -P) * SL * 4)
+            : "memory", "scc");
+    } else {
+        asm volatile(
+            SWA_DSREAD("ds_read_b32 %[r00], %[va] offset:" SWA_OFF(0) "\n\t")
+            SWA_DSREAD("ds_read_b32 %[r10], %[va] offset:" SWA_OFF(1) "\n\t")
+            SWA_DSREAD("ds_read_b32 %[r20], %[va] offset:" SWA_OFF(2) "\n\t")
+            SWA_DSREAD("ds_read_b32 %[r30], %[va] offset:" SWA_OFF(3) "\n\t")
+            SWA_BODY(SWA_STEP1, r00, r10, r20, r30, 4, 5, 6, 7, 7)
+            : [p0] "+v"(p0), [acc] "+v"(acc), [va] "+v"(va), [ng] "+s"(ng), [r00] "=&v"(r00), [r10] "=&v"(r10),
+              [r20] "=&v"(r20), [r30] "=&v"(r30), [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c)
+            : [one] "v"(one), [s2] "v"(s2), [X] "v"(X), [len] "s"(len), [rem] "s"(rem),
+              [k0] "i"(FWD ? 0 : 2 * P - 1), [kd] "i"(FWD ? 1 : -1), [sl4] "i"(SL * 4),
+              [gstep] "i"((FWD ? P : -P) * SL * 4)
+            : "memory", "scc");
+    }
+    return __ballot(acc < 0.0f) != 0;
+}
+#undef SWA_S2
+#undef SWA_BODY
+#undef SWA_IFREM
+#undef SWA_IFLEN
+#undef SWA_STEP1
+#undef SWA_STEP2
+#undef SWA_ROL
+#undef SWA_ROR
+#undef SWA_OFF
+#undef SWA_WAIT
+#undef SWA_DSREAD
+#undef SWA_DSMIN
+
 __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_in)
 {
     lds_float *D = (lds_float *)Dg;  // the distance arrays live in LDS: keep ds_* addressing
@@ -594,12 +756,21 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
     pw = __builtin_amdgcn_readfirstlane(pw);
     // every BASELINE room is 92 columns wide (pitch 95): its sweeps get immediate-offset addressing
     if (pw == 95) {
+#ifdef SIMAPS_SWEEP_C  // the C loop with compile-time pitch (reference for the asm loop)
         switch (dir) {
         case 0: return sweep_t<0, 2, 95>(D, h, w, pw);
         case 1: return sweep_t<1, 2, 95>(D, h, w, pw);
         case 2: return h <= 63 ? sweep_t<2, 1, 95>(D, w, h, pw) : sweep_t<2, 2, 95>(D, w, h, pw);
         default: return h <= 63 ? sweep_t<3, 1, 95>(D, w, h, pw) : sweep_t<3, 2, 95>(D, w, h, pw);
         }
+#else
+        switch (dir) {
+        case 0: return sweep_asm<0, 2, 95>(D, h, w);
+        case 1: return sweep_asm<1, 2, 95>(D, h, w);
+        case 2: return h <= 63 ? sweep_asm<2, 1, 95>(D, w, h) : sweep_asm<2, 2, 95>(D, w, h);
+        default: return h <= 63 ? sweep_asm<3, 1, 95>(D, w, h) : sweep_asm<3, 2, 95>(D, w, h);
+        }
+#endif
     }
     switch (dir) {
     case 0: return w <= 63 ? sweep_t<0, 1, 0>(D, h, w, pw) : sweep_t<0, 2, 0>(D, h, w, pw);
@@ -650,6 +821,7 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
 #ifdef SIMAPS_PHASE_STAMPS
         if (tid == 0 && round < 4) STAMP_NB(18 + round);
         if (round == 0) STAMP_NB(32 + wave);
+        if (round == 0 && wave == 0) STAMP_CLK(44);
 #endif
         // waves go to SIMD (wave % 4): source 1's directions are rotated by 2 so that every SIMD
         // hosts one row sweep and one column sweep (the long ones would otherwise share two SIMDs)
@@ -667,6 +839,7 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
         if (round == 0 && wave == 0) STAMP_NB(22);
         if (round == 0 && wave == 2) STAMP_NB(23);
         if (round == 0) STAMP_NB(24 + wave);
+        if (round == 0 && wave == 0) STAMP_CLK(45);
 #endif
         g.sync();
         if (!sh.changed[round % 3] || round >= max_rounds) {
