@@ -294,18 +294,26 @@ template <int G>
 __device__ __forceinline__ void cspace_load(OccLoad<G> &L, const uint8_t *__restrict__ occ, int H, int W, int i0, int j0,
                                             int h, int w, int t)
 {
+    // Unconditional buffer loads: a cell outside the map or the window gets offset 0xffffffff, which
+    // the buffer's range check turns into 0 -- no exec-masked branch per load, so all of them are in
+    // flight at once (bounds-checked pointer loads compiled to one branch + vmcnt(0) round trip each).
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)occ, (short)0, H * W, 0x00020000);
     const int lane = t & 63, wave = t >> 6;
     const int wh = h + 2 * RMAX, ww = w + 2 * RMAX;  // <= 126 x 134
     const int c = t & 127, r0 = t >> 7;
 #pragma unroll
     for (int q = 0; q < OccLoad<G>::NQ; q++) {
         const int rr = r0 + (G / 128) * q, gi = i0 - RMAX + rr, gj = j0 - RMAX + c;
-        L.v[q] = (rr < wh && c < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
+        const bool in = ((unsigned)rr < (unsigned)wh) & ((unsigned)c < (unsigned)ww) & ((unsigned)gi < (unsigned)H) &
+                        ((unsigned)gj < (unsigned)W);
+        L.v[q] = __builtin_amdgcn_raw_buffer_load_b8(rs, in ? gi * W + gj : -1, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < OccLoad<G>::NU; u++) {
         const int rr = 8 * wave + (lane >> 3) + (G / 8) * u, cc = 128 + (lane & 7), gi = i0 - RMAX + rr, gj = j0 - RMAX + cc;
-        L.v2[u] = (rr < wh && cc < ww && gi >= 0 && gi < H && gj >= 0 && gj < W) ? occ[(size_t)gi * W + gj] : 0;
+        const bool in = ((unsigned)rr < (unsigned)wh) & ((unsigned)cc < (unsigned)ww) & ((unsigned)gi < (unsigned)H) &
+                        ((unsigned)gj < (unsigned)W);
+        L.v2[u] = __builtin_amdgcn_raw_buffer_load_b8(rs, in ? gi * W + gj : -1, 0, 0);
     }
 }
 
@@ -333,13 +341,19 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
 #pragma unroll
         for (int q = 0; q < OccLoad<G>::NQ; q++) {
             const int rr = r0 + (G / 128) * q;
-            const uint64_t m = __ballot(rr < whM && c < wwM && L.v[q] != 0);
+            const uint64_t m = __ballot(L.v[q] != 0);  // 0 outside the window (cspace_load)
             if (lane == 0 && rr < whM) S.win[rr][wave & 1] = m;
+#ifdef SIMAPS_PHASE_STAMPS
+            if (q == 0 && t == 0) STAMP_NB(46);
+#endif
         }
+#ifdef SIMAPS_PHASE_STAMPS
+        if (t == 0) STAMP_NB(47);
+#endif
 #pragma unroll
         for (int u = 0; u < OccLoad<G>::NU; u++) {
             const int rb = 8 * wave + (G / 8) * u, rr = rb + (lane >> 3), cc = 128 + (lane & 7);
-            const uint64_t m = __ballot(rr < whM && cc < wwM && L.v2[u] != 0);
+            const uint64_t m = __ballot(L.v2[u] != 0);
             if (lane < 8 && rb + lane < whM) S.win[rb + lane][2] = (m >> (8 * lane)) & 0xffu;
         }
     }
@@ -1454,6 +1468,9 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
     const int t = g.t, H = cfg.H, W = cfg.W;
     const int h = cfg.room_h, w = cfg.room_w;
     OccLoad<G> occ_regs;  // issued first: they depend on the map slot only
+#ifdef SIMAPS_PHASE_STAMPS
+    if (t == 0 && ag.map_slot >= 0) STAMP_NB(43);  // the agent record has landed
+#endif
     cspace_load<G>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, h, w, t);
     const simaps_robot *rb = robots + ev.robot_off;
     if (t == 0) {
