@@ -50,7 +50,7 @@ namespace {
 constexpr int NT = 1024;
 #ifdef SIMAPS_PHASE_STAMPS
 // Diagnostic build only (libsimaps_prof.so): per-workgroup s_memrealtime (100 MHz) stamps.
-constexpr int MAX_STAMP_WG = 8192, NSTAMP = 48;
+constexpr int MAX_STAMP_WG = 8192, NSTAMP = 64;
 __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
 // (a barrier first, so a stamp marks the moment the SLOWEST wave finished the previous phase)
 #define STAMP(k)                                                                                 \
@@ -281,6 +281,9 @@ __device__ __forceinline__ float wave_max(float v)
 // occ: the agent's occupancy map [H, W] (nonzero = obstacle).  r = disk radius (<= RMAX).
 // The window loads are issued first thing by the group that builds the cspace (cspace_load, for the
 // largest radius, so they need no robot descriptor) and land in registers.
+// distance-array pitch: (w + 2) | 1 floats (odd: column-wise sweeps hit at most 2-way bank conflicts)
+__device__ __forceinline__ int sssp_pitch(int w) { return (w + 2) | 1; }
+
 constexpr int RMAX = 7;  // floor(RADIUS * 96) <= 6 for every robot class (envs.py:2421)
 // G threads cover the window: words 0-1 of a row (columns 0..127): thread -> (row t / 128 + (G / 128) q,
 // column t % 128), so every wave holds 64 consecutive columns of one row (one ballot per row word);
@@ -331,8 +334,12 @@ __device__ __forceinline__ unsigned row16_or(unsigned x)
 // inside the room rect (envs.py:2453).  No LDS staging, no atomics: window words come straight from
 // the loaded registers by ballots; each 16-lane DPP row computes one output row, lane = disk row dy.
 // Group g (g.n == G threads) -- the whole workgroup, or the sweep group while the render group works.
+// With dist (the get_state sweep track), the 16 lanes that compute a row's free bits also write
+// that row of every distance array (free +inf, blocked / border -inf; sssp_init_sources then sets
+// the snapped sources to 0): no separate init pass over the arrays.
 template <int G>
-__device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L, int h, int w, int r, const Group &g)
+__device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L, int h, int w, int r, const Group &g,
+                                             float *dist = nullptr, int nsrc = 0)
 {
     const int t = g.t, lane = t & 63, wave = t >> 6;
     const int whM = h + 2 * RMAX, wwM = w + 2 * RMAX;
@@ -364,6 +371,14 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
     int hw = -1;  // disk(r) half-width of row dy (skimage disk: dx^2 + dy^2 <= r^2)
     if (dy <= r)
         while ((hw + 1) * (hw + 1) + dy * dy <= r * r) hw++;
+    const int pw = sssp_pitch(w);
+    if (dist) {  // border rows 0 and h + 1
+        for (int k = t; k < pw; k += G)
+            for (int s = 0; s < nsrc; s++) {
+                dist[s * DIST_FLOATS + k] = -INFINITY;
+                dist[s * DIST_FLOATS + (h + 1) * pw + k] = -INFINITY;
+            }
+    }
     for (int base = 0; base < h; base += G / 16) {  // uniform: every lane takes part in the DPP ORs
         const int row = base + (t >> 4);
         B128 acc = {0, 0};
@@ -373,9 +388,14 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
         }
         const unsigned a0 = row16_or((unsigned)acc.lo), a1 = row16_or((unsigned)(acc.lo >> 32));
         const unsigned a2 = row16_or((unsigned)acc.hi), a3 = row16_or((unsigned)(acc.hi >> 32));
-        if ((t & 15) == 0 && row < h) {
-            const uint64_t lo = ((uint64_t)a1 << 32) | a0, hi = ((uint64_t)a3 << 32) | a2;
-            S.freeb[row] = {~lo & fm.lo, ~hi & fm.hi};
+        const uint64_t lo = ((uint64_t)a1 << 32) | a0, hi = ((uint64_t)a3 << 32) | a2;
+        const B128 fr = {~lo & fm.lo, ~hi & fm.hi};
+        if ((t & 15) == 0 && row < h) S.freeb[row] = fr;
+        if (dist && row < h) {
+            for (int c = t & 15; c < pw; c += 16) {
+                const float v = (c >= 1 && c <= w && b_test(fr, c - 1)) ? INFINITY : -INFINITY;
+                for (int s = 0; s < nsrc; s++) dist[s * DIST_FLOATS + (row + 1) * pw + c] = v;
+            }
         }
     }
     g.sync();
@@ -502,7 +522,6 @@ __device__ __forceinline__ float from_next_lane(float v)  // lane i <- lane i+1
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x134, 0xf, 0xf, true));  // wave_rol:1
 }
 
-__device__ __forceinline__ int sssp_pitch(int w) { return (w + 2) | 1; }
 
 constexpr unsigned NINF_BITS = 0xff800000u;  // blocked / border cells
 
@@ -816,6 +835,16 @@ __device__ __forceinline__ void sssp_init(Shared &sh, const SsspScratch &S, floa
     g.sync();
 }
 
+// group g, after build_cspace(dist) and snap_sources: the snapped (free) sources start at 0
+__device__ __forceinline__ void sssp_init_sources(Shared &sh, float *dist, int nsrc, const Group &g)
+{
+    const int t = g.t, pw = sssp_pitch(sh.w);
+    if (t < nsrc && sh.src_ok[t])
+        dist[t * DIST_FLOATS + (sh.src_s[t][0] - sh.i0 + 1) * pw + (sh.src_s[t][1] - sh.j0 + 1)] = 0.0f;
+    if (t < 3) sh.changed[t] = 0;
+    g.sync();
+}
+
 // the sweep group (waves 0 .. 4*nsrc-1): rounds of concurrent sweeps until one changes nothing
 __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, const Group &g)
 {
@@ -900,6 +929,35 @@ __device__ __forceinline__ void sssp_scale(Shared &sh, float *dist, int nsrc, fl
             d = d != INFINITY ? (d / 96.0f) * scale : un;
         }
         if (g.t == 0) sh.unreach[s] = un;
+    }
+}
+
+// group g, after the rounds: finite distances -> global shortest-path map values in one pass
+// (envs.py:2288-2300: img = sp / 96, img[img < 0] = img.max(), img *= scale); blocked / unreachable
+// cells keep +-inf, which the distance phase reads as sh.unreach[s] = (max(sp) / 96) * scale
+// (division and scaling are monotone, so the max of the scaled values is the scaled max).
+__device__ __forceinline__ void sssp_finish_scale(Shared &sh, float *dist, int nsrc, float scale, const Group &g)
+{
+    const int cells = (sh.h + 2) * sssp_pitch(sh.w);
+    for (int s = 0; s < nsrc; s++) {
+        float m = -1.0f;
+        for (int q = g.t; q < cells; q += g.n) {
+            float &d = dist[s * DIST_FLOATS + q];
+            const float v = d;
+            if (fabsf(v) != INFINITY) {
+                m = fmaxf(m, v);
+                d = (v / 96.0f) * scale;
+            }
+        }
+        m = wave_max(m);
+        if ((g.t & 63) == 0) sh.red[s][g.t >> 6] = m;
+    }
+    g.sync();
+    if (g.t < nsrc) {
+        float mm = sh.red[g.t][0];
+        for (int k = 1; k < g.nw; k++) mm = fmaxf(mm, sh.red[g.t][k]);
+        sh.dmax[g.t] = mm;
+        sh.unreach[g.t] = (mm / 96.0f) * scale;
     }
 }
 
@@ -1282,7 +1340,11 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         uint32_t v = gq_v(k);
         asm volatile("" : "+v"(v));
         const int a = (int)(v >> 8), b = (int)(v & 0xffu);
+#ifdef SIMAPS_ABL_NOROBOT  // diagnostic: no robot stamps in the overhead / robot channels
+        unsigned rs = 0;
+#else
         unsigned rs = rblk[(a >> 3) * RBLK_PITCH + (b >> 3)];
+#endif
         unsigned m = 0;
         while (rs) {
             const int q = __builtin_ctz(rs);
@@ -1352,9 +1414,10 @@ static_assert(PPT * NT == LW * LW, "pixel split");
 
 // Distance channels (all 16 waves): Euclidean map, then shortest-path maps; local -= local.min()
 // (envs.py:2213-2216), so every value is kept in registers until the block minimum is known.
-// The sweep group has already turned dist[] into channel values (sssp_scale), border cells
-// included: cell 0 of each array holds the "unreachable" value, which is also the value of every
-// global pixel outside the room rect, so an out-of-rect pixel just reads cell 0.  Everything the
+// The sweep group has already turned the finite dist[] values into channel values
+// (sssp_finish_scale); blocked, unreachable and border cells still hold +-inf and read as the
+// "unreachable" value, which is also the value of every global pixel outside the room rect, so an
+// out-of-rect pixel just reads cell 0 (a border corner).  Everything the
 // per-pixel loop needs from `sh` is read once into registers: the loop is straight-line code.
 __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, const simaps_env &ev, const float *dist, int nsrc,
                                          const uint16_t *tab)
@@ -1405,10 +1468,11 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
     for (int s = 0; s < 2; s++) {  // envs.py:2288-2300, 2514-2517 (scaled in place by sssp_scale)
         if (s >= nsrc) continue;
         const lds_float *D = (const lds_float *)(dist + s * DIST_FLOATS);
+        const float un = sh.unreach[s];  // blocked / unreachable / outside the rect (cell 0)
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
             const float v = D[max(cell[k], 0)];
-            vals[1 + s][k] = cell[k] < 0 ? 0.0f : v;
+            vals[1 + s][k] = cell[k] < 0 ? 0.0f : (fabsf(v) == INFINITY ? un : v);
             mins[1 + s] = fminf(mins[1 + s], vals[1 + s][k]);
         }
     }
@@ -1490,16 +1554,17 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
         }
         sh.nsrc = ns;
     }
-    build_cspace<G>(S, occ_regs, h, w, geo.cspace_r[rb[ag.robot].type], g);  // (its first sync publishes sh)
+    build_cspace<G>(S, occ_regs, h, w, geo.cspace_r[rb[ag.robot].type], g, dist, nsrc);  // (its first sync publishes sh)
     if (t == 0) STAMP_NB(2);
     if (dbg.cspace) {
         for (int k = t; k < h * w; k += g.n) dbg.cspace[(size_t)n * h * w + k] = b_test(S.freeb[k / w], k % w) ? 1 : 0;
     }
     if (nsrc > 0) {
         snap_sources(sh, S, nsrc, g);
-        sssp_init(sh, S, dist, nsrc, g);
+        if (t == 0) STAMP_NB(48);
+        sssp_init_sources(sh, dist, nsrc, g);
     }
-    // every read of the cspace scratch is done (sssp_init ended with a group sync): the render
+    // every read of the cspace scratch is done (snap_sources ended with a group sync): the render
     // group may now overwrite it with its raster tile
     if (t == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1510,9 +1575,15 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
 #ifndef SIMAPS_ABL_NOSWEEP  // diagnostic: render alone (distance channels wrong)
     sssp_rounds(sh, dist, nsrc, g);
 #endif
-    sssp_finish(sh, dist, nsrc, g);  // while the render waves finish
-    if (dbg.dist) dump_dist(sh, dist, dbg.dist + (size_t)n * 2 * h * w, g);
-    sssp_scale(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);
+    if (t == 0) STAMP_NB(49);
+    if (dbg.dist) {  // debug: the raw distances first
+        sssp_finish(sh, dist, nsrc, g);
+        dump_dist(sh, dist, dbg.dist + (size_t)n * 2 * h * w, g);
+        sssp_scale(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);
+    } else {
+        sssp_finish_scale(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);  // while the render waves finish
+    }
+    if (t == 0) STAMP_NB(50);
 }
 
 __global__ void __launch_bounds__(NT) get_state_kernel(
@@ -1630,6 +1701,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             }
         }
 
+        if (t == 0) STAMP_NB(51);
         // ---- rotated robot stamps (Mapper._create_global_robot_map, envs.py:2251-2276): each robot's
         // scipy-rotated mask, evaluated once per workgroup into a <= 32 x 32 bit tile at its global box.
         // a wave covers tile rows bi, bi + 1 of one robot (64 cells): bits by ballot, no atomics

@@ -34,7 +34,7 @@ def main():
     for _ in range(3):
         b.render(out)
     torch.cuda.synchronize()
-    st = np.zeros((8192, 48), dtype=np.uint64)
+    st = np.zeros((8192, 64), dtype=np.uint64)
     b.render(out)
     torch.cuda.synchronize()
     assert L.simaps_debug_read_stamps(st.ctypes.data) == 0
@@ -42,8 +42,8 @@ def main():
     us = lambda k1, k0: float(np.median((st[:, k1] - st[:, k0]) / 100.0))  # noqa: E731
     res = {'config': args.config, 'layout': args.layout, 'N': b.N,
            'total_us_median': us(6, 0), 'span_us': float((st[:, 6].max() - st[:, 0].min()) / 100.0),
-           'sweep_track_us': {'agent_load': us(43, 0), 'first_ballot': us(46, 43), 'all_ballots': us(47, 46), 'v2_ballots_sync': us(15, 47), 'cspace_loads_ballots': us(15, 0), 'cspace_dilate': us(2, 15), 'cspace': us(2, 0), 'snap_init': us(3, 2), 'rounds_finish_scale': us(7, 3), 'end': us(7, 0)},
-           'render_track_us': {'params': us(9, 0), 'stamps': us(1, 9), 'sampleidx_fast': us(40, 1), 'sampleidx_fp64': us(41, 40),
+           'sweep_track_us': {'agent_load': us(43, 0), 'first_ballot': us(46, 43), 'all_ballots': us(47, 46), 'v2_ballots_sync': us(15, 47), 'cspace_loads_ballots': us(15, 0), 'cspace_dilate': us(2, 15), 'cspace': us(2, 0), 'snap': us(48, 2), 'init': us(3, 48), 'rounds': us(49, 3), 'finish': us(50, 49), 'scale': us(7, 50), 'rounds_finish_scale': us(7, 3), 'end': us(7, 0)},
+           'render_track_us': {'params': us(9, 0), 'blocksets': us(51, 9), 'stamp_tiles': us(1, 51), 'sampleidx_fast': us(40, 1), 'sampleidx_fp64': us(41, 40),
                                'raster1': us(42, 41), 'gather_issue': us(14, 42), 'intention_sample': us(13, 14),
                                'overhead_robot': us(11, 13), 'rest': us(8, 11), 'end': us(8, 0)},
            'join_us': us(4, 0),
