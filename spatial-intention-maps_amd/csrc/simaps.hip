@@ -82,7 +82,6 @@ __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
 #endif
 constexpr int MAX_SEG = 128;     // intention / history segments per agent
 constexpr int RBLK = (CROP + 7) / 8;  // 8 x 8 blocks per crop side (robot sets, render_maps)
-constexpr int RBLK_PITCH = 32;        // row pitch of the block table: 0xff >> 3 = 31 is a row / column no robot touches
 constexpr int SEG_PER_ROBOT = SIMAPS_MAX_PATH - 1;
 constexpr int MAX_ROWS = 112;    // room rect rows (bit-row arrays)
 constexpr int WIN_WORDS = 3;     // occupancy window row: up to 192 bits
@@ -194,7 +193,6 @@ struct RobotP {
     int tpi, tpj;            // target end-effector pixel
     unsigned code0;          // robot-code bits of a class-mask pixel (robot_bits)
     float seg_val;
-    uint32_t sbits[2][32];   // rotated stamp inside the box: [0] class mask, [1] lifted-cube mask
 };
 
 struct Seg {
@@ -224,7 +222,6 @@ struct Shared {
     int colbest[2][SIMAPS_MAX_ROOM_W];
     int envg[2][SIMAPS_MAX_ROOM_W];  // Voronoi envelope (rect columns) per source
     unsigned bar[2][4];              // group barriers {count, generation, timeout, -}: [0] sweeps, [1] render
-    uint32_t rblk[RBLK_PITCH * RBLK_PITCH / 4];  // per 8 x 8 crop block: bit q = robot q's stamp box overlaps it
     int changed[3];                  // rotating per-round "some sweep improved a cell" flags
     int scratch_free;                // the cspace scratch may be reused as the raster tile
     uint32_t mwin[5 * 24 + 20];      // robot mask windows: [5][24] bit rows + [5][4] ints (stamp tiles)
@@ -244,6 +241,12 @@ constexpr int OFF_UNION = OFF_DIST + align16(2 * DIST_FLOATS * 4);
 constexpr int TILE_BYTES = TILE * TILE * 4;
 constexpr int UNION_BYTES = align16((int)sizeof(SsspScratch) > TILE_BYTES ? (int)sizeof(SsspScratch) : TILE_BYTES);
 constexpr int LDS_BYTES = OFF_UNION + UNION_BYTES;
+// The crop's robot-code map (u8 per crop pixel + a zero guard for outside pixels), built by the
+// stamps phase and read by the overhead / robot channels before the first raster pass: it shares the
+// union with the sweep track's scratch (disjoint offsets) and with the raster tile (later in time).
+constexpr int OFF_CMAP = OFF_UNION + align16((int)sizeof(SsspScratch));
+constexpr int CMAP_BYTES = align16(CROP * CROP + 16);
+static_assert(OFF_CMAP + CMAP_BYTES <= OFF_UNION + UNION_BYTES, "code map fits the union");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(offsetof(RobotP, bi0) % 16 == 0 && sizeof(RobotP) % 16 == 0, "RobotP box loads as one b128");
 
@@ -1177,20 +1180,6 @@ __device__ __forceinline__ void intention_channel_order(Shared &sh, const simaps
 // equal the fp64 ones.  The few pixels inside that band (~0.2%) take the exact fp64 rot_src.
 constexpr float SAMPLE_EPS = 4e-4f;
 
-// robot r's stamp bit tiles -> the overhead seg bits / robot-map code of global pixel (gi, gj)
-// (Mapper._create_global_robot_map, envs.py:2251-2276): bit g = seg value (g + 5) / 8
-// (SEG_VALUES robot_group_{g+1}), bit 4 = 0.5, bit 5 = 1.0; the max over robots is the highest bit
-__device__ __forceinline__ unsigned robot_bits(const RobotP &P, int gi, int gj)
-{
-    const int a = gi - P.bi0, b = gj - P.bj0;
-    unsigned bits = 0;
-    if ((unsigned)a <= (unsigned)(P.bi1 - P.bi0) && (unsigned)b <= (unsigned)(P.bj1 - P.bj0)) {
-        if ((P.sbits[0][a] >> b) & 1u) bits |= P.code0;
-        if ((P.sbits[1][a] >> b) & 1u) bits |= 1u << 5;  // lifted-cube mask, value 1.0
-    }
-    return bits;
-}
-
 // NPT: output pixels per render thread (18 / 12 / 9 for 8 / 12 / 16 render waves), a compile-time
 // constant so every pixel loop is exact (no bounds tests) and its index math folds.
 template <int NPT>
@@ -1288,13 +1277,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         STAMP_NB(41);
     }
 #endif
-    wait_scratch(sh);
-#ifndef SIMAPS_ABL_NORASTER
-    if (npass > 0) raster_lines(sh, tile, cfg, rb, paths, encs[0], true, g);
-#endif
-    if (g.t == 0) STAMP_NB(42);
-    // every overhead gather of the thread in flight at once, issued after the first raster (whose
-    // integer divisions and fp64 need the registers); the intention samples and stores run meanwhile
+    // every overhead gather of the thread in flight at once; the robot-code lookups run meanwhile
     float ovv[MAXPG];
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
@@ -1308,49 +1291,31 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         ovv[k] = *reinterpret_cast<const float *>(reinterpret_cast<const char *>(ovh) + (unsigned)(v != 0xffffu ? idx : 0) * 4u);
 #endif
     }
-#ifdef SIMAPS_PHASE_STAMPS
-    if (g.t == 0) {
-        asm volatile("" ::"v"(gqp[0]), "v"(gqp[8]));
-        STAMP_NB(14);
-    }
-#endif
-    // sample one rasterised pass into channel c (then the tile may be reused)
-    auto sample_pass = [&](int c) {
-        if (g.t == 0) STAMP_NB(12);
+    if (g.t == 0) STAMP_NB(42);
+    // overhead / robot channels (Mapper._create_global_overhead_map / _create_global_robot_map,
+    // envs.py:2244-2276) from the crop's robot-code map (stamps phase): one LDS byte per pixel.
+    // Bit g of the code = seg value (g + 5) / 8 (SEG_VALUES robot_group_{g+1}), bit 4 = 0.5,
+    // bit 5 = 1.0 (lifted-cube mask); the max over robots is the highest bit.  Outside pixels
+    // (0xffff) read the zero guard after the map.
+    const uint8_t *cmap = reinterpret_cast<const uint8_t *>(tile) + (OFF_CMAP - OFF_UNION);
+    unsigned codes[(MAXPG + 3) / 4] = {};
 #pragma unroll
-        for (int k = 0; k < MAXPG; k++) {
-            const int p = g.t + k * GN;
-            uint32_t v = gq_v(k);
-            asm volatile("" : "+v"(v));
-            rc.put(c, p, v != 0xffffu ? tile_sample(tile, ci0 + (int)(v >> 8), cj0 + (int)(v & 0xffu), sh.pi, sh.pj) : 0.0f);
-        }
-        g.sync();
-    };
-    if (npass > 0) sample_pass(ch);
-    if (g.t == 0) STAMP_NB(13);
-    // overhead / robot channels: per pixel, the 8 x 8 crop block's robot set (sh.rblk, built in the
-    // stamps phase) selects the few robots whose stamp box can contain it
-    const uint8_t *rblk = reinterpret_cast<const uint8_t *>(sh.rblk);
+    for (int k = 0; k < MAXPG; k++) {
+        const uint32_t v = gq_v(k);
+#ifdef SIMAPS_ABL_NOROBOT  // diagnostic: no robot stamps in the overhead / robot channels
+        const unsigned m = 0;
+#else
+        const unsigned m = cmap[v != 0xffffu ? (int)(v >> 8) * CROP + (int)(v & 0xffu) : CROP * CROP];
+#endif
+        codes[k >> 2] |= m << (8 * (k & 3));
+    }
+    if (g.t == 0) STAMP_NB(14);
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
         const int p = g.t + k * GN;
-        // an outside pixel (0xffff) reads block (31, 31), which no robot touches.  (The asm keeps the
-        // per-pixel index math and validity test here instead of hoisted above the gathers, where 18
-        // pixels' worth of it would not fit the register budget.)
         uint32_t v = gq_v(k);
         asm volatile("" : "+v"(v));
-        const int a = (int)(v >> 8), b = (int)(v & 0xffu);
-#ifdef SIMAPS_ABL_NOROBOT  // diagnostic: no robot stamps in the overhead / robot channels
-        unsigned rs = 0;
-#else
-        unsigned rs = rblk[(a >> 3) * RBLK_PITCH + (b >> 3)];
-#endif
-        unsigned m = 0;
-        while (rs) {
-            const int q = __builtin_ctz(rs);
-            rs &= rs - 1;
-            m |= robot_bits(sh.rob[q], ci0 + a, cj0 + b);
-        }
+        const unsigned m = (codes[k >> 2] >> (8 * (k & 3))) & 0xffu;
         const unsigned ms = m & 0xfu, mr = m >> 4;
         const float vseg = ms ? (float)(31 - __builtin_clz(ms) + 5) * 0.125f : 0.0f;
         const float vrob = (mr & 2u) ? 1.0f : ((mr & 1u) ? 0.5f : 0.0f);
@@ -1363,8 +1328,30 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
 #endif
     }
     if (g.t == 0) STAMP_NB(11);
-    // the second history / intention pass (history + intention configs), after the overhead values
-    // are consumed: its raster needs the registers the gathers held
+    // sample one rasterised pass into channel c (then the tile may be reused)
+    auto sample_pass = [&](int c) {
+        if (g.t == 0) STAMP_NB(12);
+#pragma unroll
+        for (int k = 0; k < MAXPG; k++) {
+            const int p = g.t + k * GN;
+            uint32_t v = gq_v(k);
+            asm volatile("" : "+v"(v));
+            rc.put(c, p, v != 0xffffu ? tile_sample(tile, ci0 + (int)(v >> 8), cj0 + (int)(v & 0xffu), sh.pi, sh.pj) : 0.0f);
+        }
+        g.sync();
+    };
+    // history / intention passes, rasterised into the LDS tile, which overwrites the code map (every
+    // render wave has read it: group barrier) and the sweep track's scratch (wait for its release)
+    if (npass > 0) {
+        g.sync();
+        wait_scratch(sh);
+#ifndef SIMAPS_ABL_NORASTER
+        raster_lines(sh, tile, cfg, rb, paths, encs[0], true, g);
+#endif
+        if (g.t == 0) STAMP_NB(13);
+        sample_pass(ch);
+    }
+    // the second history / intention pass (history + intention configs)
     if (npass > 1) {
 #ifndef SIMAPS_ABL_NORASTER
         raster_lines(sh, tile, cfg, rb, paths, encs[1], false, g);
@@ -1401,7 +1388,12 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         }
     }
     // hand the sample indices to the distance phase: crop-relative (row << 8 | col), 0xffff = cval
-    // (the tile region is free: every raster pass ended with a group barrier)
+    // (the tile region is free: every raster pass ended with a group barrier; without one, wait for
+    // every render wave's code-map reads and for the sweep track's scratch release)
+    if (npass == 0) {
+        g.sync();
+        wait_scratch(sh);
+    }
     uint16_t *tab = reinterpret_cast<uint16_t *>(tile);
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
@@ -1674,7 +1666,10 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
             P.code0 = (1u << r.group_index) | (r.type != SIMAPS_LIFTING ? 1u << 5 : (!r.lifting ? 1u << 4 : 0u));
         }
-        if (t < RBLK_PITCH * RBLK_PITCH / 4) sh.rblk[t] = 0u;
+        {   // the crop's robot-code map starts empty
+            uint4 *cz = reinterpret_cast<uint4 *>(smem + OFF_CMAP);
+            for (int k = t; k < CMAP_BYTES / 16; k += g.n) cz[k] = uint4{0u, 0u, 0u, 0u};
+        }
         // the first history / intention pass's segment table, one lane per robot (raster_lines)
         if ((cfg.use_history_map || cfg.use_intention_map) && t >= 320 && t < 320 + ev.num_robots)
             seg_table(sh, cfg, rb, paths, cfg.use_history_map ? 4 : cfg.intention_map_encoding, t - 320, ag.robot);
@@ -1687,24 +1682,14 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         g.sync();
         if (t == 0) STAMP_NB(9);
         if (cfg.use_intention_channels && t == 256) intention_channel_order(sh, cfg, rb);
-        // robot sets of the 8 x 8 crop blocks: a stamp box (<= 32 x 32) overlaps <= 5 x 5 blocks
-        if (t < 25 * ev.num_robots) {
-            const int q = t / 25, d = t % 25;
-            const RobotP &P = sh.rob[q];
-            const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
-            const int a0 = max(P.bi0 - ci0, 0), a1 = min(P.bi1 - ci0, CROP - 1);
-            const int b0 = max(P.bj0 - cj0, 0), b1 = min(P.bj1 - cj0, CROP - 1);
-            const int ba = (a0 >> 3) + d / 5, bb = (b0 >> 3) + d % 5;
-            if (a0 <= a1 && b0 <= b1 && ba <= (a1 >> 3) && bb <= (b1 >> 3)) {
-                const int blk = ba * RBLK_PITCH + bb;
-                atomicOr(&sh.rblk[blk >> 2], (1u << q) << (8 * (blk & 3)));
-            }
-        }
 
         if (t == 0) STAMP_NB(51);
         // ---- rotated robot stamps (Mapper._create_global_robot_map, envs.py:2251-2276): each robot's
-        // scipy-rotated mask, evaluated once per workgroup into a <= 32 x 32 bit tile at its global box.
-        // a wave covers tile rows bi, bi + 1 of one robot (64 cells): bits by ballot, no atomics
+        // scipy-rotated mask, evaluated once per workgroup over its <= 32 x 32 global box; the set
+        // pixels inside the crop OR their code into the crop's robot-code map (bit g = seg value
+        // (g + 5) / 8 of SEG_VALUES robot_group_{g+1}, bit 4 = 0.5, bit 5 = 1.0 lifted-cube mask)
+        uint32_t *cmap32 = reinterpret_cast<uint32_t *>(smem + OFF_CMAP);
+        const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
         for (int item = t; item < ev.num_robots * 1024; item += g.n) {
             const int k = item >> 10, cell = item & 1023, bi = cell >> 5, bj = cell & 31;
             RobotP &P = sh.rob[k];
@@ -1721,12 +1706,11 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
                 b0 = bit(P.type);
                 b1 = P.type == SIMAPS_LIFTING && P.lifting && bit(4);
             }
-            const uint64_t w0 = __ballot(b0), w1 = __ballot(b1);
-            if ((t & 63) == 0) {
-                P.sbits[0][bi] = (uint32_t)w0;
-                P.sbits[0][bi + 1] = (uint32_t)(w0 >> 32);
-                P.sbits[1][bi] = (uint32_t)w1;
-                P.sbits[1][bi + 1] = (uint32_t)(w1 >> 32);
+            const unsigned code = (b0 ? P.code0 : 0u) | (b1 ? 1u << 5 : 0u);
+            const int ca = gi - ci0, cb = gj - cj0;
+            if (code && (unsigned)ca < (unsigned)CROP && (unsigned)cb < (unsigned)CROP) {
+                const int pos = ca * CROP + cb;
+                atomicOr(&cmap32[pos >> 2], code << (8 * (pos & 3)));
             }
         }
         g.sync();

@@ -44,8 +44,8 @@ def main():
            'total_us_median': us(6, 0), 'span_us': float((st[:, 6].max() - st[:, 0].min()) / 100.0),
            'sweep_track_us': {'agent_load': us(43, 0), 'first_ballot': us(46, 43), 'all_ballots': us(47, 46), 'v2_ballots_sync': us(15, 47), 'cspace_loads_ballots': us(15, 0), 'cspace_dilate': us(2, 15), 'cspace': us(2, 0), 'snap': us(48, 2), 'init': us(3, 48), 'rounds': us(49, 3), 'finish': us(50, 49), 'scale': us(7, 50), 'rounds_finish_scale': us(7, 3), 'end': us(7, 0)},
            'render_track_us': {'params': us(9, 0), 'blocksets': us(51, 9), 'stamp_tiles': us(1, 51), 'sampleidx_fast': us(40, 1), 'sampleidx_fp64': us(41, 40),
-                               'raster1': us(42, 41), 'gather_issue': us(14, 42), 'intention_sample': us(13, 14),
-                               'overhead_robot': us(11, 13), 'rest': us(8, 11), 'end': us(8, 0)},
+                               'gather_issue': us(42, 41), 'code_lookup': us(14, 42), 'overhead_robot': us(11, 14),
+                               'raster1': us(13, 11), 'sample_rest': us(8, 13), 'end': us(8, 0)},
            'join_us': us(4, 0),
            'distance_us': {'values': us(16, 5), 'block_min': us(17, 16), 'stores': us(6, 17), 'all': us(6, 5)},
            'sweep_rounds_us': {'round_%d' % r: us(19 + r, 18 + r) for r in range(3)},
