@@ -1690,27 +1690,56 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         // (g + 5) / 8 of SEG_VALUES robot_group_{g+1}, bit 4 = 0.5, bit 5 = 1.0 lifted-cube mask)
         uint32_t *cmap32 = reinterpret_cast<uint32_t *>(smem + OFF_CMAP);
         const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
-        for (int item = t; item < ev.num_robots * 1024; item += g.n) {
-            const int k = item >> 10, cell = item & 1023, bi = cell >> 5, bj = cell & 31;
-            RobotP &P = sh.rob[k];
-            const int gi = P.bi0 + bi, gj = P.bj0 + bj;
-            bool b0 = false, b1 = false;
-            int m0, m1;
+        // Waves own robots (nw / nr waves per robot, interleaved over its box rows); per wave-item 2
+        // box rows (lane -> row 2 rp + lane / 32, column lane % 32).  The robot's parameters and mask
+        // window bounds are loaded once per wave.  Source positions in fp32 where they are surely away
+        // from the rounding / bounds boundaries, else exactly in fp64 (rot_src).
+        const int ln = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+        const int nrb = ev.num_robots, wpr = nrb <= nw ? nw / nrb : 1;
+        for (int kk = wv; kk < nrb * wpr; kk += nw) {
+            const int k = kk % nrb, sub = kk / nrb;
+            const RobotP &P = sh.rob[k];
+            const int bi0 = __builtin_amdgcn_readfirstlane(P.bi0), bi1 = __builtin_amdgcn_readfirstlane(P.bi1);
+            const int bj0 = P.bj0, bj1 = P.bj1, st_i = P.st_i, st_j = P.st_j;
+            const int type = P.type;
+            const bool cube = type == SIMAPS_LIFTING && P.lifting;
+            const unsigned code0 = P.code0;
             const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
-            if (gi <= P.bi1 && gj <= P.bj1 && rot_src(R, LW, gi - P.st_i, gj - P.st_j, m0, m1)) {
-                auto bit = [&](int m) {
-                    const int *mi = reinterpret_cast<const int *>(sh.mwin + 120 + 4 * m);
-                    const int r = m0 - mi[0], c = m1 - mi[1];
-                    return r >= 0 && r < mi[2] && c >= 0 && c < mi[3] && ((sh.mwin[m * 24 + r] >> c) & 1u);
-                };
-                b0 = bit(P.type);
-                b1 = P.type == SIMAPS_LIFTING && P.lifting && bit(4);
-            }
-            const unsigned code = (b0 ? P.code0 : 0u) | (b1 ? 1u << 5 : 0u);
-            const int ca = gi - ci0, cb = gj - cj0;
-            if (code && (unsigned)ca < (unsigned)CROP && (unsigned)cb < (unsigned)CROP) {
-                const int pos = ca * CROP + cb;
-                atomicOr(&cmap32[pos >> 2], code << (8 * (pos & 3)));
+            const float c = (float)R.c, sn = (float)R.s, f0 = (float)R.f0, f1 = (float)R.f1;
+            const int *mt = reinterpret_cast<const int *>(sh.mwin + 120 + 4 * type);
+            const int *mc = reinterpret_cast<const int *>(sh.mwin + 120 + 4 * 4);
+            const int mt0 = mt[0], mt1 = mt[1], mt2 = mt[2], mt3 = mt[3];
+            const int mc0 = mc[0], mc1 = mc[1], mc2 = mc[2], mc3 = mc[3];
+            for (int rp = sub; 2 * rp <= bi1 - bi0; rp += wpr) {
+                const int gi = bi0 + 2 * rp + (ln >> 5), gj = bj0 + (ln & 31);
+                unsigned code = 0;
+                if (gi <= bi1 && gj <= bj1) {
+                    const int o0 = gi - st_i, o1 = gj - st_j;
+                    const float hi = LW - 1;
+                    const float s0 = ((float)o0 * c + (float)o1 * sn) + f0, s1 = ((float)o0 * (-sn) + (float)o1 * c) + f1;
+                    const float u0 = s0 + 0.5f, u1 = s1 + 0.5f;
+                    const float k0 = floorf(u0), k1 = floorf(u1);
+                    const float m_in = fmaxf(fabsf(s0 - 0.5f * hi), fabsf(s1 - 0.5f * hi));
+                    const float m_fr = fmaxf(fabsf(u0 - k0 - 0.5f), fabsf(u1 - k1 - 0.5f));
+                    const bool out = m_in > 0.5f * hi + SAMPLE_EPS;
+                    const bool sure = out || (m_in < 0.5f * hi - SAMPLE_EPS && m_fr < 0.5f - SAMPLE_EPS);
+                    int m0 = (int)k0, m1 = (int)k1;
+                    bool in = !out;
+                    if (!sure) in = rot_src(R, LW, o0, o1, m0, m1);
+                    if (in) {
+                        const int r = m0 - mt0, cc = m1 - mt1;
+                        if ((unsigned)r < (unsigned)mt2 && (unsigned)cc < (unsigned)mt3 && ((sh.mwin[type * 24 + r] >> cc) & 1u))
+                            code = code0;
+                        const int r2 = m0 - mc0, c2 = m1 - mc1;
+                        if (cube && (unsigned)r2 < (unsigned)mc2 && (unsigned)c2 < (unsigned)mc3 && ((sh.mwin[4 * 24 + r2] >> c2) & 1u))
+                            code |= 1u << 5;
+                    }
+                }
+                const int ca = gi - ci0, cb = gj - cj0;
+                if (code && (unsigned)ca < (unsigned)CROP && (unsigned)cb < (unsigned)CROP) {
+                    const int pos = ca * CROP + cb;
+                    atomicOr(&cmap32[pos >> 2], code << (8 * (pos & 3)));
+                }
             }
         }
         g.sync();
