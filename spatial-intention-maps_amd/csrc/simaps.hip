@@ -223,6 +223,7 @@ struct Shared {
     int envg[2][SIMAPS_MAX_ROOM_W];  // Voronoi envelope (rect columns) per source
     unsigned bar[2][4];              // group barriers {count, generation, timeout, -}: [0] sweeps, [1] render
     int changed[3];                  // rotating per-round "some sweep improved a cell" flags
+    uint64_t dirty[2][4][2];         // per source and sweep direction: lines (bit L - 1) to relax again
     int scratch_free;                // the cspace scratch may be reused as the raster tile
     uint32_t mwin[5 * 24 + 20];      // robot mask windows: [5][24] bit rows + [5][4] ints (stamp tiles)
     Seg seg[MAX_SEG];
@@ -681,7 +682,7 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw_rt)
     "v_sub_f32 %[e], %[d], %[" #RA1 "]\n\t"                                                        \
     SWA_DSREAD("ds_read_b32 %[" #RA0 "], %[va] offset:" SWA_OFF(J + 4) "\n\t")                     \
     SWA_DSREAD("ds_read_b32 %[" #RA1 "], %[va] offset:(" SWA_OFF(J + 4) "+%[sa4])\n\t")            \
-    "v_min3_f32 %[acc], %[acc], %[b], %[e]\n\t"
+    "v_min3_f32 %[accg], %[accg], %[b], %[e]\n\t"
 // CPL 1: m = min3(|p| + 1, prev-lane |p| + s2, next-lane |p| + s2)
 #define SWA_STEP1(RA0, J, W)                                                                       \
     "v_add_f32_e64 %[a], |%[p0]|, %[one]\n\t"                                                      \
@@ -693,30 +694,65 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw_rt)
     "v_minimum3_f32 %[p0], %[a], %[" #RA0 "], %[X]\n\t"                                            \
     "v_sub_f32 %[b], %[a], %[" #RA0 "]\n\t"                                                        \
     SWA_DSREAD("ds_read_b32 %[" #RA0 "], %[va] offset:" SWA_OFF(J + 4) "\n\t")                     \
-    "v_min_f32 %[acc], %[b], %[acc]\n\t"
+    "v_min_f32 %[accg], %[b], %[accg]\n\t"
 #define SWA_IFLEN(J) "s_cmp_le_i32 %[len], " #J "\n\t s_cbranch_scc1 3f\n\t"
 #define SWA_IFREM(J) "s_cmp_le_i32 %[rem], " #J "\n\t s_cbranch_scc1 3f\n\t"
+// After each full group: fold the group's change accumulator; a group that improved a cell records
+// its step range [tg, tg + 3]; one that did not ends the sweep once it lies past the last dirty
+// line (tg + 3 > tmax): every later line is clean, so the rest of the sweep would change nothing.
+#define SWA_GROUP_END                                                                              \
+    "v_cmp_gt_f32_e64 %[cm], 0, %[accg]\n\t"                                                       \
+    "v_min_f32_e32 %[acc], %[accg], %[acc]\n\t"                                                    \
+    "v_mov_b32_e32 %[accg], 0\n\t"                                                                 \
+    "s_cmp_lg_u64 %[cm], 0\n\t"                                                                    \
+    "s_cbranch_scc0 7f\n\t"                                                                        \
+    "s_min_i32 %[imin], %[imin], %[tg]\n\t"                                                        \
+    "s_add_i32 %[imax], %[tg], 3\n\t"                                                              \
+    "s_branch 8f\n"                                                                                \
+    "7:\n\t"                                                                                       \
+    "s_cmp_gt_i32 %[tg], %[txm3]\n\t"                                                              \
+    "s_cbranch_scc1 3f\n"                                                                          \
+    "8:\n\t"                                                                                       \
+    "s_add_i32 %[tg], %[tg], 4\n\t"
 // lgkmcnt after the 2P prologue / steady-state reads: first group j -> ops issued after line j's read
 #define SWA_BODY(STEP, R0_, R1_, R2_, R3_, W0, W1, W2, W3, WS)                                     \
     SWA_IFLEN(0) STEP(R0_, 0, W0) SWA_IFLEN(1) STEP(R1_, 1, W1) SWA_IFLEN(2) STEP(R2_, 2, W2)      \
     SWA_IFLEN(3) STEP(R3_, 3, W3)                                                                  \
     "v_add_u32_e32 %[va], %[gstep], %[va]\n\t"                                                     \
+    SWA_GROUP_END                                                                                  \
     "s_cmp_eq_u32 %[ng], 0\n\t"                                                                    \
     "s_cbranch_scc1 2f\n"                                                                          \
     "1:\n\t"                                                                                       \
     STEP(R0_, 0, WS) STEP(R1_, 1, WS) STEP(R2_, 2, WS) STEP(R3_, 3, WS)                            \
     "v_add_u32_e32 %[va], %[gstep], %[va]\n\t"                                                     \
+    SWA_GROUP_END                                                                                  \
     "s_sub_u32 %[ng], %[ng], 1\n\t"                                                                \
     "s_cmp_lg_u32 %[ng], 0\n\t"                                                                    \
     "s_cbranch_scc1 1b\n"                                                                          \
     "2:\n\t"                                                                                       \
     SWA_IFREM(0) STEP(R0_, 0, WS) SWA_IFREM(1) STEP(R1_, 1, WS) SWA_IFREM(2) STEP(R2_, 2, WS)      \
     "3:\n\t"                                                                                       \
+    "v_cmp_gt_f32_e64 %[cm], 0, %[accg]\n\t"                                                       \
+    "v_min_f32_e32 %[acc], %[accg], %[acc]\n\t"                                                    \
+    "s_cmp_lg_u64 %[cm], 0\n\t"                                                                    \
+    "s_cbranch_scc0 9f\n\t"                                                                        \
+    "s_min_i32 %[imin], %[imin], %[tg]\n\t"                                                        \
+    "s_add_i32 %[imax], %[tg], 3\n"                                                                \
+    "9:\n\t"                                                                                       \
     "s_waitcnt lgkmcnt(0)\n\t"
 #define SWA_S2(RA, J, W) SWA_STEP2(RA##0, RA##1, J, W)
 
+// Result of one directional sweep: lanes that improved a cell anywhere (their lines, for the
+// perpendicular directions) and the step range of the groups that improved one (for the opposite
+// direction); imin > imax when nothing improved.
+struct SweepOut {
+    uint64_t lanes;
+    int imin, imax;
+};
+
+// Sweep steps t0 .. (early exit past tmax) of a line space of len lines.
 template <int DIR, int CPL, int PWC>
-__device__ bool sweep_asm(lds_float *__restrict__ D, int len, int span)
+__device__ SweepOut sweep_asm(lds_float *__restrict__ D, int len, int span, int t0, int tmax)
 {
     static_assert(PWC > 0, "compile-time pitch");
     constexpr bool VERT = DIR < 2, FWD = (DIR & 1) == 0;
@@ -727,13 +763,17 @@ __device__ bool sweep_asm(lds_float *__restrict__ D, int len, int span)
     const bool act = lane < nact;
     const int own = act ? lane : lane & ((1 << (31 - __clz(nact))) - 1);
     lds_float *Dl = D + (1 + CPL * own) * SA;
-    // group base at step 0; lines j = 0 .. 2P - 1 of a group at offset (k0 + j kd) * SL * 4 >= 0
-    uint32_t va = (uint32_t)(uintptr_t)(FWD ? Dl + SL : Dl + (len - (2 * P - 1)) * SL);
+    // group base at step t0; lines j = 0 .. 2P - 1 of a group at offset (k0 + j kd) * SL * 4 >= 0
+    uint32_t va = (uint32_t)(uintptr_t)(FWD ? Dl + (1 + t0) * SL : Dl + (len - t0 - (2 * P - 1)) * SL);
     float one = act ? 1.0f : INFINITY, s2 = act ? SQRT2F : INFINITY, X = act ? INFINITY : -INFINITY;
-    float p0 = INFINITY, p1 = INFINITY, acc = 0.0f;
+    float p0 = INFINITY, p1 = INFINITY, acc = 0.0f, accg = 0.0f;
     float r00, r01, r10, r11, r20, r21, r30, r31, a, b, c, d, e, f;
-    int ng = len > P ? (len - P) / P : 0;   // steady-state groups after the first
-    const int rem = len > P ? (len - P) % P : 0;
+    const int lenr = len - t0;                 // steps from t0 to the end
+    int ng = lenr > P ? (lenr - P) / P : 0;    // steady-state groups after the first
+    const int rem = lenr > P ? (lenr - P) % P : 0;
+    const int txm3 = tmax - t0 - 3;
+    int tg = 0, imin = 1 << 30, imax = -1;
+    uint64_t cm;
     if constexpr (CPL == 2) {
         asm volatile(
             SWA_DSREAD("ds_read_b32 %[r00], %[va] offset:" SWA_OFF(0) "\n\t")
@@ -745,11 +785,12 @@ __device__ bool sweep_asm(lds_float *__restrict__ D, int len, int span)
             SWA_DSREAD("ds_read_b32 %[r30], %[va] offset:" SWA_OFF(3) "\n\t")
             SWA_DSREAD("ds_read_b32 %[r31], %[va] offset:(" SWA_OFF(3) "+%[sa4])\n\t")
             SWA_BODY(SWA_S2, r0, r1, r2, r3, 8, 10, 12, 14, 14)
-            : [p0] "+v"(p0), [p1] "+v"(p1), [acc] "+v"(acc), [va] "+v"(va), [ng] "+s"(ng), [r00] "=&v"(r00),
+            : [p0] "+v"(p0), [p1] "+v"(p1), [acc] "+v"(acc), [accg] "+v"(accg), [va] "+v"(va), [ng] "+s"(ng),
+              [tg] "+s"(tg), [imin] "+s"(imin), [imax] "+s"(imax), [cm] "=&s"(cm), [r00] "=&v"(r00),
               [r01] "=&v"(r01), [r10] "=&v"(r10), [r11] "=&v"(r11), [r20] "=&v"(r20), [r21] "=&v"(r21),
               [r30] "=&v"(r30), [r31] "=&v"(r31), [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d),
               [e] "=&v"(e), [f] "=&v"(f)
-            : [one] "v"(one), [s2] "v"(s2), [X] "v"(X), [len] "s"(len), [rem] "s"(rem),
+            : [one] "v"(one), [s2] "v"(s2), [X] "v"(X), [len] "s"(lenr), [rem] "s"(rem), [txm3] "s"(txm3),
               [k0] "i"(FWD ? 0 : 2 * P - 1), [kd] "i"(FWD ? 1 : -1), [sl4] "i"(SL * 4), [sa4] "i"(SA * 4),
               [gstep] "i"((FWD ? P : -P) * SL * 4)
             : "memory", "scc");
@@ -760,17 +801,19 @@ __device__ bool sweep_asm(lds_float *__restrict__ D, int len, int span)
             SWA_DSREAD("ds_read_b32 %[r20], %[va] offset:" SWA_OFF(2) "\n\t")
             SWA_DSREAD("ds_read_b32 %[r30], %[va] offset:" SWA_OFF(3) "\n\t")
             SWA_BODY(SWA_STEP1, r00, r10, r20, r30, 4, 5, 6, 7, 7)
-            : [p0] "+v"(p0), [acc] "+v"(acc), [va] "+v"(va), [ng] "+s"(ng), [r00] "=&v"(r00), [r10] "=&v"(r10),
+            : [p0] "+v"(p0), [acc] "+v"(acc), [accg] "+v"(accg), [va] "+v"(va), [ng] "+s"(ng), [tg] "+s"(tg),
+              [imin] "+s"(imin), [imax] "+s"(imax), [cm] "=&s"(cm), [r00] "=&v"(r00), [r10] "=&v"(r10),
               [r20] "=&v"(r20), [r30] "=&v"(r30), [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c)
-            : [one] "v"(one), [s2] "v"(s2), [X] "v"(X), [len] "s"(len), [rem] "s"(rem),
+            : [one] "v"(one), [s2] "v"(s2), [X] "v"(X), [len] "s"(lenr), [rem] "s"(rem), [txm3] "s"(txm3),
               [k0] "i"(FWD ? 0 : 2 * P - 1), [kd] "i"(FWD ? 1 : -1), [sl4] "i"(SL * 4),
               [gstep] "i"((FWD ? P : -P) * SL * 4)
             : "memory", "scc");
     }
-    return __ballot(acc < 0.0f) != 0;
+    return SweepOut{__ballot(acc < 0.0f), t0 + imin, min(t0 + imax, len - 1)};
 }
 #undef SWA_S2
 #undef SWA_BODY
+#undef SWA_GROUP_END
 #undef SWA_IFREM
 #undef SWA_IFLEN
 #undef SWA_STEP1
@@ -782,7 +825,42 @@ __device__ bool sweep_asm(lds_float *__restrict__ D, int len, int span)
 #undef SWA_DSREAD
 #undef SWA_DSMIN
 
-__device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_in)
+// ---- dirty lines -------------------------------------------------------------------------------
+// Each source keeps, per sweep direction, a 128-bit mask of the lines (bit L - 1 = line L) whose
+// values changed since that direction last relaxed out of them.  Invariant: the current values of a
+// clean line were relaxed (in that direction) into the next line.  A sweep snapshot-clears its mask,
+// starts at its first dirty line and ends at the first group past its last dirty line that improves
+// nothing; then it marks what it lowered: the lines of its improving steps for the opposite direction
+// and the lines of its improving lanes for the two perpendicular ones (conservative supersets).
+// Marks follow the sweep's own writes (its asm drains them) and a snapshot precedes the sweep's
+// reads, so a decrease is either seen by a sweep or left marked for the next round.  A round in which
+// nothing improves adds no marks and leaves every mask empty: the fixpoint.
+__device__ __forceinline__ uint64_t spread2(uint32_t x)  // bit i -> bits 2i and 2i + 1
+{
+    uint64_t v = x;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    v = (v | (v << 1)) & 0x5555555555555555ull;
+    return v | (v << 1);
+}
+__device__ __forceinline__ uint64_t bits64(int a, int b)  // bits a .. b of a word, a <= b within [0, 63]
+{
+    return (b >= 63 ? ~0ull : ((1ull << (b + 1)) - 1)) & (~0ull << a);
+}
+__device__ __forceinline__ void mark_lines(uint64_t *m, uint64_t lo, uint64_t hi)
+{
+    if (lo) __hip_atomic_fetch_or(&m[0], lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (hi) __hip_atomic_fetch_or(&m[1], hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void mark_range(uint64_t *m, int a, int b)  // bits a .. b, 0 <= a <= b <= 127
+{
+    mark_lines(m, a <= 63 ? bits64(a, min(b, 63)) : 0ull, b >= 64 ? bits64(max(a, 64) - 64, b - 64) : 0ull);
+}
+
+// One sweep of direction dir_in over source dm's array; true if it improved a cell.
+__device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_in, uint64_t (*dm)[2])
 {
     lds_float *D = (lds_float *)Dg;  // the distance arrays live in LDS: keep ds_* addressing
     // wave-uniform loop bounds: scalar loop control, no exec-mask merges at the back edge
@@ -790,30 +868,59 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
     h = __builtin_amdgcn_readfirstlane(h);
     w = __builtin_amdgcn_readfirstlane(w);
     pw = __builtin_amdgcn_readfirstlane(pw);
-    // every BASELINE room is 92 columns wide (pitch 95): its sweeps get immediate-offset addressing
-    if (pw == 95) {
-#ifdef SIMAPS_SWEEP_C  // the C loop with compile-time pitch (reference for the asm loop)
-        switch (dir) {
-        case 0: return sweep_t<0, 2, 95>(D, h, w, pw);
-        case 1: return sweep_t<1, 2, 95>(D, h, w, pw);
-        case 2: return h <= 63 ? sweep_t<2, 1, 95>(D, w, h, pw) : sweep_t<2, 2, 95>(D, w, h, pw);
-        default: return h <= 63 ? sweep_t<3, 1, 95>(D, w, h, pw) : sweep_t<3, 2, 95>(D, w, h, pw);
-        }
-#else
-        switch (dir) {
-        case 0: return sweep_asm<0, 2, 95>(D, h, w);
-        case 1: return sweep_asm<1, 2, 95>(D, h, w);
-        case 2: return h <= 63 ? sweep_asm<2, 1, 95>(D, w, h) : sweep_asm<2, 2, 95>(D, w, h);
-        default: return h <= 63 ? sweep_asm<3, 1, 95>(D, w, h) : sweep_asm<3, 2, 95>(D, w, h);
-        }
+    const bool vert = dir < 2, fwd = (dir & 1) == 0;
+    const int len = vert ? h : w, span = vert ? w : h;
+    const int lane = threadIdx.x & 63;
+    uint64_t mlo = 0, mhi = 0;
+    if (lane == 0) {  // snapshot-and-clear this direction's dirty lines (before any read of the array)
+        mlo = __hip_atomic_exchange(&dm[dir][0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        mhi = __hip_atomic_exchange(&dm[dir][1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    mlo = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(mlo >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)mlo);
+    mhi = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(mhi >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)mhi);
+    if (!(mlo | mhi)) return false;
+    const int blo = mlo ? __builtin_ctzll(mlo) : 64 + __builtin_ctzll(mhi);
+    const int bhi = mhi ? 127 - __builtin_clzll(mhi) : 63 - __builtin_clzll(mlo);
+    const int t0 = fwd ? blo : len - 1 - bhi, tmax = fwd ? bhi : len - 1 - blo;  // step t: line fwd ? t + 1 : len - t
+    if (pw == 95
+#ifdef SIMAPS_SWEEP_C
+        && false
 #endif
+    ) {  // every BASELINE room is 92 columns wide (pitch 95): the asm loop with immediate offsets
+        SweepOut o;
+        switch (dir) {
+        case 0: o = sweep_asm<0, 2, 95>(D, h, w, t0, tmax); break;
+        case 1: o = sweep_asm<1, 2, 95>(D, h, w, t0, tmax); break;
+        case 2: o = h <= 63 ? sweep_asm<2, 1, 95>(D, w, h, t0, tmax) : sweep_asm<2, 2, 95>(D, w, h, t0, tmax); break;
+        default: o = h <= 63 ? sweep_asm<3, 1, 95>(D, w, h, t0, tmax) : sweep_asm<3, 2, 95>(D, w, h, t0, tmax); break;
+        }
+        if (!o.lanes) return false;
+        if (lane == 0) {
+            const int a = fwd ? o.imin : len - 1 - o.imax, b = fwd ? o.imax : len - 1 - o.imin;
+            mark_range(dm[dir ^ 1], max(a, 0), min(b, 127));
+            const int cpl = span <= 63 ? 1 : 2;
+            const uint64_t lo = cpl == 1 ? o.lanes : spread2((uint32_t)o.lanes);
+            const uint64_t hi = cpl == 1 ? 0ull : spread2((uint32_t)(o.lanes >> 32));
+            const int p = vert ? 2 : 0;
+            mark_lines(dm[p], lo, hi);
+            mark_lines(dm[p + 1], lo, hi);
+        }
+        return true;
     }
+    // runtime pitch: a full sweep; if it improved anything, every line of the others is marked
+    bool chg;
     switch (dir) {
-    case 0: return w <= 63 ? sweep_t<0, 1, 0>(D, h, w, pw) : sweep_t<0, 2, 0>(D, h, w, pw);
-    case 1: return w <= 63 ? sweep_t<1, 1, 0>(D, h, w, pw) : sweep_t<1, 2, 0>(D, h, w, pw);
-    case 2: return h <= 63 ? sweep_t<2, 1, 0>(D, w, h, pw) : sweep_t<2, 2, 0>(D, w, h, pw);
-    default: return h <= 63 ? sweep_t<3, 1, 0>(D, w, h, pw) : sweep_t<3, 2, 0>(D, w, h, pw);
+    case 0: chg = w <= 63 ? sweep_t<0, 1, 0>(D, h, w, pw) : sweep_t<0, 2, 0>(D, h, w, pw); break;
+    case 1: chg = w <= 63 ? sweep_t<1, 1, 0>(D, h, w, pw) : sweep_t<1, 2, 0>(D, h, w, pw); break;
+    case 2: chg = h <= 63 ? sweep_t<2, 1, 0>(D, w, h, pw) : sweep_t<2, 2, 0>(D, w, h, pw); break;
+    default: chg = h <= 63 ? sweep_t<3, 1, 0>(D, w, h, pw) : sweep_t<3, 2, 0>(D, w, h, pw); break;
     }
+    if (chg && lane == 0)
+        for (int d2 = 0; d2 < 4; d2++)
+            if (d2 != dir) mark_range(dm[d2], 0, (d2 < 2 ? h : w) - 1);
+    return chg;
 }
 
 // group g: free cells +inf, blocked / border -inf, sources 0 (one pass over the rect rows)
@@ -835,6 +942,11 @@ __device__ __forceinline__ void sssp_init(Shared &sh, const SsspScratch &S, floa
         }
     }
     if (tid < 3) sh.changed[tid] = 0;
+    if (tid < 8) {  // every line of every direction is dirty
+        const int s = tid >> 2, d2 = tid & 3, n = d2 < 2 ? h : w;
+        sh.dirty[s][d2][0] = n >= 64 ? ~0ull : (1ull << n) - 1;
+        sh.dirty[s][d2][1] = n <= 64 ? 0ull : (n >= 128 ? ~0ull : (1ull << (n - 64)) - 1);
+    }
     g.sync();
 }
 
@@ -845,6 +957,11 @@ __device__ __forceinline__ void sssp_init_sources(Shared &sh, float *dist, int n
     if (t < nsrc && sh.src_ok[t])
         dist[t * DIST_FLOATS + (sh.src_s[t][0] - sh.i0 + 1) * pw + (sh.src_s[t][1] - sh.j0 + 1)] = 0.0f;
     if (t < 3) sh.changed[t] = 0;
+    if (t >= 64 && t < 64 + 16) {  // only the source's row / column is dirty (all else is +-inf)
+        const int q = t - 64, s = q >> 3, d2 = (q >> 1) & 3, word = q & 1;
+        const int bit = s < nsrc && sh.src_ok[s] ? (d2 < 2 ? sh.src_s[s][0] - sh.i0 : sh.src_s[s][1] - sh.j0) : -1;
+        sh.dirty[s][d2][word] = bit >= 0 && (bit >> 6) == word ? 1ull << (bit & 63) : 0ull;
+    }
     g.sync();
 }
 
@@ -879,7 +996,7 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
 #ifdef SIMAPS_DIAG_ONESRC  // diagnostic (wrong results): only source 0 sweeps
         if (arr == 1) {} else
 #endif
-        if (sh.src_ok[arr] && sweep(dist + arr * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3) && (tid & 63) == 0)
+        if (sh.src_ok[arr] && sweep(dist + arr * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3, sh.dirty[arr]) && (tid & 63) == 0)
             sh.changed[round % 3] = 1;
 #ifdef SIMAPS_PHASE_STAMPS
         if (round == 0 && wave == 0) STAMP_NB(22);
