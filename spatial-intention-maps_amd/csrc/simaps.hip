@@ -84,6 +84,7 @@ constexpr int MAX_SEG = 128;     // intention / history segments per agent
 constexpr int RBLK = (CROP + 7) / 8;  // 8 x 8 blocks per crop side (robot sets, render_maps)
 constexpr int SEG_PER_ROBOT = SIMAPS_MAX_PATH - 1;
 constexpr int MAX_ROWS = 112;    // room rect rows (bit-row arrays)
+constexpr int RMAX = 7;  // floor(RADIUS * 96) <= 6 for every robot class (envs.py:2421)
 constexpr int WIN_WORDS = 3;     // occupancy window row: up to 192 bits
 constexpr int MAX_WIN_ROWS = MAX_ROWS + 16;
 constexpr unsigned INF_BITS = 0x7f800000u;
@@ -233,6 +234,7 @@ struct Shared {
 struct SsspScratch {
     uint64_t win[MAX_WIN_ROWS][WIN_WORDS];
     B128 freeb[MAX_ROWS];
+    B128 dtab[RMAX + 1][MAX_WIN_ROWS];  // window row dilated horizontally by +-j, rect columns (build_cspace)
 };
 
 constexpr int align16(int x) { return (x + 15) & ~15; }
@@ -288,7 +290,6 @@ __device__ __forceinline__ float wave_max(float v)
 // distance-array pitch: (w + 2) | 1 floats (odd: column-wise sweeps hit at most 2-way bank conflicts)
 __device__ __forceinline__ int sssp_pitch(int w) { return (w + 2) | 1; }
 
-constexpr int RMAX = 7;  // floor(RADIUS * 96) <= 6 for every robot class (envs.py:2421)
 // G threads cover the window: words 0-1 of a row (columns 0..127): thread -> (row t / 128 + (G / 128) q,
 // column t % 128), so every wave holds 64 consecutive columns of one row (one ballot per row word);
 // word 2 (columns 128..133): thread -> (row 8 * wave + lane / 8 + (G / 8) u, column 128 + lane % 8).
@@ -370,12 +371,32 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
     }
     g.sync();
     if (t == 0) STAMP_NB(15);
+    // (1) one lane per window row: its horizontal dilations by +-j (j = 0 .. r) over the rect
+    // columns, T_j = T_{j-1} | (row >> (RMAX + j)) | (row >> (RMAX - j)) (128-bit windows of the
+    // 192-bit row, compile-time shifts)
+    if (t < whM) {
+        const uint64_t x0 = S.win[t][0], x1 = S.win[t][1], x2 = S.win[t][2];
+        auto sh192 = [&](int s_) -> B128 {  // bits s_ .. s_ + 127 of the row
+            if (s_ == 0) return B128{x0, x1};
+            return B128{(x0 >> s_) | (x1 << (64 - s_)), (x1 >> s_) | (x2 << (64 - s_))};
+        };
+        B128 T = sh192(RMAX);
+        S.dtab[0][t] = T;
+#pragma unroll
+        for (int j = 1; j <= RMAX; j++) {
+            if (j <= r) {
+                T = b_or(T, b_or(sh192(RMAX + j), sh192(RMAX - j)));
+                S.dtab[j][t] = T;
+            }
+        }
+    }
     const B128 fm = b_mask(w);
     const int dy = (t & 15) - r;
     int hw = -1;  // disk(r) half-width of row dy (skimage disk: dx^2 + dy^2 <= r^2)
     if (dy <= r)
         while ((hw + 1) * (hw + 1) + dy * dy <= r * r) hw++;
     const int pw = sssp_pitch(w);
+    if (t == 0) STAMP_CLK(52);
     if (dist) {  // border rows 0 and h + 1
         for (int k = t; k < pw; k += G)
             for (int s = 0; s < nsrc; s++) {
@@ -383,26 +404,46 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
                 dist[s * DIST_FLOATS + (h + 1) * pw + k] = -INFINITY;
             }
     }
+    if (t == 0) STAMP_CLK(53);
+    g.sync();
+    // (2) 16 lanes per output row, lane = disk row dy: one table read, then a DPP OR over the lanes
     for (int base = 0; base < h; base += G / 16) {  // uniform: every lane takes part in the DPP ORs
         const int row = base + (t >> 4);
         B128 acc = {0, 0};
-        if (row < h && hw >= 0) {
-            const uint64_t *wrow = S.win[row + RMAX + dy];
-            for (int k = -hw; k <= hw; k++) acc = b_or(acc, win_get(wrow, RMAX + k));
-        }
+        if (row < h && hw >= 0) acc = S.dtab[hw][row + RMAX + dy];
+#ifdef SIMAPS_PHASE_STAMPS
+        if (t == 0 && base == 0) { asm volatile("" ::"v"(acc.lo), "v"(acc.hi)); STAMP_CLK(54); }
+#endif
         const unsigned a0 = row16_or((unsigned)acc.lo), a1 = row16_or((unsigned)(acc.lo >> 32));
         const unsigned a2 = row16_or((unsigned)acc.hi), a3 = row16_or((unsigned)(acc.hi >> 32));
+#ifdef SIMAPS_PHASE_STAMPS
+        if (t == 0 && base == 0) { asm volatile("" ::"v"(a0), "v"(a3)); STAMP_CLK(55); }
+#endif
         const uint64_t lo = ((uint64_t)a1 << 32) | a0, hi = ((uint64_t)a3 << 32) | a2;
         const B128 fr = {~lo & fm.lo, ~hi & fm.hi};
         if ((t & 15) == 0 && row < h) S.freeb[row] = fr;
-        if (dist && row < h) {
-            for (int c = t & 15; c < pw; c += 16) {
-                const float v = (c >= 1 && c <= w && b_test(fr, c - 1)) ? INFINITY : -INFINITY;
-                for (int s = 0; s < nsrc; s++) dist[s * DIST_FLOATS + (row + 1) * pw + c] = v;
+        if (dist && row < h) {  // array column c = rect column c - 1 (fr << 1: column 0 and c > w blocked)
+            const uint64_t f1lo = fr.lo << 1, f1hi = (fr.hi << 1) | (fr.lo >> 63);
+            const uint32_t part[4] = {(uint32_t)f1lo, (uint32_t)(f1lo >> 32), (uint32_t)f1hi, (uint32_t)(f1hi >> 32)};
+            float *drow = dist + (row + 1) * pw;
+            const int l16 = t & 15;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {  // c = l16 + 16 i < pw <= 123
+                const int c = l16 + 16 * i;
+                if (16 * i < pw) {
+                    const float v = ((part[i >> 1] >> (l16 + 16 * (i & 1))) & 1u) ? INFINITY : -INFINITY;
+                    if (c < pw)
+                        for (int s = 0; s < nsrc; s++) drow[s * DIST_FLOATS + c] = v;
+                }
             }
         }
+#ifdef SIMAPS_PHASE_STAMPS
+        if (t == 0) STAMP_CLK(base == 0 ? 56 : 57);
+#endif
     }
+    if (t == 0) STAMP_CLK(58);
     g.sync();
+    if (t == 0) STAMP_CLK(59);
 }
 
 // ------------------------------------------------------------------------------------------------

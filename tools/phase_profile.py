@@ -51,6 +51,7 @@ def main():
            'sweep_rounds_us': {'round_%d' % r: us(19 + r, 18 + r) for r in range(3)},
            'wave_sweep_r0_us': {'start': [us(32 + w, 18) for w in range(8)], 'end': [us(24 + w, 18) for w in range(8)]},
            'clock_mhz_sweep_w0': float(np.median((st[:, 45] - st[:, 44]) / ((st[:, 24] - st[:, 18]) / 100.0))),
+           'dilate_clk_from52': {str(k): float(np.median(st[:, k].astype(np.int64) - st[:, 52].astype(np.int64))) for k in (53, 54, 55, 56, 57, 58, 59)},
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())}}
     print(json.dumps(res, indent=1))
 
