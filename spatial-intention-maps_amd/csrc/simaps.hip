@@ -287,6 +287,16 @@ __device__ __forceinline__ float wave_max(float v)
 // occ: the agent's occupancy map [H, W] (nonzero = obstacle).  r = disk radius (<= RMAX).
 // The window loads are issued first thing by the group that builds the cspace (cspace_load, for the
 // largest radius, so they need no robot descriptor) and land in registers.
+// RN(v / 96) for v == 0 or 1 <= v < 2^32 (every SPFA distance): the reciprocal product with one FMA
+// correction, exhaustively checked against IEEE division over that range (the general division is
+// ~10 instructions)
+__device__ __forceinline__ float div96(float v)
+{
+    const float r = 1.0f / 96.0f;
+    const float q0 = v * r;
+    return fmaf(fmaf(-q0, 96.0f, v), r, q0);
+}
+
 // distance-array pitch: (w + 2) | 1 floats (odd: column-wise sweeps hit at most 2-way bank conflicts)
 __device__ __forceinline__ int sssp_pitch(int w) { return (w + 2) | 1; }
 
@@ -1076,41 +1086,28 @@ __device__ __forceinline__ void sssp_finish(Shared &sh, float *dist, int nsrc, c
     }
 }
 
-// group g, after sssp_finish: dist[] -> the global shortest-path map values in place, so the division
-// runs in the sweep group's slack instead of the distance phase (envs.py:2288-2300: img = sp / 96,
-// img[img < 0] = img.max(), img *= scale; max(sp) / 96 == max(sp / 96): division is monotone)
-__device__ __forceinline__ void sssp_scale(Shared &sh, float *dist, int nsrc, float scale, const Group &g)
-{
-    g.sync();  // sh.dmax
-    const int cells = (sh.h + 2) * sssp_pitch(sh.w);
-    for (int s = 0; s < nsrc; s++) {
-        const float un = (sh.dmax[s] / 96.0f) * scale;
-        for (int q = g.t; q < cells; q += g.n) {
-            float &d = dist[s * DIST_FLOATS + q];
-            d = d != INFINITY ? (d / 96.0f) * scale : un;
-        }
-        if (g.t == 0) sh.unreach[s] = un;
-    }
-}
-
-// group g, after the rounds: finite distances -> global shortest-path map values in one pass
-// (envs.py:2288-2300: img = sp / 96, img[img < 0] = img.max(), img *= scale); blocked / unreachable
-// cells keep +-inf, which the distance phase reads as sh.unreach[s] = (max(sp) / 96) * scale
-// (division and scaling are monotone, so the max of the scaled values is the scaled max).
-__device__ __forceinline__ void sssp_finish_scale(Shared &sh, float *dist, int nsrc, float scale, const Group &g)
+// group g, after the rounds: the maximum reachable distance per source, read-only (envs.py:2288-2300:
+// img = sp / 96, img[img < 0] = img.max(), img *= scale).  The distance phase scales the values it
+// samples and reads blocked / unreachable / border cells (+-inf) as sh.unreach[s] =
+// (max(sp) / 96) * scale (division and scaling are monotone: the max of the scaled values is the
+// scaled max).
+__device__ __forceinline__ void sssp_max(Shared &sh, const float *dist, int nsrc, float scale, const Group &g)
 {
     const int cells = (sh.h + 2) * sssp_pitch(sh.w);
     for (int s = 0; s < nsrc; s++) {
-        float m = -1.0f;
-        for (int q = g.t; q < cells; q += g.n) {
-            float &d = dist[s * DIST_FLOATS + q];
-            const float v = d;
-            if (fabsf(v) != INFINITY) {
-                m = fmaxf(m, v);
-                d = (v / 96.0f) * scale;
-            }
+        const float *D = dist + s * DIST_FLOATS;
+        float m0 = -1.0f, m1 = -1.0f;
+        int q = g.t;
+        for (; q + g.n < cells; q += 2 * g.n) {  // two reads in flight per iteration
+            const float v0 = D[q], v1 = D[q + g.n];
+            m0 = fabsf(v0) != INFINITY ? fmaxf(m0, v0) : m0;
+            m1 = fabsf(v1) != INFINITY ? fmaxf(m1, v1) : m1;
         }
-        m = wave_max(m);
+        if (q < cells) {
+            const float v0 = D[q];
+            m0 = fabsf(v0) != INFINITY ? fmaxf(m0, v0) : m0;
+        }
+        const float m = wave_max(fmaxf(m0, m1));
         if ((g.t & 63) == 0) sh.red[s][g.t >> 6] = m;
     }
     g.sync();
@@ -1564,10 +1561,9 @@ static_assert(PPT * NT == LW * LW, "pixel split");
 
 // Distance channels (all 16 waves): Euclidean map, then shortest-path maps; local -= local.min()
 // (envs.py:2213-2216), so every value is kept in registers until the block minimum is known.
-// The sweep group has already turned the finite dist[] values into channel values
-// (sssp_finish_scale); blocked, unreachable and border cells still hold +-inf and read as the
-// "unreachable" value, which is also the value of every global pixel outside the room rect, so an
-// out-of-rect pixel just reads cell 0 (a border corner).  Everything the
+// A finite dist[] value d becomes (d / 96) * scale here; blocked, unreachable and border cells hold
+// +-inf and read as the "unreachable" value (sssp_max), which is also the value of every global pixel
+// outside the room rect, so an out-of-rect pixel just reads cell 0 (a border corner).  Everything the
 // per-pixel loop needs from `sh` is read once into registers: the loop is straight-line code.
 __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, const simaps_env &ev, const float *dist, int nsrc,
                                          const uint16_t *tab)
@@ -1619,10 +1615,11 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
         if (s >= nsrc) continue;
         const lds_float *D = (const lds_float *)(dist + s * DIST_FLOATS);
         const float un = sh.unreach[s];  // blocked / unreachable / outside the rect (cell 0)
+        const float scale = (float)cfg.shortest_path_map_scale;
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
             const float v = D[max(cell[k], 0)];
-            vals[1 + s][k] = cell[k] < 0 ? 0.0f : (fabsf(v) == INFINITY ? un : v);
+            vals[1 + s][k] = cell[k] < 0 ? 0.0f : (fabsf(v) == INFINITY ? un : div96(v) * scale);
             mins[1 + s] = fminf(mins[1 + s], vals[1 + s][k]);
         }
     }
@@ -1726,12 +1723,13 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
     sssp_rounds(sh, dist, nsrc, g);
 #endif
     if (t == 0) STAMP_NB(49);
-    if (dbg.dist) {  // debug: the raw distances first
+    if (dbg.dist) {  // debug: the raw distances (unreachable -> +inf, read as sh.unreach like -inf)
         sssp_finish(sh, dist, nsrc, g);
         dump_dist(sh, dist, dbg.dist + (size_t)n * 2 * h * w, g);
-        sssp_scale(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);
+        g.sync();
+        if (t < nsrc) sh.unreach[t] = (sh.dmax[t] / 96.0f) * (float)cfg.shortest_path_map_scale;
     } else {
-        sssp_finish_scale(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);  // while the render waves finish
+        sssp_max(sh, dist, nsrc, (float)cfg.shortest_path_map_scale, g);  // while the render waves finish
     }
     if (t == 0) STAMP_NB(50);
 }
