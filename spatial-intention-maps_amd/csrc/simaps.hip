@@ -1329,12 +1329,6 @@ __device__ __forceinline__ void intention_channel_order(Shared &sh, const simaps
 //
 // Sample indices (Mapper._get_local_map, envs.py:2200-2211; rot_src): each output pixel's source
 // index in the crop is computed once per pixel and reused by every channel and the distance phase.
-// Fast path in fp32: |s_f32 - s_f64| < 1e-4 for every term range here (|o| <= 144, |f| <= 200,
-// five roundings of <= 2^-24 relative), so wherever s_f32 + 0.5 lies more than SAMPLE_EPS from an
-// integer and s_f32 more than SAMPLE_EPS from the crop bounds, floor(s + 0.5) and the in-crop test
-// equal the fp64 ones.  The few pixels inside that band (~0.2%) take the exact fp64 rot_src.
-constexpr float SAMPLE_EPS = 4e-4f;
-
 // NPT: output pixels per render thread (18 / 12 / 9 for 8 / 12 / 16 render waves), a compile-time
 // constant so every pixel loop is exact (no bounds tests) and its index math folds.
 template <int NPT>
@@ -1353,35 +1347,21 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     constexpr int GN = NP / NPT;  // == g.n
     static_assert(GN * NPT == NP && GN % 64 == 0, "render group split");
     uint32_t gqp[(MAXPG + 1) / 2];
-    {
+    {   // every pixel exactly in fp64 (rot_src's arithmetic, branch-free): cheaper than an fp32 fast path
+        // whose rounding-band fallback diverges in most waves
         const Rot R = sh.rot;
-        const float c = (float)R.c, sn = (float)R.s, f0 = (float)R.f0, f1 = (float)R.f1;
         const int oa = R.S0 / 2 - LW / 2, ob = R.S1 / 2 - LW / 2;
-        const float hi = CROP - 1;
+        const double hd = CROP - 1;
         int a = g.t / LW, b = g.t % LW;  // pixel p = g.t + k * GN, walked incrementally
         constexpr int da = GN / LW, db = GN % LW;
 #pragma unroll
         for (int k = 0; k < MAXPG; k++) {
-            uint32_t v = 0xffffu;
-            {
-#if defined(SIMAPS_ABL_NOGPIX)
-                v = ((uint32_t)(a + 20) << 8) | (uint32_t)(b + 20);
-#else
-                const float o0 = (float)(a + oa), o1 = (float)(b + ob);
-                const float s0 = (o0 * c + o1 * sn) + f0, s1 = (o0 * (-sn) + o1 * c) + f1;
-                const float u0 = s0 + 0.5f, u1 = s1 + 0.5f;
-                const float k0 = floorf(u0), k1 = floorf(u1);
-                // distances to the crop bounds and to the rounding boundaries, branch-free
-                const float m_in = fmaxf(fabsf(s0 - 0.5f * hi), fabsf(s1 - 0.5f * hi));
-                const float m_fr = fmaxf(fabsf(u0 - k0 - 0.5f), fabsf(u1 - k1 - 0.5f));
-                const int out = m_in > 0.5f * hi + SAMPLE_EPS;
-                const int sure = out | ((m_in < 0.5f * hi - SAMPLE_EPS) & (m_fr < 0.5f - SAMPLE_EPS));
-                const int i0 = (int)k0, i1 = (int)k1;
-                const int inmap = ((unsigned)(ci0 + i0) < (unsigned)H) & ((unsigned)(cj0 + i1) < (unsigned)W);
-                const uint32_t vin = ((out ^ 1) & inmap) ? (((uint32_t)i0 << 8) | (uint32_t)i1) : 0xffffu;
-                v = sure ? vin : 0xfffeu;  // 0xfffe: exact fp64 below
-#endif
-            }
+            const double d0 = a + oa, d1 = b + ob;
+            const double s0 = (d0 * R.c + d1 * R.s) + R.f0, s1 = (d0 * (-R.s) + d1 * R.c) + R.f1;
+            const int in = (s0 >= 0.0) & (s0 <= hd) & (s1 >= 0.0) & (s1 <= hd);
+            const int i0 = (int)floor(s0 + 0.5), i1 = (int)floor(s1 + 0.5);
+            const int inmap = ((unsigned)(ci0 + i0) < (unsigned)H) & ((unsigned)(cj0 + i1) < (unsigned)W);
+            const uint32_t v = (in & inmap) ? (((uint32_t)i0 << 8) | (uint32_t)i1) : 0xffffu;
             if (k & 1) gqp[k >> 1] |= v << 16;
             else gqp[k >> 1] = v | (k == MAXPG - 1 ? 0xffff0000u : 0u);
             a += da;
@@ -1394,27 +1374,6 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
             STAMP_NB(40);
         }
 #endif
-        // the pixels in the rounding band: exact fp64 rot_src (a separate pass keeps the fp64
-        // temporaries out of the fast loop's register budget)
-        bool any = false;
-#pragma unroll
-        for (int k = 0; k < (MAXPG + 1) / 2; k++) any |= ((gqp[k] & 0xffffu) == 0xfffeu) | ((gqp[k] >> 16) == 0xfffeu);
-        if (any) {
-#pragma unroll
-            for (int k = 0; k < MAXPG; k++) {
-                const uint32_t cur = (gqp[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
-                if (cur == 0xfffeu) {
-                    const int p = g.t + k * GN;
-                    int i0, i1;
-                    uint32_t v = 0xffffu;
-                    if (rot_src(R, CROP, p / LW + oa, p % LW + ob, i0, i1)) {
-                        const int gi = ci0 + i0, gj = cj0 + i1;
-                        if (gi >= 0 && gi < H && gj >= 0 && gj < W) v = ((uint32_t)i0 << 8) | (uint32_t)i1;
-                    }
-                    gqp[k >> 1] ^= (v ^ 0xfffeu) << ((k & 1) * 16);
-                }
-            }
-        }
     }
     auto gq_v = [&](int k) -> uint32_t { return (gqp[k >> 1] >> ((k & 1) * 16)) & 0xffffu; };
     // channel index after overhead / robot / distance channels (envs.py:2071-2113 order)
@@ -1848,8 +1807,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
         // Waves own robots (nw / nr waves per robot, interleaved over its box rows); per wave-item 2
         // box rows (lane -> row 2 rp + lane / 32, column lane % 32).  The robot's parameters and mask
-        // window bounds are loaded once per wave.  Source positions in fp32 where they are surely away
-        // from the rounding / bounds boundaries, else exactly in fp64 (rot_src).
+        // window bounds are loaded once per wave; source positions exactly in fp64 (rot_src).
         const int ln = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
         const int nrb = ev.num_robots, wpr = nrb <= nw ? nw / nrb : 1;
         for (int kk = wv; kk < nrb * wpr; kk += nw) {
@@ -1861,7 +1819,6 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             const bool cube = type == SIMAPS_LIFTING && P.lifting;
             const unsigned code0 = P.code0;
             const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
-            const float c = (float)R.c, sn = (float)R.s, f0 = (float)R.f0, f1 = (float)R.f1;
             const int *mt = reinterpret_cast<const int *>(sh.mwin + 120 + 4 * type);
             const int *mc = reinterpret_cast<const int *>(sh.mwin + 120 + 4 * 4);
             const int mt0 = mt[0], mt1 = mt[1], mt2 = mt[2], mt3 = mt[3];
@@ -1870,18 +1827,8 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
                 const int gi = bi0 + 2 * rp + (ln >> 5), gj = bj0 + (ln & 31);
                 unsigned code = 0;
                 if (gi <= bi1 && gj <= bj1) {
-                    const int o0 = gi - st_i, o1 = gj - st_j;
-                    const float hi = LW - 1;
-                    const float s0 = ((float)o0 * c + (float)o1 * sn) + f0, s1 = ((float)o0 * (-sn) + (float)o1 * c) + f1;
-                    const float u0 = s0 + 0.5f, u1 = s1 + 0.5f;
-                    const float k0 = floorf(u0), k1 = floorf(u1);
-                    const float m_in = fmaxf(fabsf(s0 - 0.5f * hi), fabsf(s1 - 0.5f * hi));
-                    const float m_fr = fmaxf(fabsf(u0 - k0 - 0.5f), fabsf(u1 - k1 - 0.5f));
-                    const bool out = m_in > 0.5f * hi + SAMPLE_EPS;
-                    const bool sure = out || (m_in < 0.5f * hi - SAMPLE_EPS && m_fr < 0.5f - SAMPLE_EPS);
-                    int m0 = (int)k0, m1 = (int)k1;
-                    bool in = !out;
-                    if (!sure) in = rot_src(R, LW, o0, o1, m0, m1);
+                    int m0, m1;
+                    const bool in = rot_src(R, LW, gi - st_i, gj - st_j, m0, m1);
                     if (in) {
                         const int r = m0 - mt0, cc = m1 - mt1;
                         if ((unsigned)r < (unsigned)mt2 && (unsigned)cc < (unsigned)mt3 && ((sh.mwin[type * 24 + r] >> cc) & 1u))

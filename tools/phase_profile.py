@@ -52,6 +52,9 @@ def main():
            'wave_sweep_r0_us': {'start': [us(32 + w, 18) for w in range(8)], 'end': [us(24 + w, 18) for w in range(8)]},
            'clock_mhz_sweep_w0': float(np.median((st[:, 45] - st[:, 44]) / ((st[:, 24] - st[:, 18]) / 100.0))),
            'dilate_clk_from52': {str(k): float(np.median(st[:, k].astype(np.int64) - st[:, 52].astype(np.int64))) for k in (53, 54, 55, 56, 57, 58, 59)},
+           'spread_us': {name: [float(np.percentile((st[:, k1].astype(np.int64) - st[:, 0].astype(np.int64)) / 100.0, q)) for q in (10, 50, 90, 100)]
+                         for name, k1 in (('sweep_end', 7), ('render_end', 8), ('join', 4), ('total', 6))},
+           'start_skew_us': float((np.percentile(st[:, 0], 100) - np.percentile(st[:, 0], 0)) / 100.0),
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())}}
     print(json.dumps(res, indent=1))
 
