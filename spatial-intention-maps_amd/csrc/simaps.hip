@@ -50,7 +50,7 @@ namespace {
 constexpr int NT = 1024;
 #ifdef SIMAPS_PHASE_STAMPS
 // Diagnostic build only (libsimaps_prof.so): per-workgroup s_memrealtime (100 MHz) stamps.
-constexpr int MAX_STAMP_WG = 8192, NSTAMP = 64;
+constexpr int MAX_STAMP_WG = 8192, NSTAMP = 80;
 __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
 // (a barrier first, so a stamp marks the moment the SLOWEST wave finished the previous phase)
 #define STAMP(k)                                                                                 \
@@ -799,6 +799,7 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw_rt)
 struct SweepOut {
     uint64_t lanes;
     int imin, imax;
+    int steps;  // lines processed (diagnostics)
 };
 
 // Sweep steps t0 .. (early exit past tmax) of a line space of len lines.
@@ -860,7 +861,7 @@ __device__ SweepOut sweep_asm(lds_float *__restrict__ D, int len, int span, int 
               [gstep] "i"((FWD ? P : -P) * SL * 4)
             : "memory", "scc");
     }
-    return SweepOut{__ballot(acc < 0.0f), t0 + imin, min(t0 + imax, len - 1)};
+    return SweepOut{__ballot(acc < 0.0f), t0 + imin, min(t0 + imax, len - 1), min(tg + 4, lenr)};
 }
 #undef SWA_S2
 #undef SWA_BODY
@@ -911,7 +912,7 @@ __device__ __forceinline__ void mark_range(uint64_t *m, int a, int b)  // bits a
 }
 
 // One sweep of direction dir_in over source dm's array; true if it improved a cell.
-__device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_in, uint64_t (*dm)[2])
+__device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_in, uint64_t (*dm)[2], int &steps)
 {
     lds_float *D = (lds_float *)Dg;  // the distance arrays live in LDS: keep ds_* addressing
     // wave-uniform loop bounds: scalar loop control, no exec-mask merges at the back edge
@@ -947,6 +948,7 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
         case 2: o = h <= 63 ? sweep_asm<2, 1, 95>(D, w, h, t0, tmax) : sweep_asm<2, 2, 95>(D, w, h, t0, tmax); break;
         default: o = h <= 63 ? sweep_asm<3, 1, 95>(D, w, h, t0, tmax) : sweep_asm<3, 2, 95>(D, w, h, t0, tmax); break;
         }
+        steps += o.steps;
         if (!o.lanes) return false;
         if (lane == 0) {
             const int a = fwd ? o.imin : len - 1 - o.imax, b = fwd ? o.imax : len - 1 - o.imin;
@@ -1029,6 +1031,7 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
         else __builtin_amdgcn_s_setprio(2);
     }
 #endif
+    int steps = 0;  // lines this wave processed (diagnostics)
     for (int round = 0;; round++) {
         if (tid == 0) sh.changed[(round + 1) % 3] = 0;
         const int s = wave >> 2;
@@ -1047,7 +1050,7 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
 #ifdef SIMAPS_DIAG_ONESRC  // diagnostic (wrong results): only source 0 sweeps
         if (arr == 1) {} else
 #endif
-        if (sh.src_ok[arr] && sweep(dist + arr * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3, sh.dirty[arr]) && (tid & 63) == 0)
+        if (sh.src_ok[arr] && sweep(dist + arr * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3, sh.dirty[arr], steps) && (tid & 63) == 0)
             sh.changed[round % 3] = 1;
 #ifdef SIMAPS_PHASE_STAMPS
         if (round == 0 && wave == 0) STAMP_NB(22);
@@ -1058,6 +1061,9 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
         g.sync();
         if (!sh.changed[round % 3] || round >= max_rounds) {
             if (tid == 0) sh.rounds = round >= max_rounds ? -1 : round + 1;
+#ifdef SIMAPS_PHASE_STAMPS
+            if ((tid & 63) == 0 && blockIdx.x < MAX_STAMP_WG) g_stamps[blockIdx.x * NSTAMP + 64 + wave] = steps;
+#endif
             break;
         }
     }
@@ -1204,6 +1210,7 @@ __device__ __forceinline__ void raster_lines(Shared &sh, float *tile, const sima
     const int thick = cfg.intention_map_line_thickness;
     if (!have_table && tid < sh.nr) seg_table(sh, cfg, rb, paths, enc, tid, sh.me);
     g.sync();
+    if (tid == 0 && have_table) STAMP_NB(60);
     const int ti0 = sh.pi - TILE_HALF, tj0 = sh.pj - TILE_HALF;
     if (enc == SIMAPS_ENC_CIRCLE) {
         if (tid < sh.nr && tid != sh.me && !sh.rob[tid].idle) {
@@ -1245,6 +1252,7 @@ __device__ __forceinline__ void raster_lines(Shared &sh, float *tile, const sima
             }
         }
     }
+    if (tid == 0 && have_table) STAMP_NB(61);
     g.sync();
 }
 
@@ -1459,6 +1467,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     if (npass > 0) {
         g.sync();
         wait_scratch(sh);
+        if (g.t == 0) STAMP_NB(62);
 #ifndef SIMAPS_ABL_NORASTER
         raster_lines(sh, tile, cfg, rb, paths, encs[0], true, g);
 #endif

@@ -34,7 +34,7 @@ def main():
     for _ in range(3):
         b.render(out)
     torch.cuda.synchronize()
-    st = np.zeros((8192, 64), dtype=np.uint64)
+    st = np.zeros((8192, 80), dtype=np.uint64)
     b.render(out)
     torch.cuda.synchronize()
     assert L.simaps_debug_read_stamps(st.ctypes.data) == 0
@@ -45,7 +45,7 @@ def main():
            'sweep_track_us': {'agent_load': us(43, 0), 'first_ballot': us(46, 43), 'all_ballots': us(47, 46), 'v2_ballots_sync': us(15, 47), 'cspace_loads_ballots': us(15, 0), 'cspace_dilate': us(2, 15), 'cspace': us(2, 0), 'snap': us(48, 2), 'init': us(3, 48), 'rounds': us(49, 3), 'finish': us(50, 49), 'scale': us(7, 50), 'rounds_finish_scale': us(7, 3), 'end': us(7, 0)},
            'render_track_us': {'params': us(9, 0), 'blocksets': us(51, 9), 'stamp_tiles': us(1, 51), 'sampleidx_fast': us(40, 1), 'sampleidx_fp64': us(41, 40),
                                'gather_issue': us(42, 41), 'code_lookup': us(14, 42), 'overhead_robot': us(11, 14),
-                               'raster1': us(13, 11), 'sample_rest': us(8, 13), 'end': us(8, 0)},
+                               'raster_sync_wait': us(62, 11), 'raster_zero_sync': us(60, 62), 'raster_lines': us(61, 60), 'raster_endsync': us(13, 61), 'raster1': us(13, 11), 'sample_rest': us(8, 13), 'end': us(8, 0)},
            'join_us': us(4, 0),
            'distance_us': {'values': us(16, 5), 'block_min': us(17, 16), 'stores': us(6, 17), 'all': us(6, 5)},
            'sweep_rounds_us': {'round_%d' % r: us(19 + r, 18 + r) for r in range(3)},
@@ -55,6 +55,7 @@ def main():
            'spread_us': {name: [float(np.percentile((st[:, k1].astype(np.int64) - st[:, 0].astype(np.int64)) / 100.0, q)) for q in (10, 50, 90, 100)]
                          for name, k1 in (('sweep_end', 7), ('render_end', 8), ('join', 4), ('total', 6))},
            'start_skew_us': float((np.percentile(st[:, 0], 100) - np.percentile(st[:, 0], 0)) / 100.0),
+           'sweep_steps_per_wave': [float(np.median(st[:, 64 + w].astype(np.int64))) for w in range(8)],
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())}}
     print(json.dumps(res, indent=1))
 
