@@ -222,8 +222,9 @@ struct Shared {
     RobotP rob[SIMAPS_MAX_ROBOTS];
     int colbest[2][SIMAPS_MAX_ROOM_W];
     int envg[2][SIMAPS_MAX_ROOM_W];  // Voronoi envelope (rect columns) per source
-    unsigned bar[2][4];              // group barriers {count, generation, timeout, -}: [0] sweeps, [1] render
-    int changed[3];                  // rotating per-round "some sweep improved a cell" flags
+    unsigned bar[4][4];              // group barriers {count, generation, timeout, -}: [0] sweep track, [1] render,
+                                     // [2 + s] source s's sweep waves (rounds)
+    int changed[2][3];               // per source, rotating per-round "some sweep improved a cell" flags
     uint64_t dirty[2][4][2];         // per source and sweep direction: lines (bit L - 1) to relax again
     int scratch_free;                // the cspace scratch may be reused as the raster tile
     uint32_t mwin[5 * 24 + 20];      // robot mask windows: [5][24] bit rows + [5][4] ints (stamp tiles)
@@ -994,7 +995,8 @@ __device__ __forceinline__ void sssp_init(Shared &sh, const SsspScratch &S, floa
             for (int s = 0; s < nsrc; s++) dist[s * DIST_FLOATS + k] = k == sidx[s] ? 0.0f : v;
         }
     }
-    if (tid < 3) sh.changed[tid] = 0;
+    if (tid < 6) (&sh.changed[0][0])[tid] = 0;
+    if (tid == 6) sh.rounds = 0;
     if (tid < 8) {  // every line of every direction is dirty
         const int s = tid >> 2, d2 = tid & 3, n = d2 < 2 ? h : w;
         sh.dirty[s][d2][0] = n >= 64 ? ~0ull : (1ull << n) - 1;
@@ -1009,7 +1011,8 @@ __device__ __forceinline__ void sssp_init_sources(Shared &sh, float *dist, int n
     const int t = g.t, pw = sssp_pitch(sh.w);
     if (t < nsrc && sh.src_ok[t])
         dist[t * DIST_FLOATS + (sh.src_s[t][0] - sh.i0 + 1) * pw + (sh.src_s[t][1] - sh.j0 + 1)] = 0.0f;
-    if (t < 3) sh.changed[t] = 0;
+    if (t < 6) (&sh.changed[0][0])[t] = 0;
+    if (t == 6) sh.rounds = 0;
     if (t >= 64 && t < 64 + 16) {  // only the source's row / column is dirty (all else is +-inf)
         const int q = t - 64, s = q >> 3, d2 = (q >> 1) & 3, word = q & 1;
         const int bit = s < nsrc && sh.src_ok[s] ? (d2 < 2 ? sh.src_s[s][0] - sh.i0 : sh.src_s[s][1] - sh.j0) : -1;
@@ -1019,22 +1022,27 @@ __device__ __forceinline__ void sssp_init_sources(Shared &sh, float *dist, int n
 }
 
 // the sweep group (waves 0 .. 4*nsrc-1): rounds of concurrent sweeps until one changes nothing
-__device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, const Group &g)
+// the sweep waves (waves 0 .. 4*nsrc-1, four per source): rounds of concurrent sweeps until one
+// changes nothing.  Each source runs its own rounds (its own 4-wave barrier and change flags): the
+// two distance arrays are independent, so neither waits for the other's longest sweep.
+__device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, const Group &)
 {
     const int tid = threadIdx.x, wave = tid >> 6;
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
     const int max_rounds = h * w + 16;  // a converged round changes nothing; the cap guards a bug
+    const int s = wave >> 2;
+    const Group gs{tid & 255, 256, sh.bar[2 + s], 4};
+    int *changed = sh.changed[s];
 #ifdef SIMAPS_SWEEP_PRIO
     {   // issue priority: the longer sweeps first (VALU arbitration is priority, then age)
-        const int s = wave >> 2, dir = (wave + 2 * s) & 3;
+        const int dir = (wave + 2 * s) & 3;
         if ((dir >= 2) == (w >= h)) __builtin_amdgcn_s_setprio(3);
         else __builtin_amdgcn_s_setprio(2);
     }
 #endif
     int steps = 0;  // lines this wave processed (diagnostics)
     for (int round = 0;; round++) {
-        if (tid == 0) sh.changed[(round + 1) % 3] = 0;
-        const int s = wave >> 2;
+        if ((tid & 255) == 0) changed[(round + 1) % 3] = 0;
 #ifdef SIMAPS_PHASE_STAMPS
         if (tid == 0 && round < 4) STAMP_NB(18 + round);
         if (round == 0) STAMP_NB(32 + wave);
@@ -1042,25 +1050,21 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
 #endif
         // waves go to SIMD (wave % 4): source 1's directions are rotated by 2 so that every SIMD
         // hosts one row sweep and one column sweep (the long ones would otherwise share two SIMDs)
-#ifdef SIMAPS_DIAG_SWAP_ARRAYS  // diagnostic: waves 0-3 sweep array 1, waves 4-7 array 0
-        const int arr = nsrc == 2 ? 1 - s : s;
-#else
-        const int arr = s;
-#endif
 #ifdef SIMAPS_DIAG_ONESRC  // diagnostic (wrong results): only source 0 sweeps
-        if (arr == 1) {} else
+        if (s == 1) {} else
 #endif
-        if (sh.src_ok[arr] && sweep(dist + arr * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3, sh.dirty[arr], steps) && (tid & 63) == 0)
-            sh.changed[round % 3] = 1;
+        if (sh.src_ok[s] && sweep(dist + s * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3, sh.dirty[s], steps) && (tid & 63) == 0)
+            changed[round % 3] = 1;
 #ifdef SIMAPS_PHASE_STAMPS
         if (round == 0 && wave == 0) STAMP_NB(22);
         if (round == 0 && wave == 2) STAMP_NB(23);
         if (round == 0) STAMP_NB(24 + wave);
         if (round == 0 && wave == 0) STAMP_CLK(45);
 #endif
-        g.sync();
-        if (!sh.changed[round % 3] || round >= max_rounds) {
-            if (tid == 0) sh.rounds = round >= max_rounds ? -1 : round + 1;
+        gs.sync();
+        if (!changed[round % 3] || round >= max_rounds) {
+            if ((tid & 255) == 0)  // cap hit: 1 << 20 (status bit 1)
+                __hip_atomic_fetch_max(&sh.rounds, round >= max_rounds ? 1 << 20 : round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef SIMAPS_PHASE_STAMPS
             if ((tid & 63) == 0 && blockIdx.x < MAX_STAMP_WG) g_stamps[blockIdx.x * NSTAMP + 64 + wave] = steps;
 #endif
@@ -1128,7 +1132,7 @@ __device__ __forceinline__ void sssp_max(Shared &sh, const float *dist, int nsrc
 // all threads (single-kernel users: sssp_grid_kernel, sp_distance_kernel)
 __device__ __forceinline__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
 {
-    if (threadIdx.x < 8) (&sh.bar[0][0])[threadIdx.x] = 0u;
+    if (threadIdx.x < 16) (&sh.bar[0][0])[threadIdx.x] = 0u;
     sssp_init(sh, S, dist, nsrc, Group{(int)threadIdx.x, NT, nullptr, NT / 64});
     const int wave = threadIdx.x >> 6;
     if (wave < 4 * nsrc) sssp_rounds(sh, dist, nsrc, Group{(int)threadIdx.x, 256 * nsrc, sh.bar[0], 4 * nsrc});
@@ -1690,6 +1694,7 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
 #ifndef SIMAPS_ABL_NOSWEEP  // diagnostic: render alone (distance channels wrong)
     sssp_rounds(sh, dist, nsrc, g);
 #endif
+    g.sync();  // each source ran its own rounds: both arrays are final only now
     if (t == 0) STAMP_NB(49);
     if (dbg.dist) {  // debug: the raw distances (unreachable -> +inf, read as sh.unreach like -inf)
         sssp_finish(sh, dist, nsrc, g);
@@ -1728,7 +1733,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     // sources and sweep the distance arrays (4 waves per source); the other waves compute the robot
     // parameters and stamp tiles and render every channel that does not need distances.
     const int cs_waves = nsrc > 0 ? 4 * nsrc : (dbg.cspace ? 4 : 0);
-    if (tid < 8) (&sh.bar[0][0])[tid] = 0u;
+    if (tid < 16) (&sh.bar[0][0])[tid] = 0u;
     if (tid == 8) sh.scratch_free = cs_waves == 0;
     const simaps_env ev = envs[ag.env];
     lds_barrier();  // the group barriers are zeroed
@@ -1884,9 +1889,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     if (dbg.status && tid == 0) {
         int st = 0;
         for (int s = 0; s < nsrc; s++) st |= sh.src_ok[s] ? 0 : 1;
-        if (nsrc > 0 && sh.rounds < 0) st |= 2;
-        if (sh.bar[0][2] | sh.bar[1][2]) st |= 4;
-        dbg.status[n] = st | ((nsrc > 0 ? sh.rounds : 0) << 8);
+        if (nsrc > 0 && sh.rounds >= (1 << 20)) st |= 2;
+        if (sh.bar[0][2] | sh.bar[1][2] | sh.bar[2][2] | sh.bar[3][2]) st |= 4;
+        dbg.status[n] = st | ((nsrc > 0 ? sh.rounds & 0xfffff : 0) << 8);
     }
 #ifdef SIMAPS_PHASE_STAMPS
     if (tid == 0 && blockIdx.x < MAX_STAMP_WG) g_stamps[blockIdx.x * NSTAMP + 10] = (unsigned long long)sh.rounds;

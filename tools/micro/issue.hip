@@ -18,6 +18,7 @@ __global__ void bench(unsigned long long *out, int iters, int active_waves, int 
     if (wave >= active_waves) return;  // after the only barrier
     unsigned va = (threadIdx.x & 63) * 4;
     uint64_t m = 0, m2 = 0;
+    float m2f = 0.0f;
     if constexpr (K == 13) { a = (float)(threadIdx.x & 63); h = (float)active_lanes; }
     unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int it = 0; it < iters; it++) {
@@ -60,13 +61,31 @@ __global__ void bench(unsigned long long *out, int iters, int active_waves, int 
         if constexpr (K == 13)  // 16 x (v_cmpx -> exec = lanes < n, ds_min, restore exec): 3 instr per unit
             asm volatile("s_mov_b64 %4, exec\n" REP16("v_cmpx_lt_f32_e64 %1, %2, %3\n s_nop 0\n ds_min_f32 %0, %3\n s_mov_b64 exec, %4\n") "s_waitcnt lgkmcnt(0)\n"
                          : "+v"(va), "=&s"(m), "+v"(a), "+v"(h), "=&s"(m2) : : "memory", "scc");
+        if constexpr (K == 14)  // the CPL1 sweep step x16 (adds, 2 DPP, min3, ds_min, wait, minimum3, sub, ds_read, min)
+            asm volatile(REP16("v_add_f32_e64 %1, |%0|, %4\n v_add_f32_dpp %2, |%0|, %5 wave_ror:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+                               "v_add_f32_dpp %3, |%0|, %5 wave_rol:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n v_min3_f32 %1, %1, %2, %3\n"
+                               "ds_min_f32 %6, %1 offset:64\n s_waitcnt lgkmcnt(4)\n v_minimum3_f32 %0, %1, %7, %8\n v_sub_f32 %2, %1, %7\n"
+                               "ds_read_b32 %7, %6 offset:128\n v_min_f32 %9, %2, %9\n") "s_waitcnt lgkmcnt(0)\n"
+                         : "+v"(a), "=&v"(b), "=&v"(c), "=&v"(d), "+v"(e), "+v"(f), "+v"(va), "+v"(g), "+v"(h), "+v"(m2f) : : "memory");
+        if constexpr (K == 15)  // same without DPP (plain adds)
+            asm volatile(REP16("v_add_f32_e64 %1, |%0|, %4\n v_add_f32_e64 %2, |%0|, %5\n"
+                               "v_add_f32_e64 %3, |%0|, %5\n v_min3_f32 %1, %1, %2, %3\n"
+                               "ds_min_f32 %6, %1 offset:64\n s_waitcnt lgkmcnt(4)\n v_minimum3_f32 %0, %1, %7, %8\n v_sub_f32 %2, %1, %7\n"
+                               "ds_read_b32 %7, %6 offset:128\n v_min_f32 %9, %2, %9\n") "s_waitcnt lgkmcnt(0)\n"
+                         : "+v"(a), "=&v"(b), "=&v"(c), "=&v"(d), "+v"(e), "+v"(f), "+v"(va), "+v"(g), "+v"(h), "+v"(m2f) : : "memory");
+        if constexpr (K == 16)  // same without LDS
+            asm volatile(REP16("v_add_f32_e64 %1, |%0|, %4\n v_add_f32_dpp %2, |%0|, %5 wave_ror:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+                               "v_add_f32_dpp %3, |%0|, %5 wave_rol:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n v_min3_f32 %1, %1, %2, %3\n"
+                               "v_minimum3_f32 %0, %1, %7, %8\n v_sub_f32 %2, %1, %7\n"
+                               "v_min_f32 %9, %2, %9\n")
+                         : "+v"(a), "=&v"(b), "=&v"(c), "=&v"(d), "+v"(e), "+v"(f), "+v"(va), "+v"(g), "+v"(h), "+v"(m2f) : : "memory");
         if constexpr (K == 12)  // 64 v_pk_add_f32
             asm volatile(REP16("v_pk_add_f32 %0, %1, %2\n v_pk_add_f32 %3, %1, %2\n v_pk_add_f32 %4, %1, %2\n v_pk_add_f32 %5, %1, %2\n")
                          : "=&v"(*(double*)&m), "+v"(*(double*)&m2), "+v"(*(double*)&va), "=&v"(*(double*)&a), "=&v"(*(double*)&c), "=&v"(*(double*)&e));
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if ((threadIdx.x & 63) == 0) out[wave] = t1 - t0;
-    if (threadIdx.x == 0) out[63] = (unsigned long long)(a + b + c + d + e + f + g + h + (float)m + (float)m2 + (float)va);
+    if (threadIdx.x == 0) out[63] = (unsigned long long)(a + b + c + d + e + f + g + h + m2f + (float)m + (float)m2 + (float)va);
 }
 
 template <int K>
@@ -88,23 +107,10 @@ int main()
 {
     unsigned long long *d;
     hipMalloc(&d, 64 * 8);
-    for (int w : {1, 8}) {
-        for (int l : {0, 1, 16, 32, 64}) run<13>("cmpx+nop+dsmin+exec (x4)", d, w, l);
-    }
-    for (int w : {1, 8}) {
-        run<0>("indep v_add_f32", d, w);
-        run<1>("dep v_add_f32", d, w);
-        run<2>("dep dpp chain(+add+nop)", d, w);
-        run<3>("v_cmp->s_or pairs", d, w);
-        run<4>("indep v_cmp->sgpr", d, w);
-        run<5>("indep s_or_b64", d, w);
-        run<6>("ds_min_f32 (64 then wait)", d, w);
-        run<7>("ds_read_b32 (64 then wait)", d, w);
-        run<8>("indep v_min3", d, w);
-        run<9>("dep ds_read roundtrip(x4 instr)", d, w);
-        run<10>("v_add_f32_e64 |abs|", d, w);
-        run<11>("indep v_add_f32_dpp", d, w);
-        run<12>("v_pk_add_f32", d, w);
+    for (int w : {1, 2, 4, 8, 16}) {
+        run<14>("CPL1 step x16 (per instr, 10/step)", d, w);
+        run<15>("CPL1 step no DPP", d, w);
+        run<16>("CPL1 step no LDS (7/step)", d, w);
     }
     return 0;
 }
