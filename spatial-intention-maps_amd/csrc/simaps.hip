@@ -85,6 +85,7 @@ constexpr int RBLK = (CROP + 7) / 8;  // 8 x 8 blocks per crop side (robot sets,
 constexpr int SEG_PER_ROBOT = SIMAPS_MAX_PATH - 1;
 constexpr int MAX_ROWS = 112;    // room rect rows (bit-row arrays)
 constexpr int RMAX = 7;  // floor(RADIUS * 96) <= 6 for every robot class (envs.py:2421)
+static_assert(2 * RMAX < 32, "cspace window funnel shifts");
 constexpr int WIN_WORDS = 3;     // occupancy window row: up to 192 bits
 constexpr int MAX_WIN_ROWS = MAX_ROWS + 16;
 constexpr unsigned INF_BITS = 0x7f800000u;
@@ -382,26 +383,8 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
     }
     g.sync();
     if (t == 0) STAMP_NB(15);
-    // (1) one lane per window row: its horizontal dilations by +-j (j = 0 .. r) over the rect
-    // columns, T_j = T_{j-1} | (row >> (RMAX + j)) | (row >> (RMAX - j)) (128-bit windows of the
-    // 192-bit row, compile-time shifts)
-    if (t < whM) {
-        const uint64_t x0 = S.win[t][0], x1 = S.win[t][1], x2 = S.win[t][2];
-        auto sh192 = [&](int s_) -> B128 {  // bits s_ .. s_ + 127 of the row
-            if (s_ == 0) return B128{x0, x1};
-            return B128{(x0 >> s_) | (x1 << (64 - s_)), (x1 >> s_) | (x2 << (64 - s_))};
-        };
-        B128 T = sh192(RMAX);
-        S.dtab[0][t] = T;
-#pragma unroll
-        for (int j = 1; j <= RMAX; j++) {
-            if (j <= r) {
-                T = b_or(T, b_or(sh192(RMAX + j), sh192(RMAX - j)));
-                S.dtab[j][t] = T;
-            }
-        }
-    }
     const B128 fm = b_mask(w);
+    const int ln = t & 63;
     const int dy = (t & 15) - r;
     int hw = -1;  // disk(r) half-width of row dy (skimage disk: dx^2 + dy^2 <= r^2)
     if (dy <= r)
@@ -416,10 +399,41 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
             }
     }
     if (t == 0) STAMP_CLK(53);
-    g.sync();
-    // (2) 16 lanes per output row, lane = disk row dy: one table read, then a DPP OR over the lanes
+    // Each wave owns 4 output rows per pass, r0 .. r0 + 3, and builds the window rows they need
+    // itself, so no group barrier separates the two steps (neighbouring waves rewrite a few shared
+    // table rows with identical values):
+    // (1) one lane per window row r0 + RMAX - r + lane (lane < 4 + 2r): its horizontal dilations by
+    //     +-j (j = 0 .. r) over the rect columns, T_j = T_{j-1} | (row >> (RMAX + j)) |
+    //     (row >> (RMAX - j)) (128-bit windows of the 192-bit row, compile-time shifts);
+    // (2) 16 lanes per output row, lane = disk row dy: one table read, then a DPP OR over the lanes.
     for (int base = 0; base < h; base += G / 16) {  // uniform: every lane takes part in the DPP ORs
-        const int row = base + (t >> 4);
+        const int r0 = base + 4 * wave;
+        if (r0 < h) {
+            const int wr = r0 + RMAX - r + ln;
+            if (ln < 4 + 2 * r && wr < whM) {
+                const uint64_t x0 = S.win[wr][0], x1 = S.win[wr][1], x2 = S.win[wr][2];
+                const uint32_t d[5] = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32), (uint32_t)x2};
+                // bits s_ .. s_ + 127 of the row (s_ <= 2 RMAX < 32): one funnel shift per dword
+                auto win4 = [&](int s_, int k) { return __builtin_amdgcn_alignbit(d[k + 1], d[k], s_); };
+                uint32_t T[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) T[k] = win4(RMAX, k);
+                S.dtab[0][wr] = B128{T[0] | ((uint64_t)T[1] << 32), T[2] | ((uint64_t)T[3] << 32)};
+#pragma unroll
+                for (int j = 1; j <= RMAX; j++) {
+                    if (j <= r) {
+#pragma unroll
+                        for (int k = 0; k < 4; k++) T[k] |= win4(RMAX + j, k) | win4(RMAX - j, k);
+                        S.dtab[j][wr] = B128{T[0] | ((uint64_t)T[1] << 32), T[2] | ((uint64_t)T[3] << 32)};
+                    }
+                }
+            }
+            // the wave's own LDS writes precede its reads (in-order LDS); keep the compiler in order
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        const int row = r0 + (ln >> 4);
         B128 acc = {0, 0};
         if (row < h && hw >= 0) acc = S.dtab[hw][row + RMAX + dy];
 #ifdef SIMAPS_PHASE_STAMPS
@@ -438,13 +452,23 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
             const uint32_t part[4] = {(uint32_t)f1lo, (uint32_t)(f1lo >> 32), (uint32_t)f1hi, (uint32_t)(f1hi >> 32)};
             float *drow = dist + (row + 1) * pw;
             const int l16 = t & 15;
+            if (pw == 95 && nsrc == 2) {  // BASELINE rooms, two sources: c = 95 is the next row's border
 #pragma unroll
-            for (int i = 0; i < 8; i++) {  // c = l16 + 16 i < pw <= 123
-                const int c = l16 + 16 * i;
-                if (16 * i < pw) {
+                for (int i = 0; i < 6; i++) {
+                    const int c = l16 + 16 * i;
                     const float v = ((part[i >> 1] >> (l16 + 16 * (i & 1))) & 1u) ? INFINITY : -INFINITY;
-                    if (c < pw)
-                        for (int s = 0; s < nsrc; s++) drow[s * DIST_FLOATS + c] = v;
+                    drow[c] = v;
+                    drow[DIST_FLOATS + c] = v;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; i++) {  // c = l16 + 16 i < pw <= 123
+                    const int c = l16 + 16 * i;
+                    if (16 * i < pw) {
+                        const float v = ((part[i >> 1] >> (l16 + 16 * (i & 1))) & 1u) ? INFINITY : -INFINITY;
+                        if (c < pw)
+                            for (int s = 0; s < nsrc; s++) drow[s * DIST_FLOATS + c] = v;
+                    }
                 }
             }
         }
