@@ -1226,18 +1226,22 @@ __device__ __forceinline__ void tile_put(unsigned *tu, int a, int b, float v, in
 
 // Rasterise one pass into the tile (max of line values per pixel).  Zeroes the tile and, unless
 // the params phase already did, builds the segment table; two group barriers.
+// (zeroed: the sweep track already zeroed the tile and the table exists: no zeroing, no barrier)
 __device__ __forceinline__ void raster_lines(Shared &sh, float *tile, const simaps_config &cfg, const simaps_robot *rb,
-                             const double *__restrict__ paths, int enc, bool have_table, const Group &g)
+                             const double *__restrict__ paths, int enc, bool have_table, const Group &g,
+                             bool zeroed = false)
 {
     const int tid = g.t, lane = threadIdx.x & 63, wave = g.t >> 6, nwaves = g.n >> 6;
-    uint4 *tz = reinterpret_cast<uint4 *>(tile);
-    for (int k = tid; k < TILE * TILE / 4; k += g.n) tz[k] = uint4{0u, 0u, 0u, 0u};
-    static_assert(TILE * TILE % 4 == 0, "tile zeroing");
     unsigned *tu = reinterpret_cast<unsigned *>(tile);
     const float scale_f = (float)cfg.intention_map_scale;
     const int thick = cfg.intention_map_line_thickness;
-    if (!have_table && tid < sh.nr) seg_table(sh, cfg, rb, paths, enc, tid, sh.me);
-    g.sync();
+    if (!(zeroed && have_table)) {
+        uint4 *tz = reinterpret_cast<uint4 *>(tile);
+        for (int k = tid; k < TILE * TILE / 4; k += g.n) tz[k] = uint4{0u, 0u, 0u, 0u};
+        if (!have_table && tid < sh.nr) seg_table(sh, cfg, rb, paths, enc, tid, sh.me);
+        g.sync();
+    }
+    static_assert(TILE * TILE % 4 == 0, "tile zeroing");
     if (tid == 0 && have_table) STAMP_NB(60);
     const int ti0 = sh.pi - TILE_HALF, tj0 = sh.pj - TILE_HALF;
     if (enc == SIMAPS_ENC_CIRCLE) {
@@ -1369,7 +1373,8 @@ __device__ __forceinline__ void intention_channel_order(Shared &sh, const simaps
 // constant so every pixel loop is exact (no bounds tests) and its index math folds.
 template <int NPT>
 __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry &geo, const float *__restrict__ ovh,
-                            const simaps_robot *rb, const double *__restrict__ paths, float *tile)
+                            const simaps_robot *rb, const double *__restrict__ paths, float *tile,
+                            const uint8_t *cmap, bool early_tile)
 {
     const simaps_config &cfg = rc.cfg;
     Shared &sh = rc.sh;
@@ -1447,7 +1452,6 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     // Bit g of the code = seg value (g + 5) / 8 (SEG_VALUES robot_group_{g+1}), bit 4 = 0.5,
     // bit 5 = 1.0 (lifted-cube mask); the max over robots is the highest bit.  Outside pixels
     // (0xffff) read the zero guard after the map.
-    const uint8_t *cmap = reinterpret_cast<const uint8_t *>(tile) + (OFF_CMAP - OFF_UNION);
     unsigned codes[(MAXPG + 3) / 4] = {};
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
@@ -1493,11 +1497,13 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     // history / intention passes, rasterised into the LDS tile, which overwrites the code map (every
     // render wave has read it: group barrier) and the sweep track's scratch (wait for its release)
     if (npass > 0) {
-        g.sync();
+        // early_tile: the code map lies outside the tile and the sweep track zeroed the tile when it
+        // released its scratch -- no barrier; else every render wave must be done with the code map
+        if (!early_tile) g.sync();
         wait_scratch(sh);
         if (g.t == 0) STAMP_NB(62);
 #ifndef SIMAPS_ABL_NORASTER
-        raster_lines(sh, tile, cfg, rb, paths, encs[0], true, g);
+        raster_lines(sh, tile, cfg, rb, paths, encs[0], true, g, early_tile);
 #endif
         if (g.t == 0) STAMP_NB(13);
         sample_pass(ch);
@@ -1542,7 +1548,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     // (the tile region is free: every raster pass ended with a group barrier; without one, wait for
     // every render wave's code-map reads and for the sweep track's scratch release)
     if (npass == 0) {
-        g.sync();
+        if (!early_tile) g.sync();
         wait_scratch(sh);
     }
     uint16_t *tab = reinterpret_cast<uint16_t *>(tile);
@@ -1670,7 +1676,7 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
                                             const Geometry &geo, const simaps_agent &ag, const simaps_env &ev,
                                             const simaps_robot *__restrict__ robots,
                                             const uint8_t *__restrict__ occupancy, int nsrc, const simaps_debug &dbg,
-                                            int n, const Group &g)
+                                            int n, const Group &g, bool zero_tile)
 {
     const int t = g.t, H = cfg.H, W = cfg.W;
     const int h = cfg.room_h, w = cfg.room_w;
@@ -1708,7 +1714,12 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
         sssp_init_sources(sh, dist, nsrc, g);
     }
     // every read of the cspace scratch is done (snap_sources ended with a group sync): the render
-    // group may now overwrite it with its raster tile
+    // group may now overwrite it with its raster tile -- zeroed here first when early_tile
+    if (zero_tile) {
+        uint4 *tz = reinterpret_cast<uint4 *>(&S);
+        for (int k = t; k < TILE * TILE / 4; k += g.n) tz[k] = uint4{0u, 0u, 0u, 0u};
+        g.sync();
+    }
     if (t == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         __hip_atomic_store(&sh.scratch_free, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1757,8 +1768,15 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     // sources and sweep the distance arrays (4 waves per source); the other waves compute the robot
     // parameters and stamp tiles and render every channel that does not need distances.
     const int cs_waves = nsrc > 0 ? 4 * nsrc : (dbg.cspace ? 4 : 0);
+    // Small rooms (every small_* BASELINE config): the crop's robot-code map fits in the tail of
+    // distance array 1, outside the raster tile, and the sweep track zeroes the tile when it
+    // releases its scratch (early_tile).  Otherwise the code map lies in the union after the sweep
+    // scratch and the render track zeroes the tile after a barrier.
+    const bool early_tile =
+        nsrc > 0 && (cfg.room_h + 2) * sssp_pitch(cfg.room_w) * 4 <= DIST_FLOATS * 4 - CMAP_BYTES;
+    uint8_t *cmap = reinterpret_cast<uint8_t *>(smem) + (early_tile ? OFF_UNION - CMAP_BYTES : OFF_CMAP);
     if (tid < 16) (&sh.bar[0][0])[tid] = 0u;
-    if (tid == 8) sh.scratch_free = cs_waves == 0;
+    if (tid == 16) sh.scratch_free = cs_waves == 0;
     const simaps_env ev = envs[ag.env];
     lds_barrier();  // the group barriers are zeroed
     if (tid == 0) STAMP_NB(0);
@@ -1766,8 +1784,8 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const RenderCtx rc{cfg, sh, out, C, n};
     if ((tid >> 6) < cs_waves) {
         const Group g{tid, 64 * cs_waves, sh.bar[0], cs_waves};
-        if (cs_waves == 8) sweep_track<512>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g);
-        else sweep_track<256>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g);
+        if (cs_waves == 8) sweep_track<512>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g, early_tile);
+        else sweep_track<256>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g, early_tile);
         STAMP_NB(7);
     } else {
         const int nw = NT / 64 - cs_waves;
@@ -1820,7 +1838,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             P.code0 = (1u << r.group_index) | (r.type != SIMAPS_LIFTING ? 1u << 5 : (!r.lifting ? 1u << 4 : 0u));
         }
         {   // the crop's robot-code map starts empty
-            uint4 *cz = reinterpret_cast<uint4 *>(smem + OFF_CMAP);
+            uint4 *cz = reinterpret_cast<uint4 *>(cmap);
             for (int k = t; k < CMAP_BYTES / 16; k += g.n) cz[k] = uint4{0u, 0u, 0u, 0u};
         }
         // the first history / intention pass's segment table, one lane per robot (raster_lines)
@@ -1841,7 +1859,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         // scipy-rotated mask, evaluated once per workgroup over its <= 32 x 32 global box; the set
         // pixels inside the crop OR their code into the crop's robot-code map (bit g = seg value
         // (g + 5) / 8 of SEG_VALUES robot_group_{g+1}, bit 4 = 0.5, bit 5 = 1.0 lifted-cube mask)
-        uint32_t *cmap32 = reinterpret_cast<uint32_t *>(smem + OFF_CMAP);
+        uint32_t *cmap32 = reinterpret_cast<uint32_t *>(cmap);
         const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
         // Waves own robots (nw / nr waves per robot, interleaved over its box rows); per wave-item 2
         // box rows (lane -> row 2 rp + lane / 32, column lane % 32).  The robot's parameters and mask
@@ -1887,9 +1905,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         if (t == 0) STAMP_NB(1);
 #ifndef SIMAPS_ABL_NORENDER  // diagnostic: sweeps alone (output channels 0.. left unwritten)
         const float *ovh = overhead + (size_t)ag.map_slot * H * W;
-        if (nw == 8) render_maps<18>(rc, g, geo, ovh, rb, paths, tile);
-        else if (nw == 12) render_maps<12>(rc, g, geo, ovh, rb, paths, tile);
-        else render_maps<9>(rc, g, geo, ovh, rb, paths, tile);
+        if (nw == 8) render_maps<18>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile);
+        else if (nw == 12) render_maps<12>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile);
+        else render_maps<9>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile);
 #endif
         if (t == 0) STAMP_NB(8);
     }
