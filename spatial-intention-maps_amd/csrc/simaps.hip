@@ -253,6 +253,9 @@ constexpr int OFF_CMAP = OFF_UNION + align16((int)sizeof(SsspScratch));
 constexpr int CMAP_BYTES = align16(CROP * CROP + 16);
 static_assert(OFF_CMAP + CMAP_BYTES <= OFF_UNION + UNION_BYTES, "code map fits the union");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+static_assert(DIST_FLOATS <= 0x4000 && OFF_DIST + (DIST_FLOATS + 0x3fff) * 4 <= LDS_BYTES,
+              "distance-phase cell reads: cells fit 14 bits, the masked cval read stays in LDS");
+static_assert(2 * LW * LW * 2 <= TILE_BYTES, "sample-index + cell tables fit the raster tile");
 static_assert(offsetof(RobotP, bi0) % 16 == 0 && sizeof(RobotP) % 16 == 0, "RobotP box loads as one b128");
 
 // ------------------------------------------------------------------------------------------------
@@ -1551,10 +1554,20 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         if (!early_tile) g.sync();
         wait_scratch(sh);
     }
+    // second table: the distance-array cell of each pixel (0 = outside the room rect, whose border
+    // cell reads +-inf; 0xffff = cval), so the 16-wave distance phase does no index math
     uint16_t *tab = reinterpret_cast<uint16_t *>(tile);
+    uint16_t *tcell = tab + NP;
+    const int ri0 = ci0 - cfg.room_i0, rj0 = cj0 - cfg.room_j0, pw = sssp_pitch(cfg.room_w);
+    const unsigned rh = cfg.room_h, rw = cfg.room_w;
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
-        tab[g.t + k * GN] = (uint16_t)gq_v(k);
+        const uint32_t v = gq_v(k);
+        const int r = ri0 + (int)(v >> 8), c = rj0 + (int)(v & 0xffu);
+        const int in = (int)((unsigned)r < rh) & (int)((unsigned)c < rw);
+        const uint32_t cell = v == 0xffffu ? 0xffffu : (uint32_t)(((r + 1) * pw + c + 1) & -in);
+        tab[g.t + k * GN] = (uint16_t)v;
+        tcell[g.t + k * GN] = (uint16_t)cell;
     }
 }
 
@@ -1577,37 +1590,26 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
     const int nd = has_eu + nsrc;
     if (nd == 0) return;
     const int ch = 1 + !!cfg.use_robot_map;
-    const int ci0 = __builtin_amdgcn_readfirstlane(sh.pi - HALF_CROP);
-    const int cj0 = __builtin_amdgcn_readfirstlane(sh.pj - HALF_CROP);
-    const int ri0 = __builtin_amdgcn_readfirstlane(ci0 - sh.i0), rj0 = __builtin_amdgcn_readfirstlane(cj0 - sh.j0);
-    const unsigned h = __builtin_amdgcn_readfirstlane(sh.h), w = __builtin_amdgcn_readfirstlane(sh.w);
-    const int pw = sssp_pitch(w);
-    // per pixel: the rect cell index (0 = outside the rect), or -1 outside the rotated crop
-    int cell[PPT];
-    unsigned gpx[PPT];  // (gi << 16) | gj for the Euclidean map
-    unsigned tv[PPT];
+    // per pixel: the distance-array cell (0 = outside the rect), 0xffff outside the rotated crop
+    // (render_maps' second table)
+    unsigned cell[PPT];
 #pragma unroll
-    for (int k = 0; k < PPT; k++) tv[k] = tab[tid + k * NT];
-#pragma unroll
-    for (int k = 0; k < PPT; k++) {  // selects as arithmetic: no exec-mask blocks between the loads
-        const unsigned v = tv[k];
-        const int r = ri0 + (int)(v >> 8), c = rj0 + (int)(v & 0xffu);
-        const int in = (int)((unsigned)r < h) & (int)((unsigned)c < w);
-        cell[k] = (((r + 1) * pw + c + 1) & -in) | -(int)(v == 0xffffu);
-        gpx[k] = ((unsigned)(ci0 + (int)(v >> 8)) << 16) | (unsigned)(cj0 + (int)(v & 0xffu));
-    }
+    for (int k = 0; k < PPT; k++) cell[k] = tab[LW * LW + tid + k * NT];
     // vals[0]: Euclidean map (first, envs.py:2083-2084) if present; vals[1 + s]: source s.  Each
     // branch is wave-uniform and outside the pixel loop, so a channel's loads issue back to back.
     float vals[3][PPT];
     float mins[3] = {INFINITY, INFINITY, INFINITY};
     if (has_eu) {  // envs.py:2278-2286
         const float eus = (float)cfg.distance_to_receptacle_map_scale;
+        const int ci0 = __builtin_amdgcn_readfirstlane(sh.pi - HALF_CROP);
+        const int cj0 = __builtin_amdgcn_readfirstlane(sh.pj - HALF_CROP);
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
-            const int gi = gpx[k] >> 16, gj = gpx[k] & 0xffff;
+            const unsigned tv = tab[tid + k * NT];
+            const int gi = ci0 + (int)(tv >> 8), gj = cj0 + (int)(tv & 0xffu);
             const double px = ((gj + 0.5) - (double)W / 2) / PPM, py = ((double)H / 2 - (gi + 0.5)) / PPM;
             const double dx = ev.receptacle_x - px, dy = ev.receptacle_y - py;
-            const float v = cell[k] < 0 ? 0.0f : (float)sqrt(dx * dx + dy * dy) * eus;
+            const float v = cell[k] == 0xffffu ? 0.0f : (float)sqrt(dx * dx + dy * dy) * eus;
             vals[0][k] = v;
             mins[0] = fminf(mins[0], v);
         }
@@ -1620,8 +1622,8 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
         const float scale = (float)cfg.shortest_path_map_scale;
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
-            const float v = D[max(cell[k], 0)];
-            vals[1 + s][k] = cell[k] < 0 ? 0.0f : (fabsf(v) == INFINITY ? un : div96(v) * scale);
+            const float v = D[cell[k] & 0x3fffu];  // cval: an in-LDS read, discarded
+            vals[1 + s][k] = cell[k] == 0xffffu ? 0.0f : (fabsf(v) == INFINITY ? un : div96(v) * scale);
             mins[1 + s] = fminf(mins[1 + s], vals[1 + s][k]);
         }
     }
