@@ -253,9 +253,13 @@ constexpr int OFF_CMAP = OFF_UNION + align16((int)sizeof(SsspScratch));
 constexpr int CMAP_BYTES = align16(CROP * CROP + 16);
 static_assert(OFF_CMAP + CMAP_BYTES <= OFF_UNION + UNION_BYTES, "code map fits the union");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-static_assert(DIST_FLOATS <= 0x4000 && OFF_DIST + (DIST_FLOATS + 0x3fff) * 4 <= LDS_BYTES,
-              "distance-phase cell reads: cells fit 14 bits, the masked cval read stays in LDS");
-static_assert(2 * LW * LW * 2 <= TILE_BYTES, "sample-index + cell tables fit the raster tile");
+// distance phase: a cval pixel's cell byte offset (16 bits, 4-aligned, past every real cell; its
+// read stays inside the LDS allocation and is discarded)
+constexpr unsigned CVAL_OFF = 0xfffcu;
+static_assert(DIST_FLOATS * 4 <= (int)CVAL_OFF && OFF_DIST + DIST_FLOATS * 4 + (int)CVAL_OFF + 4 <= LDS_BYTES,
+              "distance-phase cell offsets fit 16 bits, the cval read stays in LDS");
+static_assert(LW * LW * 4 <= TILE_BYTES, "sample-index + cell tables fit the raster tile");
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 static_assert(offsetof(RobotP, bi0) % 16 == 0 && sizeof(RobotP) % 16 == 0, "RobotP box loads as one b128");
 
 // ------------------------------------------------------------------------------------------------
@@ -1330,6 +1334,13 @@ struct RenderCtx {
         // 32-bit byte offset from an SGPR base: one VGPR per address (saddr form), no 64-bit adds
         *reinterpret_cast<float *>(reinterpret_cast<char *>(out) + idx * 4u) = v;
     }
+    // chw only: 4 consecutive pixels p .. p + 3 (p % 4 == 0) of channel ch, one 16-byte store
+    __device__ __forceinline__ void put4(int ch, int p, float4 v) const
+    {
+        unsigned idx = ch * LW * LW + p;
+        asm volatile("" : "+v"(idx));
+        *reinterpret_cast<float4 *>(reinterpret_cast<char *>(out) + idx * 4u) = v;
+    }
 };
 
 // Mapper._get_intention_channels (envs.py:2349-2378), the per-agent part: robots ordered by
@@ -1554,10 +1565,9 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         if (!early_tile) g.sync();
         wait_scratch(sh);
     }
-    // second table: the distance-array cell of each pixel (0 = outside the room rect, whose border
-    // cell reads +-inf; 0xffff = cval), so the 16-wave distance phase does no index math
+    // and the byte offset of each pixel's distance-array cell (0 = outside the room rect: the border
+    // cell, +-inf; CVAL_OFF = cval), so the 16-wave distance phase does no index math
     uint16_t *tab = reinterpret_cast<uint16_t *>(tile);
-    uint16_t *tcell = tab + NP;
     const int ri0 = ci0 - cfg.room_i0, rj0 = cj0 - cfg.room_j0, pw = sssp_pitch(cfg.room_w);
     const unsigned rh = cfg.room_h, rw = cfg.room_w;
 #pragma unroll
@@ -1565,9 +1575,9 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         const uint32_t v = gq_v(k);
         const int r = ri0 + (int)(v >> 8), c = rj0 + (int)(v & 0xffu);
         const int in = (int)((unsigned)r < rh) & (int)((unsigned)c < rw);
-        const uint32_t cell = v == 0xffffu ? 0xffffu : (uint32_t)(((r + 1) * pw + c + 1) & -in);
+        const uint32_t cell = v == 0xffffu ? CVAL_OFF : (uint32_t)(((r + 1) * pw + c + 1) & -in) * 4u;
         tab[g.t + k * GN] = (uint16_t)v;
-        tcell[g.t + k * GN] = (uint16_t)cell;
+        tab[NP + g.t + k * GN] = (uint16_t)cell;
     }
 }
 
@@ -1590,11 +1600,17 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
     const int nd = has_eu + nsrc;
     if (nd == 0) return;
     const int ch = 1 + !!cfg.use_robot_map;
-    // per pixel: the distance-array cell (0 = outside the rect), 0xffff outside the rotated crop
-    // (render_maps' second table)
-    unsigned cell[PPT];
+    // Pixels of this thread: two aligned quads 4 * (tid + j * NT) + [0, 4) (in the chw layout one
+    // 16-byte store per channel each) and the single pixel 8 * NT + tid.
+    static_assert(PPT == 9, "two quads + one pixel per thread");
+    auto pix = [&](int k) { return k < 8 ? 4 * (tid + (k >> 2) * NT) + (k & 3) : 8 * NT + tid; };
+    // per pixel: the byte offset of its distance-array cell (0 = outside the rect: the border cell,
+    // +-inf), CVAL_OFF outside the rotated crop (render_maps' second table), used as the LDS address
+    unsigned coff[PPT];
 #pragma unroll
-    for (int k = 0; k < PPT; k++) cell[k] = tab[LW * LW + tid + k * NT];
+    for (int k = 0; k < PPT; k++) {
+        coff[k] = __builtin_nontemporal_load(tab + LW * LW + pix(k));  // one ds_read_u16 each, no unpacking
+    }
     // vals[0]: Euclidean map (first, envs.py:2083-2084) if present; vals[1 + s]: source s.  Each
     // branch is wave-uniform and outside the pixel loop, so a channel's loads issue back to back.
     float vals[3][PPT];
@@ -1605,27 +1621,47 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
         const int cj0 = __builtin_amdgcn_readfirstlane(sh.pj - HALF_CROP);
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
-            const unsigned tv = tab[tid + k * NT];
-            const int gi = ci0 + (int)(tv >> 8), gj = cj0 + (int)(tv & 0xffu);
+            const unsigned sv = tab[pix(k)];
+            const int gi = ci0 + (int)(sv >> 8), gj = cj0 + (int)(sv & 0xffu);
             const double px = ((gj + 0.5) - (double)W / 2) / PPM, py = ((double)H / 2 - (gi + 0.5)) / PPM;
             const double dx = ev.receptacle_x - px, dy = ev.receptacle_y - py;
-            const float v = cell[k] == 0xffffu ? 0.0f : (float)sqrt(dx * dx + dy * dy) * eus;
+            const float v = coff[k] == CVAL_OFF ? 0.0f : (float)sqrt(dx * dx + dy * dy) * eus;
             vals[0][k] = v;
             mins[0] = fminf(mins[0], v);
         }
     }
+    // Source channels (envs.py:2288-2300): a finite distance d -> div96(d) * scale, two pixels per
+    // packed-fp32 op; +-inf -> NaN there (inf - inf in div96), which fminf against the unreachable
+    // value replaces (with |scale|, un = div96(max finite) * |scale| bounds every finite value; a
+    // negative scale flips the signs afterwards, exactly); cval -> +0.
+    const float scale = (float)cfg.shortest_path_map_scale;
+    const bool neg = scale < 0.0f;
+    const float as = fabsf(scale);
 #pragma unroll
-    for (int s = 0; s < 2; s++) {  // envs.py:2288-2300, 2514-2517 (scaled in place by sssp_scale)
+    for (int s = 0; s < 2; s++) {
         if (s >= nsrc) continue;
-        const lds_float *D = (const lds_float *)(dist + s * DIST_FLOATS);
-        const float un = sh.unreach[s];  // blocked / unreachable / outside the rect (cell 0)
-        const float scale = (float)cfg.shortest_path_map_scale;
+        typedef __attribute__((address_space(3))) const char lds_cchar;
+        lds_cchar *D = (lds_cchar *)(dist + s * DIST_FLOATS);
+        const float un = neg ? -sh.unreach[s] : sh.unreach[s];
+        float v[PPT + 1];
 #pragma unroll
-        for (int k = 0; k < PPT; k++) {
-            const float v = D[cell[k] & 0x3fffu];  // cval: an in-LDS read, discarded
-            vals[1 + s][k] = cell[k] == 0xffffu ? 0.0f : (fabsf(v) == INFINITY ? un : div96(v) * scale);
-            mins[1 + s] = fminf(mins[1 + s], vals[1 + s][k]);
+        for (int k = 0; k < PPT; k++) v[k] = *(const lds_float *)(D + coff[k]);
+        v[PPT] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < PPT; k += 2) {
+            const f32x2 d = {v[k], v[k + 1]};
+            const f32x2 q0 = d * (1.0f / 96.0f);
+            const f32x2 e = __builtin_elementwise_fma(-q0, f32x2{96.0f, 96.0f}, d);
+            const f32x2 x = __builtin_elementwise_fma(e, f32x2{1.0f / 96.0f, 1.0f / 96.0f}, q0) * as;
+            vals[1 + s][k] = coff[k] == CVAL_OFF ? 0.0f : fminf(x.x, un);
+            if (k + 1 < PPT) vals[1 + s][k + 1] = coff[k + 1] == CVAL_OFF ? 0.0f : fminf(x.y, un);
         }
+        if (neg) {
+#pragma unroll
+            for (int k = 0; k < PPT; k++) vals[1 + s][k] = coff[k] == CVAL_OFF ? 0.0f : -vals[1 + s][k];
+        }
+#pragma unroll
+        for (int k = 0; k < PPT; k++) mins[1 + s] = fminf(mins[1 + s], vals[1 + s][k]);
     }
     if (tid == 0) STAMP_NB(16);
 #pragma unroll
@@ -1647,8 +1683,17 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
     for (int q = 0; q < 3; q++) {
         if (q == 0 ? !has_eu : q > nsrc) continue;
         const int c = ch + q - 1 + has_eu;
+        const float m = mins[q];
+        if (cfg.layout_chw) {
 #pragma unroll
-        for (int k = 0; k < PPT; k++) rc.put(c, tid + k * NT, vals[q][k] - mins[q]);
+            for (int j = 0; j < 2; j++)
+                rc.put4(c, 4 * (tid + j * NT), make_float4(vals[q][4 * j] - m, vals[q][4 * j + 1] - m,
+                                                            vals[q][4 * j + 2] - m, vals[q][4 * j + 3] - m));
+            rc.put(c, 8 * NT + tid, vals[q][8] - m);
+        } else {
+#pragma unroll
+            for (int k = 0; k < PPT; k++) rc.put(c, pix(k), vals[q][k] - m);
+        }
     }
 }
 

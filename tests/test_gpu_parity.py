@@ -96,6 +96,21 @@ def test_oracle_parity_fresh_seeds(S, cfg):
         _check_state(st[n], O.agent_state(scenes[e], a), scenes[e]['flags'], len(scenes[e]['robots']))
 
 
+@pytest.mark.parametrize('scale', [-0.5, 0.0, 3.0])
+def test_shortest_path_map_scale_signs(S, scale):
+    """The distance phase scales with |scale| and flips signs afterwards; unreachable / blocked
+    cells become the scaled max (envs.py:2288-2300) and cval pixels stay +0, for any scale."""
+    batch, K, synthetic = S
+    for cfg in ['lifting_4-small_divider', 'lifting_2_pushing_2-large_empty-all', 'rescue_4-small_empty']:
+        scenes = [synthetic.make_scene(cfg, 200 + e) for e in range(2)]
+        for sc in scenes:
+            sc['flags'] = dict(sc['flags'], shortest_path_map_scale=scale)
+        b = batch.StateBatch(scenes)
+        st = b.as_hwc(b.render()).cpu().numpy()
+        for n, (e, a) in enumerate(b.agents):
+            _check_state(st[n], O.agent_state(scenes[e], a), scenes[e]['flags'], len(scenes[e]['robots']))
+
+
 def test_full_size_lifting_4_small_divider_properties(S):
     """BASELINE configs[1] size (64 envs x 4 agents): determinism, channel invariants, and a
     seeded sample of agents against the oracle."""
