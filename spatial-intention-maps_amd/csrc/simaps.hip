@@ -1132,32 +1132,43 @@ __device__ __forceinline__ void sssp_finish(Shared &sh, float *dist, int nsrc, c
 // samples and reads blocked / unreachable / border cells (+-inf) as sh.unreach[s] =
 // (max(sp) / 96) * scale (division and scaling are monotone: the max of the scaled values is the
 // scaled max).
+// one wave's part (threads t, t + n, ...) of the max finite value of D[0, cells); -1 if none
+__device__ __forceinline__ float max_finite_part(const float *D, int cells, int t, int n)
+{
+    float m0 = -1.0f, m1 = -1.0f;
+    int q = t;
+    for (; q + n < cells; q += 2 * n) {  // two reads in flight per iteration
+        const float v0 = D[q], v1 = D[q + n];
+        m0 = fabsf(v0) != INFINITY ? fmaxf(m0, v0) : m0;
+        m1 = fabsf(v1) != INFINITY ? fmaxf(m1, v1) : m1;
+    }
+    if (q < cells) {
+        const float v0 = D[q];
+        m0 = fabsf(v0) != INFINITY ? fmaxf(m0, v0) : m0;
+    }
+    return wave_max(fmaxf(m0, m1));
+}
+
+// after the group barrier that follows the partial maxima sh.red[s][0, parts)
+__device__ __forceinline__ void sssp_max_final(Shared &sh, int nsrc, int parts, float scale, int t)
+{
+    if (t < nsrc) {
+        float mm = sh.red[t][0];
+        for (int k = 1; k < parts; k++) mm = fmaxf(mm, sh.red[t][k]);
+        sh.dmax[t] = mm;
+        sh.unreach[t] = (mm / 96.0f) * scale;
+    }
+}
+
 __device__ __forceinline__ void sssp_max(Shared &sh, const float *dist, int nsrc, float scale, const Group &g)
 {
     const int cells = (sh.h + 2) * sssp_pitch(sh.w);
     for (int s = 0; s < nsrc; s++) {
-        const float *D = dist + s * DIST_FLOATS;
-        float m0 = -1.0f, m1 = -1.0f;
-        int q = g.t;
-        for (; q + g.n < cells; q += 2 * g.n) {  // two reads in flight per iteration
-            const float v0 = D[q], v1 = D[q + g.n];
-            m0 = fabsf(v0) != INFINITY ? fmaxf(m0, v0) : m0;
-            m1 = fabsf(v1) != INFINITY ? fmaxf(m1, v1) : m1;
-        }
-        if (q < cells) {
-            const float v0 = D[q];
-            m0 = fabsf(v0) != INFINITY ? fmaxf(m0, v0) : m0;
-        }
-        const float m = wave_max(fmaxf(m0, m1));
+        const float m = max_finite_part(dist + s * DIST_FLOATS, cells, g.t, g.n);
         if ((g.t & 63) == 0) sh.red[s][g.t >> 6] = m;
     }
     g.sync();
-    if (g.t < nsrc) {
-        float mm = sh.red[g.t][0];
-        for (int k = 1; k < g.nw; k++) mm = fmaxf(mm, sh.red[g.t][k]);
-        sh.dmax[g.t] = mm;
-        sh.unreach[g.t] = (mm / 96.0f) * scale;
-    }
+    sssp_max_final(sh, nsrc, g.nw, scale, g.t);
 }
 
 // all threads (single-kernel users: sssp_grid_kernel, sp_distance_kernel)
@@ -1776,6 +1787,18 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
 #ifndef SIMAPS_ABL_NOSWEEP  // diagnostic: render alone (distance channels wrong)
     sssp_rounds(sh, dist, nsrc, g);
 #endif
+    if (nsrc == 2 && G == 512 && !dbg.dist) {
+        // each source's four waves take its maximum as soon as its own rounds end (the arrays are
+        // independent), overlapping the other source's remaining rounds
+        const int s = t >> 8;
+        const float m = max_finite_part(dist + s * DIST_FLOATS, (h + 2) * sssp_pitch(w), t & 255, 256);
+        if ((t & 63) == 0) sh.red[s][(t >> 6) & 3] = m;
+        g.sync();
+        if (t == 0) STAMP_NB(49);
+        sssp_max_final(sh, nsrc, 4, (float)cfg.shortest_path_map_scale, t);
+        if (t == 0) STAMP_NB(50);
+        return;
+    }
     g.sync();  // each source ran its own rounds: both arrays are final only now
     if (t == 0) STAMP_NB(49);
     if (dbg.dist) {  // debug: the raw distances (unreachable -> +inf, read as sh.unreach like -inf)
@@ -1850,6 +1873,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             const simaps_robot &me = rb[ag.robot];
             sh.rot = rot_params(CROP, 90.0 - me.heading * RAD_TO_DEG);
             pos_to_pix(me.x, me.y, H, W, sh.pi, sh.pj);
+            STAMP_NB(72);
         }
         if (t >= 128 && t < 128 + ev.num_robots) {
             const int k = t - 128;
@@ -1883,6 +1907,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             }
             P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
             P.code0 = (1u << r.group_index) | (r.type != SIMAPS_LIFTING ? 1u << 5 : (!r.lifting ? 1u << 4 : 0u));
+            if (k == 0) STAMP_NB(73);
         }
         {   // the crop's robot-code map starts empty
             uint4 *cz = reinterpret_cast<uint4 *>(cmap);
@@ -1890,13 +1915,17 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         }
         // the first history / intention pass's segment table, one lane per robot (raster_lines)
         if ((cfg.use_history_map || cfg.use_intention_map) && t >= 320 && t < 320 + ev.num_robots)
+        {
             seg_table(sh, cfg, rb, paths, cfg.use_history_map ? 4 : cfg.intention_map_encoding, t - 320, ag.robot);
+            if (t == 320) STAMP_NB(74);
+        }
         // the 5 host-computed robot mask windows (stamp tiles below)
         if (t < 5 * 24) sh.mwin[t] = geo.mbits[t / 24][t % 24];
         if (t >= 192 && t < 192 + 20) {
             const int q = t - 192, m = q >> 2, f = q & 3;
             sh.mwin[120 + q] = f == 0 ? geo.mrow0[m] : f == 1 ? geo.mcol0[m] : f == 2 ? geo.mnrows[m] : geo.mncols[m];
         }
+        if (t == 0) STAMP_NB(75);
         g.sync();
         if (t == 0) STAMP_NB(9);
         if (cfg.use_intention_channels && t == 256) intention_channel_order(sh, cfg, rb);
