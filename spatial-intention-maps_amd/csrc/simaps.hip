@@ -1268,18 +1268,57 @@ __device__ __forceinline__ void raster_lines(Shared &sh, float *tile, const sima
             tile_put(tu, a, b, scale_f, thick);
         }
     } else {
-        // one wave per segment, lanes stride over its pixels
+        // The segments' pixels, cut to the tile rows / columns along the major axis (a pixel outside
+        // them only reaches the unsampled halo), in chunks of 64 (one per lane), dealt round-robin
+        // to the waves.  Every wave builds the chunk ranges itself: lane q (and q + 64) holds slot
+        // q's first in-tile pixel and chunk count; an inclusive scan gives each slot's chunk range.
+        static_assert(SIMAPS_MAX_ROBOTS * SEG_PER_ROBOT <= 128, "two slots per lane");
         const int total = sh.nr * SEG_PER_ROBOT;
-        for (int q = wave; q < total; q += nwaves) {
-            const int k = q / SEG_PER_ROBOT, j = q % SEG_PER_ROBOT;
-            if (j >= sh.seg_robot_cnt[k]) continue;
+        int t_lo[2], nch[2], c_end[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int q = lane + 64 * h;
+            t_lo[h] = 0;
+            nch[h] = 0;
+            if (q < total && q % SEG_PER_ROBOT < sh.seg_robot_cnt[q / SEG_PER_ROBOT]) {
+                const Seg &G = sh.seg[q];
+                const int npix = G.last ? G.n : G.n - 1;  // non-final segments drop their last pixel
+                const bool steep = G.dr > G.dc;
+                const int m0 = steep ? G.si : G.sj, m1 = steep ? G.ti : G.tj, lo = steep ? ti0 : tj0;
+                int a0, a1;  // t range whose major coordinate m0 +- t lies in [lo, lo + TILE)
+                if (m1 >= m0) { a0 = lo - m0; a1 = lo + TILE - 1 - m0; }
+                else { a0 = m0 - (lo + TILE - 1); a1 = m0 - lo; }
+                a0 = max(a0, 0);
+                a1 = min(a1, npix - 1);
+                t_lo[h] = a0;
+                nch[h] = a1 >= a0 ? ((a1 - a0) >> 6) + 1 : 0;
+            }
+            int x = nch[h];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int y = __shfl_up(x, d);
+                if (lane >= d) x += y;
+            }
+            c_end[h] = x;
+        }
+        const int tot0 = __builtin_amdgcn_readlane(c_end[0], 63);
+        c_end[1] += tot0;
+        const int nchunks = __builtin_amdgcn_readlane(c_end[1], 63);
+        for (int c = wave; c < nchunks; c += nwaves) {
+            const int h = c < tot0 ? 0 : 1;
+            const uint64_t m = __ballot(h == 0 ? (c < c_end[0]) : (c < c_end[1]));  // c_end is monotone
+            const int L = __builtin_amdgcn_readfirstlane(__builtin_ctzll(m));
+            const int q = L + 64 * h;
+            const int cbeg = __builtin_amdgcn_readlane(h == 0 ? c_end[0] - nch[0] : c_end[1] - nch[1], L);
+            const int t0 = __builtin_amdgcn_readlane(h == 0 ? t_lo[0] : t_lo[1], L);
             const Seg &G = sh.seg[q];
-            const int npix = G.last ? G.n : G.n - 1;  // non-final segments drop their last pixel
+            const int npix = G.last ? G.n : G.n - 1;
             const bool steep = G.dr > G.dc;
             const int major = steep ? G.dr : G.dc, minor = steep ? G.dc : G.dr;
             const int smaj = steep ? (G.ti - G.si > 0 ? 1 : -1) : (G.tj - G.sj > 0 ? 1 : -1);
             const int smin = steep ? (G.tj - G.sj > 0 ? 1 : -1) : (G.ti - G.si > 0 ? 1 : -1);
-            for (int t = lane; t < npix; t += 64) {
+            const int t = t0 + (c - cbeg) * 64 + lane;
+            if (t < npix) {
                 int pr, pc;
                 if (t == G.n - 1) {  // skimage: rr[dc] = r1, cc[dc] = c1
                     pr = G.ti;
@@ -1926,6 +1965,12 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             sh.mwin[120 + q] = f == 0 ? geo.mrow0[m] : f == 1 ? geo.mcol0[m] : f == 2 ? geo.mnrows[m] : geo.mncols[m];
         }
         if (t == 0) STAMP_NB(75);
+#ifdef SIMAPS_PHASE_STAMPS
+        {   // each render wave's arrival at the params barrier (waves 1..6)
+            const int rw = t >> 6;
+            if (rw >= 1 && rw <= 6) STAMP_NB(rw <= 2 ? 55 + rw : 73 + rw);
+        }
+#endif
         g.sync();
         if (t == 0) STAMP_NB(9);
         if (cfg.use_intention_channels && t == 256) intention_channel_order(sh, cfg, rb);
