@@ -1064,13 +1064,15 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
     const int s = wave >> 2;
     const Group gs{tid & 255, 256, sh.bar[2 + s], 4};
     int *changed = sh.changed[s];
-#ifdef SIMAPS_SWEEP_PRIO
-    {   // issue priority: the longer sweeps first (VALU arbitration is priority, then age)
+#ifndef SIMAPS_SHORT_PRIO
+#define SIMAPS_SHORT_PRIO 2
+#endif
+    {   // issue priority over the render waves (which have slack), the longer sweeps first (VALU
+        // arbitration is priority, then age)
         const int dir = (wave + 2 * s) & 3;
         if ((dir >= 2) == (w >= h)) __builtin_amdgcn_s_setprio(3);
-        else __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(SIMAPS_SHORT_PRIO);
     }
-#endif
     int steps = 0;  // lines this wave processed (diagnostics)
     for (int round = 0;; round++) {
         if ((tid & 255) == 0) changed[(round + 1) % 3] = 0;
@@ -1893,6 +1895,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const RenderCtx rc{cfg, sh, out, C, n};
     if ((tid >> 6) < cs_waves) {
         const Group g{tid, 64 * cs_waves, sh.bar[0], cs_waves};
+#ifdef SIMAPS_TRACK_PRIO  // diagnostic: the sweep track issues ahead of the render track
+        __builtin_amdgcn_s_setprio(SIMAPS_TRACK_PRIO);
+#endif
         if (cs_waves == 8) sweep_track<512>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g, early_tile);
         else sweep_track<256>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g, early_tile);
         STAMP_NB(7);
@@ -1965,12 +1970,6 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             sh.mwin[120 + q] = f == 0 ? geo.mrow0[m] : f == 1 ? geo.mcol0[m] : f == 2 ? geo.mnrows[m] : geo.mncols[m];
         }
         if (t == 0) STAMP_NB(75);
-#ifdef SIMAPS_PHASE_STAMPS
-        {   // each render wave's arrival at the params barrier (waves 1..6)
-            const int rw = t >> 6;
-            if (rw >= 1 && rw <= 6) STAMP_NB(rw <= 2 ? 55 + rw : 73 + rw);
-        }
-#endif
         g.sync();
         if (t == 0) STAMP_NB(9);
         if (cfg.use_intention_channels && t == 256) intention_channel_order(sh, cfg, rb);

@@ -46,9 +46,7 @@ def main():
            'render_track_us': {'params': us(9, 0), 'blocksets': us(51, 9), 'stamp_tiles': us(1, 51), 'sampleidx_fast': us(40, 1), 'sampleidx_fp64': us(41, 40),
                                'gather_issue': us(42, 41), 'code_lookup': us(14, 42), 'overhead_robot': us(11, 14),
                                'raster_sync_wait': us(62, 11), 'raster_zero_sync': us(60, 62), 'raster_lines': us(61, 60), 'raster_endsync': us(13, 61), 'raster1': us(13, 11), 'sample_rest': us(8, 13), 'end': us(8, 0)},
-           'params_us': {'rot_crop': us(72, 0), 'robot0': us(73, 0), 'seg_table0': us(74, 0), 'cmap_zero_w0': us(75, 0),
-                         'wave_arrive': [us(75, 0)] + [us(55 + w if w <= 2 else 73 + w, 0) for w in range(1, 7)],
-                         'wave_arrive_p90': [float(np.percentile((st[:, 55 + w if w <= 2 else 73 + w] - st[:, 0]) / 100.0, 90)) for w in range(1, 7)]},
+           'params_us': {'rot_crop': us(72, 0), 'robot0': us(73, 0), 'seg_table0': us(74, 0), 'cmap_zero_w0': us(75, 0)},
            'join_us': us(4, 0),
            'distance_us': {'values': us(16, 5), 'block_min': us(17, 16), 'stores': us(6, 17), 'all': us(6, 5)},
            'sweep_rounds_us': {'round_%d' % r: us(19 + r, 18 + r) for r in range(3)},
