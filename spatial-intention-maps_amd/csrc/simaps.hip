@@ -406,18 +406,22 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
             }
     }
     if (t == 0) STAMP_CLK(53);
-    // Each wave owns 4 output rows per pass, r0 .. r0 + 3, and builds the window rows they need
-    // itself, so no group barrier separates the two steps (neighbouring waves rewrite a few shared
-    // table rows with identical values):
-    // (1) one lane per window row r0 + RMAX - r + lane (lane < 4 + 2r): its horizontal dilations by
+    // Each wave owns a block of R = ceil(h / waves) consecutive output rows r0 .. r0 + R - 1 and
+    // builds the window rows they need itself, once, so no group barrier separates the two steps
+    // (neighbouring waves rewrite a few shared table rows with identical values):
+    // (1) one lane per window row r0 + RMAX - r + lane (lane < R + 2r): its horizontal dilations by
     //     +-j (j = 0 .. r) over the rect columns, T_j = T_{j-1} | (row >> (RMAX + j)) |
     //     (row >> (RMAX - j)) (128-bit windows of the 192-bit row, compile-time shifts);
-    // (2) 16 lanes per output row, lane = disk row dy: one table read, then a DPP OR over the lanes.
-    for (int base = 0; base < h; base += G / 16) {  // uniform: every lane takes part in the DPP ORs
-        const int r0 = base + 4 * wave;
+    // (2) 4 output rows per step, 16 lanes per row, lane = disk row dy: one table read, then a DPP
+    //     OR over the lanes.
+    constexpr int NW = G / 64;
+    static_assert((MAX_ROWS + NW - 1) / NW + 2 * RMAX <= 64, "one table lane per window row");
+    const int R = (h + NW - 1) / NW;
+    const int r0 = wave * R;
+    {
         if (r0 < h) {
             const int wr = r0 + RMAX - r + ln;
-            if (ln < 4 + 2 * r && wr < whM) {
+            if (ln < R + 2 * r && wr < whM) {
                 const uint64_t x0 = S.win[wr][0], x1 = S.win[wr][1], x2 = S.win[wr][2];
                 const uint32_t d[5] = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32), (uint32_t)x2};
                 // bits s_ .. s_ + 127 of the row (s_ <= 2 RMAX < 32): one funnel shift per dword
@@ -440,21 +444,24 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        const int row = r0 + (ln >> 4);
+    }
+    for (int sub = 0; sub < R; sub += 4) {  // uniform: every lane takes part in the DPP ORs
+        const int row = r0 + sub + (ln >> 4);
+        const bool own = sub + (ln >> 4) < R && row < h;
         B128 acc = {0, 0};
-        if (row < h && hw >= 0) acc = S.dtab[hw][row + RMAX + dy];
+        if (own && hw >= 0) acc = S.dtab[hw][row + RMAX + dy];
 #ifdef SIMAPS_PHASE_STAMPS
-        if (t == 0 && base == 0) { asm volatile("" ::"v"(acc.lo), "v"(acc.hi)); STAMP_CLK(54); }
+        if (t == 0 && sub == 0) { asm volatile("" ::"v"(acc.lo), "v"(acc.hi)); STAMP_CLK(54); }
 #endif
         const unsigned a0 = row16_or((unsigned)acc.lo), a1 = row16_or((unsigned)(acc.lo >> 32));
         const unsigned a2 = row16_or((unsigned)acc.hi), a3 = row16_or((unsigned)(acc.hi >> 32));
 #ifdef SIMAPS_PHASE_STAMPS
-        if (t == 0 && base == 0) { asm volatile("" ::"v"(a0), "v"(a3)); STAMP_CLK(55); }
+        if (t == 0 && sub == 0) { asm volatile("" ::"v"(a0), "v"(a3)); STAMP_CLK(55); }
 #endif
         const uint64_t lo = ((uint64_t)a1 << 32) | a0, hi = ((uint64_t)a3 << 32) | a2;
         const B128 fr = {~lo & fm.lo, ~hi & fm.hi};
-        if ((t & 15) == 0 && row < h) S.freeb[row] = fr;
-        if (dist && row < h) {  // array column c = rect column c - 1 (fr << 1: column 0 and c > w blocked)
+        if ((t & 15) == 0 && own) S.freeb[row] = fr;
+        if (dist && own) {  // array column c = rect column c - 1 (fr << 1: column 0 and c > w blocked)
             const uint64_t f1lo = fr.lo << 1, f1hi = (fr.hi << 1) | (fr.lo >> 63);
             const uint32_t part[4] = {(uint32_t)f1lo, (uint32_t)(f1lo >> 32), (uint32_t)f1hi, (uint32_t)(f1hi >> 32)};
             float *drow = dist + (row + 1) * pw;
@@ -480,7 +487,7 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
             }
         }
 #ifdef SIMAPS_PHASE_STAMPS
-        if (t == 0) STAMP_CLK(base == 0 ? 56 : 57);
+        if (t == 0) STAMP_CLK(sub == 0 ? 56 : 57);
 #endif
     }
     if (t == 0) STAMP_CLK(58);
