@@ -308,6 +308,9 @@ __device__ __forceinline__ float div96(float v)
 
 // distance-array pitch: (w + 2) | 1 floats (odd: column-wise sweeps hit at most 2-way bank conflicts)
 __device__ __forceinline__ int sssp_pitch(int w) { return (w + 2) | 1; }
+// byte offset (from distance array 0) of the distance phase's cell table when it lives in that
+// array's unused tail (tail_cells: the table, 96 * 96 u16, fits after the room's cells)
+__device__ __forceinline__ int tail_cells_off(int h, int w) { return ((h + 2) * sssp_pitch(w) * 4 + 15) & ~15; }
 
 // G threads cover the window: words 0-1 of a row (columns 0..127): thread -> (row t / 128 + (G / 128) q,
 // column t % 128), so every wave holds 64 consecutive columns of one row (one ballot per row word);
@@ -1447,7 +1450,7 @@ __device__ __forceinline__ void intention_channel_order(Shared &sh, const simaps
 template <int NPT>
 __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g, const Geometry &geo, const float *__restrict__ ovh,
                             const simaps_robot *rb, const double *__restrict__ paths, float *tile,
-                            const uint8_t *cmap, bool early_tile)
+                            const uint8_t *cmap, bool early_tile, bool tail_cells, float *smem_dist)
 {
     const simaps_config &cfg = rc.cfg;
     Shared &sh = rc.sh;
@@ -1556,7 +1559,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     }
     if (g.t == 0) STAMP_NB(11);
     // sample one rasterised pass into channel c (then the tile may be reused)
-    auto sample_pass = [&](int c) {
+    auto sample_pass = [&](int c, bool last) {
         if (g.t == 0) STAMP_NB(12);
 #pragma unroll
         for (int k = 0; k < MAXPG; k++) {
@@ -1565,7 +1568,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
             asm volatile("" : "+v"(v));
             rc.put(c, p, v != 0xffffu ? tile_sample(tile, ci0 + (int)(v >> 8), cj0 + (int)(v & 0xffu), sh.pi, sh.pj) : 0.0f);
         }
-        g.sync();
+        if (!(last && tail_cells)) g.sync();  // the tile is overwritten next (raster pass or tables)
     };
     // history / intention passes, rasterised into the LDS tile, which overwrites the code map (every
     // render wave has read it: group barrier) and the sweep track's scratch (wait for its release)
@@ -1579,14 +1582,14 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         raster_lines(sh, tile, cfg, rb, paths, encs[0], true, g, early_tile);
 #endif
         if (g.t == 0) STAMP_NB(13);
-        sample_pass(ch);
+        sample_pass(ch, npass == 1);
     }
     // the second history / intention pass (history + intention configs)
     if (npass > 1) {
 #ifndef SIMAPS_ABL_NORASTER
         raster_lines(sh, tile, cfg, rb, paths, encs[1], false, g);
 #endif
-        sample_pass(ch + 1);
+        sample_pass(ch + 1, true);
     }
     ch += npass;
     // baseline intention channels (Mapper._get_intention_channels, envs.py:2349-2378)
@@ -1620,12 +1623,27 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     // hand the sample indices to the distance phase: crop-relative (row << 8 | col), 0xffff = cval
     // (the tile region is free: every raster pass ended with a group barrier; without one, wait for
     // every render wave's code-map reads and for the sweep track's scratch release)
+    // and the byte offset of each pixel's distance-array cell (0 = outside the room rect: the border
+    // cell, +-inf; CVAL_OFF = cval), so the 16-wave distance phase does no index math.  tail_cells
+    // (small rooms, no Euclidean map): only the cell table, in the unused tail of distance array 0,
+    // which no one else touches -- no barrier, no wait
+    if (tail_cells) {
+        uint16_t *tc = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(smem_dist) + tail_cells_off(cfg.room_h, cfg.room_w));
+        const int ri0 = ci0 - cfg.room_i0, rj0 = cj0 - cfg.room_j0, pw = sssp_pitch(cfg.room_w);
+        const unsigned rh = cfg.room_h, rw = cfg.room_w;
+#pragma unroll
+        for (int k = 0; k < MAXPG; k++) {
+            const uint32_t v = gq_v(k);
+            const int r = ri0 + (int)(v >> 8), c = rj0 + (int)(v & 0xffu);
+            const int in = (int)((unsigned)r < rh) & (int)((unsigned)c < rw);
+            tc[g.t + k * GN] = (uint16_t)(v == 0xffffu ? CVAL_OFF : (uint32_t)(((r + 1) * pw + c + 1) & -in) * 4u);
+        }
+        return;
+    }
     if (npass == 0) {
         if (!early_tile) g.sync();
         wait_scratch(sh);
     }
-    // and the byte offset of each pixel's distance-array cell (0 = outside the room rect: the border
-    // cell, +-inf; CVAL_OFF = cval), so the 16-wave distance phase does no index math
     uint16_t *tab = reinterpret_cast<uint16_t *>(tile);
     const int ri0 = ci0 - cfg.room_i0, rj0 = cj0 - cfg.room_j0, pw = sssp_pitch(cfg.room_w);
     const unsigned rh = cfg.room_h, rw = cfg.room_w;
@@ -1650,7 +1668,7 @@ static_assert(PPT * NT == LW * LW, "pixel split");
 // outside the room rect, so an out-of-rect pixel just reads cell 0 (a border corner).  Everything the
 // per-pixel loop needs from `sh` is read once into registers: the loop is straight-line code.
 __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, const simaps_env &ev, const float *dist, int nsrc,
-                                         const uint16_t *tab)
+                                         const uint16_t *tab, const uint16_t *tcell)
 {
     const simaps_config &cfg = rc.cfg;
     Shared &sh = rc.sh;
@@ -1668,7 +1686,7 @@ __device__ __forceinline__ void render_distance_channels(const RenderCtx &rc, co
     unsigned coff[PPT];
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
-        coff[k] = __builtin_nontemporal_load(tab + LW * LW + pix(k));  // one ds_read_u16 each, no unpacking
+        coff[k] = __builtin_nontemporal_load(tcell + pix(k));  // one ds_read_u16 each, no unpacking
     }
     // vals[0]: Euclidean map (first, envs.py:2083-2084) if present; vals[1 + s]: source s.  Each
     // branch is wave-uniform and outside the pixel loop, so a channel's loads issue back to back.
@@ -1893,6 +1911,8 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const bool early_tile =
         nsrc > 0 && (cfg.room_h + 2) * sssp_pitch(cfg.room_w) * 4 <= DIST_FLOATS * 4 - CMAP_BYTES;
     uint8_t *cmap = reinterpret_cast<uint8_t *>(smem) + (early_tile ? OFF_UNION - CMAP_BYTES : OFF_CMAP);
+    const bool tail_cells = early_tile && !cfg.use_distance_to_receptacle_map &&
+                            tail_cells_off(cfg.room_h, cfg.room_w) + LW * LW * 2 <= DIST_FLOATS * 4;
     if (tid < 16) (&sh.bar[0][0])[tid] = 0u;
     if (tid == 16) sh.scratch_free = cs_waves == 0;
     const simaps_env ev = envs[ag.env];
@@ -2032,9 +2052,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         if (t == 0) STAMP_NB(1);
 #ifndef SIMAPS_ABL_NORENDER  // diagnostic: sweeps alone (output channels 0.. left unwritten)
         const float *ovh = overhead + (size_t)ag.map_slot * H * W;
-        if (nw == 8) render_maps<18>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile);
-        else if (nw == 12) render_maps<12>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile);
-        else render_maps<9>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile);
+        if (nw == 8) render_maps<18>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile, tail_cells, dist);
+        else if (nw == 12) render_maps<12>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile, tail_cells, dist);
+        else render_maps<9>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile, tail_cells, dist);
 #endif
         if (t == 0) STAMP_NB(8);
     }
@@ -2043,7 +2063,10 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
 
     // ---- all waves: distance channels (need the converged sweeps)
     STAMP(5);
-    render_distance_channels(rc, ev, dist, nsrc, reinterpret_cast<const uint16_t *>(tile));
+    render_distance_channels(rc, ev, dist, nsrc, reinterpret_cast<const uint16_t *>(tile),
+                             tail_cells ? reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(dist) +
+                                                                          tail_cells_off(cfg.room_h, cfg.room_w))
+                                        : reinterpret_cast<const uint16_t *>(tile) + LW * LW);
     STAMP(6);
 
     // ---- debug outputs
