@@ -250,6 +250,10 @@ constexpr int LDS_BYTES = OFF_UNION + UNION_BYTES;
 // stamps phase and read by the overhead / robot channels before the first raster pass: it shares the
 // union with the sweep track's scratch (disjoint offsets) and with the raster tile (later in time).
 constexpr int OFF_CMAP = OFF_UNION + align16((int)sizeof(SsspScratch));
+// early_tile: the raster tile's first SCRATCH_Q 16-byte words overlap the cspace scratch (zeroed by
+// the sweep track once it is released); the render track zeroes the rest at its start
+constexpr int SCRATCH_Q = align16((int)sizeof(SsspScratch)) / 16;
+static_assert(SCRATCH_Q <= TILE * TILE / 4, "scratch inside the tile");
 constexpr int CMAP_BYTES = align16(CROP * CROP + 16);
 static_assert(OFF_CMAP + CMAP_BYTES <= OFF_UNION + UNION_BYTES, "code map fits the union");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -1841,7 +1845,7 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
     // group may now overwrite it with its raster tile -- zeroed here first when early_tile
     if (zero_tile) {
         uint4 *tz = reinterpret_cast<uint4 *>(&S);
-        for (int k = t; k < TILE * TILE / 4; k += g.n) tz[k] = uint4{0u, 0u, 0u, 0u};
+        for (int k = t; k < SCRATCH_Q; k += g.n) tz[k] = uint4{0u, 0u, 0u, 0u};  // the rest: render params
         g.sync();
     }
     if (t == 0) {
@@ -1983,6 +1987,10 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         {   // the crop's robot-code map starts empty
             uint4 *cz = reinterpret_cast<uint4 *>(cmap);
             for (int k = t; k < CMAP_BYTES / 16; k += g.n) cz[k] = uint4{0u, 0u, 0u, 0u};
+            if (early_tile) {  // the raster tile beyond the cspace scratch (the sweep track zeroes the rest)
+                uint4 *tz = reinterpret_cast<uint4 *>(tile);
+                for (int k = SCRATCH_Q + t; k < TILE * TILE / 4; k += g.n) tz[k] = uint4{0u, 0u, 0u, 0u};
+            }
         }
         // the first history / intention pass's segment table, one lane per robot (raster_lines)
         if ((cfg.use_history_map || cfg.use_intention_map) && t >= 320 && t < 320 + ev.num_robots)
