@@ -230,6 +230,7 @@ struct Shared {
     int scratch_free;                // the cspace scratch may be reused as the raster tile
     uint32_t mwin[5 * 24 + 20];      // robot mask windows: [5][24] bit rows + [5][4] ints (stamp tiles)
     Seg seg[MAX_SEG];
+    double seglen[MAX_SEG];          // seg_geom -> seg_ramp: each segment's scaled length
 };
 
 // SSSP scratch (aliases the raster tile, which is only used after the SSSP phase)
@@ -1242,6 +1243,48 @@ __device__ __forceinline__ void seg_table(Shared &sh, const simaps_config &cfg, 
     sh.seg_robot_cnt[k] = cnt;
 }
 
+// seg_table split over one lane per segment slot q = k * SEG_PER_ROBOT + (i - 1) (segment
+// path[i - 1] -> path[i] of robot k): seg_geom (the pixels and the scaled length) in the params
+// phase, seg_ramp (the running length L in path order, then the linspace ramp) after a barrier.
+// Same fp64 operations in the same order as seg_table; a robot's segments no longer run serially.
+__device__ __forceinline__ void seg_geom(Shared &sh, const simaps_config &cfg, const simaps_robot *rb,
+                                         const double *__restrict__ paths, int enc, int q, int me)
+{
+    const int k = q / SEG_PER_ROBOT, i = q % SEG_PER_ROBOT + 1;
+    const simaps_robot &r = rb[k];
+    const bool on = k != me && !r.idle && enc != SIMAPS_ENC_CIRCLE;
+    const int off = enc == 4 ? r.history_off : r.intention_off;
+    const int full = enc == 4 ? r.history_len : r.intention_len;
+    const bool as_line = enc == SIMAPS_ENC_LINE && full >= 2;  // [path[0], path[-1]] (envs.py:2315-2316)
+    const int len = as_line ? 2 : full;
+    if (i == 1) sh.seg_robot_cnt[k] = on && len >= 2 ? min(len - 1, SEG_PER_ROBOT) : 0;
+    if (!on || i >= len) return;
+    const int ia = i - 1, ib = as_line ? full - 1 : i;
+    const double sx = paths[2 * (off + ia)], sy = paths[2 * (off + ia) + 1];
+    const double tx = paths[2 * (off + ib)], ty = paths[2 * (off + ib) + 1];
+    const double dx = tx - sx, dy = ty - sy;
+    sh.seglen[q] = cfg.intention_map_scale * sqrt(dx * dx + dy * dy);  // envs.py:2324, 2557-2558
+    Seg &G = sh.seg[q];
+    pos_to_pix(sx, sy, cfg.H, cfg.W, G.si, G.sj);
+    pos_to_pix(tx, ty, cfg.H, cfg.W, G.ti, G.tj);
+    G.dr = abs(G.ti - G.si);
+    G.dc = abs(G.tj - G.sj);
+    G.n = (G.dr > G.dc ? G.dr : G.dc) + 1;
+    G.last = (i == len - 1);
+}
+__device__ __forceinline__ void seg_ramp(Shared &sh, int q)
+{
+    const int k = q / SEG_PER_ROBOT, j = q % SEG_PER_ROBOT;
+    if (j >= sh.seg_robot_cnt[k]) return;
+    double L = 0.0;
+    for (int m = 0; m < j; m++) L += sh.seglen[k * SEG_PER_ROBOT + m];
+    Seg &G = sh.seg[q];
+    // np.clip(np.linspace(1 - L, 1 - (L + seg), n), 0, 1) (envs.py:2335)
+    G.start = 1 - L;
+    G.stop = 1 - (L + sh.seglen[q]);
+    G.step = G.n > 1 ? (G.stop - G.start) / (G.n - 1) : 0.0;
+}
+
 // max(v) into tile cell (a, b) and, for thick lines, its 4-neighbours: the grey dilation with disk(1)
 // (envs.py:2343-2344) applied as a scatter at raster time, so a sample is one read.  The cross is
 // symmetric, so scattering each line pixel into its cross equals dilating the raster; the tile's
@@ -1289,6 +1332,7 @@ __device__ __forceinline__ void raster_lines(Shared &sh, float *tile, const sima
         // to the waves.  Every wave builds the chunk ranges itself: lane q (and q + 64) holds slot
         // q's first in-tile pixel and chunk count; an inclusive scan gives each slot's chunk range.
         static_assert(SIMAPS_MAX_ROBOTS * SEG_PER_ROBOT <= 128, "two slots per lane");
+        static_assert(320 + SIMAPS_MAX_ROBOTS * SEG_PER_ROBOT <= 512, "one params-phase lane per segment slot");
         const int total = sh.nr * SEG_PER_ROBOT;
         int t_lo[2], nch[2], c_end[2];
 #pragma unroll
@@ -1993,9 +2037,10 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             }
         }
         // the first history / intention pass's segment table, one lane per robot (raster_lines)
-        if ((cfg.use_history_map || cfg.use_intention_map) && t >= 320 && t < 320 + ev.num_robots)
-        {
-            seg_table(sh, cfg, rb, paths, cfg.use_history_map ? 4 : cfg.intention_map_encoding, t - 320, ag.robot);
+        const bool segs = (cfg.use_history_map || cfg.use_intention_map) && t >= 320 &&
+                          t < 320 + ev.num_robots * SEG_PER_ROBOT;
+        if (segs) {
+            seg_geom(sh, cfg, rb, paths, cfg.use_history_map ? 4 : cfg.intention_map_encoding, t - 320, ag.robot);
             if (t == 320) STAMP_NB(74);
         }
         // the 5 host-computed robot mask windows (stamp tiles below)
@@ -2007,6 +2052,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         if (t == 0) STAMP_NB(75);
         g.sync();
         if (t == 0) STAMP_NB(9);
+        if (segs) seg_ramp(sh, t - 320);  // (the segment table is read at raster time, many barriers later)
         if (cfg.use_intention_channels && t == 256) intention_channel_order(sh, cfg, rb);
 
         if (t == 0) STAMP_NB(51);
