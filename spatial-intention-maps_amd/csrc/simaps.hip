@@ -352,6 +352,75 @@ __device__ __forceinline__ void cspace_load(OccLoad<G> &L, const uint8_t *__rest
     }
 }
 
+// Dword variant (the sweep track, G threads, rows 4-byte aligned in a map whose window columns lie
+// inside it): each load covers 4 window columns from the aligned column a0 = (j0 - RMAX) & ~3, so the
+// window rows land shifted by sub = (j0 - RMAX) - a0 bits, which the dilation's funnel shifts absorb.
+// 128 rows x 32 dwords (columns 0..127) as 2 rows per wave load, + 128 rows x 4 dwords (128..143).
+template <int G>
+struct OccLoad4 {
+    static constexpr int NQ = 4096 / G, NU = 512 / G;
+    uint32_t v[NQ], v2[NU];
+    int sub;
+};
+__host__ __device__ __forceinline__ bool occ4_ok(int H, int W, int j0)
+{
+    const int a0 = (j0 - RMAX) & ~3;
+    return (W & 3) == 0 && j0 - RMAX >= 0 && a0 + 144 <= W;
+}
+template <int G>
+__device__ __forceinline__ void cspace_load4(OccLoad4<G> &L, const uint8_t *__restrict__ occ, int H, int W, int i0, int j0,
+                                             int h, int t)
+{
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)occ, (short)0, H * W, 0x00020000);
+    const int lane = t & 63, wave = t >> 6;
+    const int wh = h + 2 * RMAX, a0 = (j0 - RMAX) & ~3;
+    L.sub = (j0 - RMAX) - a0;
+#pragma unroll
+    for (int q = 0; q < OccLoad4<G>::NQ; q++) {
+        const int rr = 2 * (wave + (G / 64) * q) + (lane >> 5), gi = i0 - RMAX + rr;
+        const bool in = ((unsigned)rr < (unsigned)wh) & ((unsigned)gi < (unsigned)H);
+        L.v[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, in ? gi * W + a0 + 4 * (lane & 31) : -1, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < OccLoad4<G>::NU; u++) {
+        const int k = t + G * u, rr = k >> 2, gi = i0 - RMAX + rr;
+        const bool in = ((unsigned)rr < (unsigned)wh) & ((unsigned)gi < (unsigned)H);
+        L.v2[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, in ? gi * W + a0 + 128 + 4 * (k & 3) : -1, 0, 0);
+    }
+}
+// bit b of the result = (byte b of x != 0), b = 0..3
+__device__ __forceinline__ unsigned nib4(unsigned x)
+{
+    x |= x >> 4;
+    x |= x >> 2;
+    x |= x >> 1;  // bit 8b = OR of byte b's bits
+    return ((x & 0x01010101u) * 0x01020408u) >> 24;
+}
+template <int G>
+__device__ __forceinline__ void win_from_dwords(SsspScratch &S, const OccLoad4<G> &L, int whM, int t)
+{
+    const int lane = t & 63, wave = t >> 6;
+    uint32_t *win32 = reinterpret_cast<uint32_t *>(&S.win[0][0]);
+#pragma unroll
+    for (int q = 0; q < OccLoad4<G>::NQ; q++) {
+        // the 8 nibbles of lanes 8j .. 8j + 7 are word j of a row: OR them into lane 8j + 7
+        unsigned x = nib4(L.v[q]) << (4 * (lane & 7));
+        x |= (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xf, 0xf, true);  // row_shr:1
+        x |= (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x112, 0xf, 0xf, true);  // row_shr:2
+        x |= (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xf, 0xf, true);  // row_shr:4
+        const int rr = 2 * (wave + (G / 64) * q) + (lane >> 5);
+        if ((lane & 7) == 7 && rr < whM) win32[rr * 6 + ((lane >> 3) & 3)] = x;
+    }
+#pragma unroll
+    for (int u = 0; u < OccLoad4<G>::NU; u++) {
+        const int k = t + G * u, rr = k >> 2;
+        unsigned x = nib4(L.v2[u]) << (4 * (k & 3));
+        x |= (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xf, 0xf, true);
+        x |= (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x112, 0xf, 0xf, true);
+        if ((k & 3) == 3 && rr < whM) win32[rr * 6 + 4] = x;
+    }
+}
+
 // OR of x over the 16 lanes of its DPP row (quad swaps, then half-row and row mirrors)
 __device__ __forceinline__ unsigned row16_or(unsigned x)
 {
@@ -371,11 +440,14 @@ __device__ __forceinline__ unsigned row16_or(unsigned x)
 // the snapped sources to 0): no separate init pass over the arrays.
 template <int G>
 __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L, int h, int w, int r, const Group &g,
-                                             float *dist = nullptr, int nsrc = 0)
+                                             float *dist = nullptr, int nsrc = 0, const OccLoad4<G> *L4 = nullptr)
 {
     const int t = g.t, lane = t & 63, wave = t >> 6;
     const int whM = h + 2 * RMAX, wwM = w + 2 * RMAX;
-    {
+    const int sub = L4 ? L4->sub : 0;  // window bit k = column k - sub (dword loads)
+    if (L4) {
+        win_from_dwords<G>(S, *L4, whM, t);
+    } else {
         const int c = t & 127, r0 = t >> 7;
 #pragma unroll
         for (int q = 0; q < OccLoad<G>::NQ; q++) {
@@ -433,7 +505,7 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
                 const uint64_t x0 = S.win[wr][0], x1 = S.win[wr][1], x2 = S.win[wr][2];
                 const uint32_t d[5] = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32), (uint32_t)x2};
                 // bits s_ .. s_ + 127 of the row (s_ <= 2 RMAX < 32): one funnel shift per dword
-                auto win4 = [&](int s_, int k) { return __builtin_amdgcn_alignbit(d[k + 1], d[k], s_); };
+                auto win4 = [&](int s_, int k) { return __builtin_amdgcn_alignbit(d[k + 1], d[k], s_ + sub); };
                 uint32_t T[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) T[k] = win4(RMAX, k);
@@ -1853,10 +1925,13 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
     const int t = g.t, H = cfg.H, W = cfg.W;
     const int h = cfg.room_h, w = cfg.room_w;
     OccLoad<G> occ_regs;  // issued first: they depend on the map slot only
+    OccLoad4<G> occ4;
+    const bool use4 = G == 512 && occ4_ok(H, W, cfg.room_j0);  // dword loads: 9 per thread instead of 34
 #ifdef SIMAPS_PHASE_STAMPS
     if (t == 0 && ag.map_slot >= 0) STAMP_NB(43);  // the agent record has landed
 #endif
-    cspace_load<G>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, h, w, t);
+    if (use4) cspace_load4<G>(occ4, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, h, t);
+    else cspace_load<G>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, h, w, t);
     const simaps_robot *rb = robots + ev.robot_off;
     if (t == 0) {
         sh.h = h;
@@ -1875,7 +1950,7 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
         }
         sh.nsrc = ns;
     }
-    build_cspace<G>(S, occ_regs, h, w, geo.cspace_r[rb[ag.robot].type], g, dist, nsrc);  // (its first sync publishes sh)
+    build_cspace<G>(S, occ_regs, h, w, geo.cspace_r[rb[ag.robot].type], g, dist, nsrc, use4 ? &occ4 : nullptr);  // (its first sync publishes sh)
     if (t == 0) STAMP_NB(2);
     if (dbg.cspace) {
         for (int k = t; k < h * w; k += g.n) dbg.cspace[(size_t)n * h * w + k] = b_test(S.freeb[k / w], k % w) ? 1 : 0;
