@@ -2103,12 +2103,20 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             P.code0 = (1u << r.group_index) | (r.type != SIMAPS_LIFTING ? 1u << 5 : (!r.lifting ? 1u << 4 : 0u));
             if (k == 0) STAMP_NB(73);
         }
-        {   // the crop's robot-code map starts empty
-            uint4 *cz = reinterpret_cast<uint4 *>(cmap);
-            for (int k = t; k < CMAP_BYTES / 16; k += g.n) cz[k] = uint4{0u, 0u, 0u, 0u};
-            if (early_tile) {  // the raster tile beyond the cspace scratch (the sweep track zeroes the rest)
-                uint4 *tz = reinterpret_cast<uint4 *>(tile);
-                for (int k = SCRATCH_Q + t; k < TILE * TILE / 4; k += g.n) tz[k] = uint4{0u, 0u, 0u, 0u};
+        {   // the crop's robot-code map starts empty; with 8 render waves the zeroing goes to the
+            // waves without parameter work (3, 4, 6, 7), so the robot and segment waves reach the
+            // barrier sooner
+            const int w8 = t >> 6;
+            const bool z8 = g.n == 512;
+            const int zt = z8 ? (w8 == 3 || w8 == 4 ? t - 192 : (w8 >= 6 ? t - 256 : -1)) : t;
+            const int zn = z8 ? 256 : g.n;
+            if (zt >= 0) {
+                uint4 *cz = reinterpret_cast<uint4 *>(cmap);
+                for (int k = zt; k < CMAP_BYTES / 16; k += zn) cz[k] = uint4{0u, 0u, 0u, 0u};
+                if (early_tile) {  // the raster tile beyond the cspace scratch (the sweep track zeroes the rest)
+                    uint4 *tz = reinterpret_cast<uint4 *>(tile);
+                    for (int k = SCRATCH_Q + zt; k < TILE * TILE / 4; k += zn) tz[k] = uint4{0u, 0u, 0u, 0u};
+                }
             }
         }
         // the first history / intention pass's segment table, one lane per robot (raster_lines)
