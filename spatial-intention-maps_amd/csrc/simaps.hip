@@ -2056,6 +2056,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         const Group g{tid - 64 * cs_waves, 64 * nw, cs_waves ? sh.bar[1] : nullptr, nw};
         const int t = g.t;
         const simaps_robot *rb = robots + ev.robot_off;
+#if SIMAPS_RENDER_PRIO
+        __builtin_amdgcn_s_setprio(SIMAPS_RENDER_PRIO);
+#endif
         // ---- parameters (one lane per robot; the agent's own local rotation on another wave)
         if (t == 0) {
             sh.nr = ev.num_robots;
@@ -2134,6 +2137,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         }
         if (t == 0) STAMP_NB(75);
         g.sync();
+#if SIMAPS_RENDER_PRIO && SIMAPS_RENDER_PRIO_END == 1
+        __builtin_amdgcn_s_setprio(0);
+#endif
         if (t == 0) STAMP_NB(9);
         if (segs) seg_ramp(sh, t - 320);  // (the segment table is read at raster time, many barriers later)
         if (cfg.use_intention_channels && t == 256) intention_channel_order(sh, cfg, rb);
@@ -2186,6 +2192,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             }
         }
         g.sync();
+#if SIMAPS_RENDER_PRIO && SIMAPS_RENDER_PRIO_END == 2
+        __builtin_amdgcn_s_setprio(0);
+#endif
         if (t == 0) STAMP_NB(1);
 #ifndef SIMAPS_ABL_NORENDER  // diagnostic: sweeps alone (output channels 0.. left unwritten)
         const float *ovh = overhead + (size_t)ag.map_slot * H * W;
