@@ -6,7 +6,7 @@
  * hipStream_t passed as void* (NULL = default stream); every compute call is asynchronous on it.
  * Return value: 0 = ok, negative = error (see SIMAPS_E*; simaps_last_error() has the text).
  * No exceptions cross the ABI.  Thread-safe: no global mutable state besides the last-error
- * string (thread-local).
+ * string (thread-local) and the process-wide device fault word (simaps_fault_status).
  *
  * Reference interfaces replaced (file:line relative to the reference repo root):
  *   simaps_get_state    <- Mapper.get_state (envs.py:2068-2185) for a batch of agents, including
@@ -15,6 +15,8 @@
  *                          VectorEnv.get_state(all_robots=True) (envs.py:322-323) returns.
  *   simaps_sssp_grid    <- GridGraph(grid).shortest_path_image(source)
  *                          (shortest_paths/shortest_paths.pyx:24-67, 69-119, 165-167), batched.
+ *   simaps_grid_path    <- GridGraph(grid).shortest_path(source, target) (shortest_paths.pyx:121-154),
+ *                          batched, exact SPFA parents.
  *   simaps_sp_distance  <- OccupancyMap.shortest_path_distance (envs.py:2507-2512), i.e. the reward
  *                          lookup Mapper.distance_to_receptacle (envs.py:2190-2194) used by the
  *                          partial rewards (envs.py:1083-1088, 1211-1216, 1332-1336), batched.
@@ -36,13 +38,25 @@
 extern "C" {
 #endif
 
-#define SIMAPS_ABI_VERSION 2
+#define SIMAPS_ABI_VERSION 3
 
 /* error codes */
 #define SIMAPS_OK 0
 #define SIMAPS_EINVAL -1      /* bad argument / shape / flag combination */
 #define SIMAPS_EUNSUPPORTED -2 /* valid for the reference but outside this build's limits */
 #define SIMAPS_EHIP -3        /* HIP runtime error (launch / memory) */
+#define SIMAPS_EDEVICE -4     /* an earlier launch reported a device-side fault (simaps_fault_status) */
+
+/* Device-side fault bits (simaps_fault_status).  Every kernel of this library ORs them into one
+ * process-wide host-mapped word when a workgroup hits a condition that makes its output invalid;
+ * never set in a correct run.  The next simaps_get_state / simaps_sp_distance /
+ * simaps_shortest_path / simaps_sssp_grid call returns SIMAPS_EDEVICE (and clears the word) if it
+ * is set, so a fault surfaces even when no debug buffers were passed. */
+#define SIMAPS_FAULT_TIMEOUT 1u    /* a wave-group barrier or scratch hand-over gave up waiting (~0.1 s) */
+#define SIMAPS_FAULT_ROUNDS 2u     /* the SSSP round cap was hit (no convergence) */
+#define SIMAPS_FAULT_DESCRIPTOR 4u /* a descriptor field outside this build's limits was clamped: num_robots
+                                      > SIMAPS_MAX_ROBOTS, robot index >= num_robots, or a used intention /
+                                      history path longer than SIMAPS_MAX_PATH points */
 
 /* robot classes (envs.py: LiftingRobot 1169, PushingRobot 1059, ThrowingRobot 1279, RescueRobot 1346) */
 #define SIMAPS_LIFTING 0
@@ -139,11 +153,17 @@ typedef struct simaps_debug {
     int32_t *sources;  /* [N, 2, 4]: (pi, pj, snapped_i, snapped_j) for receptacle / robot sources */
     float *dist;       /* [N, 2, room_h, room_w] raw GridGraph.shortest_path_image (-1 unreachable) */
     int32_t *status;   /* [N] bit0: no free cell (sp channels undefined in the reference); bit1: SSSP
-                        round cap hit (bug guard); bits 8+: SSSP rounds to convergence */
+                        round cap hit (bug guard); bit2: barrier timeout; bit3: descriptor clamped;
+                        bits 8+: SSSP rounds to convergence */
 } simaps_debug;
 
 int simaps_abi_version(void);
 const char *simaps_last_error(void);
+
+/* The device-side fault word (SIMAPS_FAULT_* bits) as of the launches that have completed: call
+ * after synchronising the stream to cover a given launch.  clear != 0 resets it.  Returns the bits
+ * (>= 0) or SIMAPS_EHIP if the host-mapped word could not be allocated. */
+int simaps_fault_status(int clear);
 
 /* Number of channels C of the stack for an env with `num_robots` robots (envs.py:2071-2113). */
 int simaps_num_channels(const simaps_config *cfg, int num_robots);
@@ -200,6 +220,17 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
  *   and ww <= SIMAPS_MAX_ROOM_W (cells outside the window are treated as blocked). */
 int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *sources, float *dists,
                      int wi0, int wj0, int wh, int ww, void *stream);
+
+/* Batched GridGraph(grid).shortest_path(source, target) (shortest_paths.pyx:121-154) on raw cells:
+ *   grids [B, H, W] uint8 (nonzero = free), sources / targets [B, 2] int32 (row, col); out_ij
+ *   [B][max_points][2] int32 waypoint cells (source first, like pyx:152's reversed list), out_count
+ *   [B] = number of waypoints, or -needed if max_points is too small.  All DEVICE.  The SPFA replays
+ *   pyx:69-114 (edge order, SLF swap), so parents -- and waypoints -- are the reference's; the
+ *   line-of-sight pruning counts cells with grid != 1 as blocked (uint8 `1 - grid`, pyx:146).  The
+ *   window rule of simaps_sssp_grid applies.  An unreachable target gives [target] (pyx:136-137). */
+int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *sources, const int32_t *targets,
+                     int wi0, int wj0, int wh, int ww, int max_points, int32_t *out_ij, int32_t *out_count,
+                     void *stream);
 
 #ifdef __cplusplus
 }

@@ -170,7 +170,12 @@ struct Group {
                 unsigned spins = 0;
                 while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == g) {
                     __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 22)) {  // ~0.1 s: never in a correct run; flag and fall through
+#ifdef SIMAPS_DIAG_FLAG_TIMEOUT  // diagnostic build (tests/test_gpu_faults.py): raise the timeout
+                    // flag at its real site on the first spin but keep waiting, so the output stays valid
+                    if (spins == 0) __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+                    if (++spins > (1u << 22)) {  // ~0.1 s: never in a correct run; flag (-> the fault
+                        // word, SIMAPS_FAULT_TIMEOUT, at the kernel's end) and fall through
                         __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         break;
                     }
@@ -182,6 +187,27 @@ struct Group {
 };
 
 __device__ __forceinline__ Group whole_wg() { return Group{(int)threadIdx.x, 1024, nullptr, 16}; }
+
+constexpr int SIMAPS_NFAULT = 3;  // SIMAPS_FAULT_* bits
+
+// Always-on fault reporting (include/simaps.h SIMAPS_FAULT_*): one thread per workgroup, after the
+// kernel's last LDS barrier, ORs the conditions that invalidate its output into the process-wide
+// host-mapped fault word.  `desc` holds SIMAPS_FAULT_DESCRIPTOR if a descriptor was clamped.
+__device__ __forceinline__ unsigned group_faults(const unsigned (&bar)[4][4], int rounds, int nsrc)
+{
+    unsigned f = (bar[0][2] | bar[1][2] | bar[2][2] | bar[3][2]) ? SIMAPS_FAULT_TIMEOUT : 0u;
+    if (nsrc > 0 && rounds >= (1 << 20)) f |= SIMAPS_FAULT_ROUNDS;
+    return f | (bar[0][3] ? SIMAPS_FAULT_DESCRIPTOR : 0u);
+}
+__device__ __forceinline__ void post_faults(unsigned *fault, unsigned f)
+{
+    // fault[k] = 1 for bit k: plain system-scope vector stores into fine-grained host memory (no
+    // PCIe atomics needed; concurrent writers store the same value); only in a faulting workgroup,
+    // i.e. never in a correct run
+    if (fault)
+        for (int k = 0; k < SIMAPS_NFAULT; k++)
+            if (f & (1u << k)) __hip_atomic_store(fault + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // ------------------------------------------------------------------------------------------------
 // LDS layout
@@ -1486,7 +1512,7 @@ __device__ __forceinline__ void wait_scratch(Shared &sh)
         unsigned spins = 0;
         while (!__hip_atomic_load(&sh.scratch_free, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 22)) {  // never in a correct run: flag (status bit 4) and fall through
+            if (++spins > (1u << 22)) {  // never in a correct run: flag (SIMAPS_FAULT_TIMEOUT) and fall through
                 __hip_atomic_store(&sh.bar[1][2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 break;
             }
@@ -2004,7 +2030,7 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
 __global__ void __launch_bounds__(NT) get_state_kernel(
     simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents, const simaps_env *__restrict__ envs,
     const simaps_robot *__restrict__ robots, const double *__restrict__ paths, const uint8_t *__restrict__ occupancy,
-    const float *__restrict__ overhead, float *__restrict__ state, int C, simaps_debug dbg)
+    const float *__restrict__ overhead, float *__restrict__ state, int C, simaps_debug dbg, unsigned *fault)
 {
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     Shared &sh = *reinterpret_cast<Shared *>(smem);
@@ -2020,7 +2046,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     for (int rep = 0; rep < SIMAPS_REPEAT + (int)(n >> 30); rep++) {
     lds_barrier();
 #endif
-    const simaps_agent ag = agents[n];
+    simaps_agent ag = agents[n];
     // Sources of the shortest-path maps (envs.py:2071-2113 order): receptacle, then the robot.
     const int nsrc = (cfg.use_shortest_path_to_receptacle_map ? 1 : 0) + (cfg.use_shortest_path_map ? 1 : 0);
     // Two tracks run concurrently from the start: waves [0, cs_waves) build the cspace, snap the
@@ -2038,8 +2064,15 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
                             tail_cells_off(cfg.room_h, cfg.room_w) + LW * LW * 2 <= DIST_FLOATS * 4;
     if (tid < 16) (&sh.bar[0][0])[tid] = 0u;
     if (tid == 16) sh.scratch_free = cs_waves == 0;
-    const simaps_env ev = envs[ag.env];
+    simaps_env ev = envs[ag.env];
+    // descriptors come through the C ABI unchecked: clamp what would index past the LDS tables
+    // (robot records, segment slots) and report it (SIMAPS_FAULT_DESCRIPTOR)
+    const bool bad_desc = (unsigned)(ev.num_robots - 1) >= (unsigned)SIMAPS_MAX_ROBOTS ||
+                          (unsigned)ag.robot >= (unsigned)ev.num_robots;
+    ev.num_robots = min(max(ev.num_robots, 1), SIMAPS_MAX_ROBOTS);
+    if ((unsigned)ag.robot >= (unsigned)ev.num_robots) ag.robot = 0;
     lds_barrier();  // the group barriers are zeroed
+    if (tid == 0 && bad_desc) sh.bar[0][3] = 1u;
     if (tid == 0) STAMP_NB(0);
     float *out = state + (size_t)n * LW * LW * C;
     const RenderCtx rc{cfg, sh, out, C, n};
@@ -2076,6 +2109,9 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             const int k = t - 128;
             const simaps_robot &r = rb[k];
             RobotP &P = sh.rob[k];
+            if ((cfg.use_intention_map && r.intention_len > SIMAPS_MAX_PATH) ||
+                (cfg.use_history_map && r.history_len > SIMAPS_MAX_PATH))  // cut to SIMAPS_MAX_PATH points
+                __hip_atomic_store(&sh.bar[0][3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const Rot R = rot_params(LW, r.heading * RAD_TO_DEG - 90.0);
             P.c = R.c; P.s = R.s; P.f0 = R.f0; P.f1 = R.f1; P.S0 = R.S0; P.S1 = R.S1;
             int pi, pj;
@@ -2224,12 +2260,15 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             else { o[0] = o[1] = o[2] = o[3] = -1; }
         }
     }
-    if (dbg.status && tid == 0) {
-        int st = 0;
-        for (int s = 0; s < nsrc; s++) st |= sh.src_ok[s] ? 0 : 1;
-        if (nsrc > 0 && sh.rounds >= (1 << 20)) st |= 2;
-        if (sh.bar[0][2] | sh.bar[1][2] | sh.bar[2][2] | sh.bar[3][2]) st |= 4;
-        dbg.status[n] = st | ((nsrc > 0 ? sh.rounds & 0xfffff : 0) << 8);
+    if (tid == 0) {
+        const unsigned f = group_faults(sh.bar, sh.rounds, nsrc);
+        post_faults(fault, f);
+        if (dbg.status) {
+            int st = (f & SIMAPS_FAULT_ROUNDS ? 2 : 0) | (f & SIMAPS_FAULT_TIMEOUT ? 4 : 0) |
+                     (f & SIMAPS_FAULT_DESCRIPTOR ? 8 : 0);
+            for (int s = 0; s < nsrc; s++) st |= sh.src_ok[s] ? 0 : 1;
+            dbg.status[n] = st | ((nsrc > 0 ? sh.rounds & 0xfffff : 0) << 8);
+        }
     }
 #ifdef SIMAPS_PHASE_STAMPS
     if (tid == 0 && blockIdx.x < MAX_STAMP_WG) g_stamps[blockIdx.x * NSTAMP + 10] = (unsigned long long)sh.rounds;
@@ -2244,7 +2283,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(NT) sssp_grid_kernel(int H, int W, const uint8_t *__restrict__ grids,
                                                       const int32_t *__restrict__ sources, float *__restrict__ out,
-                                                      int wi0, int wj0, int wh, int ww)
+                                                      int wi0, int wj0, int wh, int ww, unsigned *fault)
 {
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     Shared &sh = *reinterpret_cast<Shared *>(smem);
@@ -2267,6 +2306,7 @@ __global__ void __launch_bounds__(NT) sssp_grid_kernel(int H, int W, const uint8
     }
     lds_barrier();
     sssp(sh, S, dist, 1);
+    if (tid == 0) post_faults(fault, group_faults(sh.bar, sh.rounds, 1));
     // A blocked source has no edges but still dist 0 (pyx:84-88 set dists[source] before the loop).
     const int src_k = sh.src_s[0][0] * W + sh.src_s[0][1];
     for (int k = tid; k < H * W; k += NT) {
@@ -2291,7 +2331,7 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
                                                          const uint8_t *__restrict__ occupancy,
                                                          const double *__restrict__ sources,
                                                          const double *__restrict__ targets, int Q,
-                                                         double *__restrict__ out)
+                                                         double *__restrict__ out, unsigned *fault)
 {
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     Shared &sh = *reinterpret_cast<Shared *>(smem);
@@ -2318,6 +2358,7 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
     snap_sources(sh, S, 1, whole_wg());
     const bool src_ok = sh.src_ok[0];
     sssp(sh, S, dist, 1);  // the source's distance image (GridGraph._spfa_with_cache, pyx:116-119)
+    if (tid == 0) post_faults(fault, group_faults(sh.bar, sh.rounds, 1));
     const int pw = sssp_pitch(sh.w);
     for (int q0 = 0; q0 < Q; q0 += 2) {  // targets snapped two at a time (snap_sources' slots)
         const int nq = Q - q0 < 2 ? Q - q0 : 2;
@@ -2381,8 +2422,18 @@ __device__ __forceinline__ bool thin_free(const Shared &sh, const SsspScratch &S
 }
 
 // wave-parallel: is every pixel of line (r0, c0) -> (r1, c1) free (thin ? cspace_thin : cspace)?
+// grid == 1 bits of a raw GridGraph grid (grid_path_kernel; kept in the unused dilation table):
+// the line-of-sight test of pyx:146 counts (1 - grid[rr, cc]) != 0 in uint8, i.e. any cell != 1
+__device__ __forceinline__ bool one_free(const Shared &sh, const SsspScratch &S, int i, int j)
+{
+    const int r = i - sh.i0, c = j - sh.j0;
+    return r >= 0 && r < sh.h && c >= 0 && c < sh.w && b_test(S.dtab[0][r], c);
+}
+
+enum LineMask { LINE_CSPACE = 0, LINE_THIN = 1, LINE_GRID_ONE = 2 };
+
 __device__ __forceinline__ bool line_free(const Shared &sh, const SsspScratch &S, int r0, int c0, int r1, int c1,
-                                          bool thin)
+                                          int mask)
 {
     const int lane = threadIdx.x & 63;
     const int n = max(abs(r1 - r0), abs(c1 - c0)) + 1;
@@ -2390,66 +2441,33 @@ __device__ __forceinline__ bool line_free(const Shared &sh, const SsspScratch &S
     for (int t = lane; t < n; t += 64) {
         int pr, pc;
         line_pixel(r0, c0, r1, c1, t, pr, pc);
-        blocked |= thin ? !thin_free(sh, S, pr, pc) : !cs_free(sh, S, pr, pc);
+        blocked |= mask == LINE_THIN ? !thin_free(sh, S, pr, pc)
+                   : mask == LINE_GRID_ONE ? !one_free(sh, S, pr, pc) : !cs_free(sh, S, pr, pc);
     }
     return __ballot(blocked) == 0;
 }
 
 constexpr int PATH_MAX_PTS = 64;
 
-__global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents,
-                                                  const simaps_env *__restrict__ envs,
-                                                  const simaps_robot *__restrict__ robots,
-                                                  const uint8_t *__restrict__ occupancy,
-                                                  const double *__restrict__ sources, const double *__restrict__ targets,
-                                                  int max_pts, double *__restrict__ out_xy, int *__restrict__ out_n)
+// Steps (3)-(6) of the movement path on the LDS-resident free bits (S.freeb) between the cells
+// sh.src_s[0] (source) and sh.src_s[1] (target), both inside the window: the exact SPFA (run_spfa:
+// the source is a free cell of the window; otherwise only the source is reached), the parent walk,
+// approximate_polygon and the line-of-sight pruning on `line_mask`.  Leaves the kept waypoints in
+// outp[0, cnt) (packed (row << 16) | col, target first, i.e. before pyx:152's reversal) and returns
+// cnt in wave 0.  All threads call it.
+__device__ int path_core(Shared &sh, SsspScratch &S, char *smem, int H, int W, bool run_spfa, int line_mask)
 {
-    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-    Shared &sh = *reinterpret_cast<Shared *>(smem);
-    float *dist = reinterpret_cast<float *>(smem + OFF_DIST);
-    int *parent = reinterpret_cast<int *>(smem + OFF_DIST) + DIST_FLOATS;
-    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
-    int *queue = reinterpret_cast<int *>(smem + OFF_UNION + align16((int)sizeof(SsspScratch)));
     static_assert(align16((int)sizeof(SsspScratch)) + DIST_FLOATS * 5 <= UNION_BYTES, "SPFA queue + flags fit the union");
-    uint8_t *inq = reinterpret_cast<uint8_t *>(queue + DIST_FLOATS);  // later: chain flags
-    int *dense = queue;  // after the SPFA: the dense path
     // after the parent walk the distance + parent arrays are free: the Douglas-Peucker stack
     // (<= 2 * points ints), then the sparse points and the kept waypoints
+    float *dist = reinterpret_cast<float *>(smem + OFF_DIST);
+    int *parent = reinterpret_cast<int *>(smem + OFF_DIST) + DIST_FLOATS;
+    int *queue = reinterpret_cast<int *>(smem + OFF_UNION + align16((int)sizeof(SsspScratch)));
+    uint8_t *inq = reinterpret_cast<uint8_t *>(queue + DIST_FLOATS);  // later: chain flags
+    int *dense = queue;  // after the SPFA: the dense path
     int *stack = reinterpret_cast<int *>(smem + OFF_DIST);
     int *sparse = stack, *outp = stack + DIST_FLOATS;
-    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const int H = cfg.H, W = cfg.W;
-    const simaps_agent ag = agents[n];
-    OccLoad<NT> occ_regs;
-    cspace_load<NT>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
-                    cfg.room_w, tid);
-    const double sx = sources[2 * n], sy = sources[2 * n + 1], tx = targets[2 * n], ty = targets[2 * n + 1];
-    if (tid == 0) {
-        const simaps_env ev = envs[ag.env];
-        sh.h = cfg.room_h;
-        sh.w = cfg.room_w;
-        sh.i0 = cfg.room_i0;
-        sh.j0 = cfg.room_j0;
-        sh.r = geo.cspace_r[robots[ev.robot_off + ag.robot].type];
-        pos_to_pix(sx, sy, H, W, sh.src_q[0][0], sh.src_q[0][1]);
-        pos_to_pix(tx, ty, H, W, sh.src_q[1][0], sh.src_q[1][1]);
-        sh.nsrc = 2;
-    }
-    lds_barrier();
-    build_cspace<NT>(S, occ_regs, sh.h, sh.w, sh.r, whole_wg());
-    double *o = out_xy + (size_t)n * max_pts * 2;
-    // (1) straight line on cspace_thin between the unsnapped pixels (envs.py:2484-2486)
-    if (tid < 64) {
-        const bool straight = line_free(sh, S, sh.src_q[0][0], sh.src_q[0][1], sh.src_q[1][0], sh.src_q[1][1], true);
-        if (lane == 0) sh.flag[0] = straight;
-    }
-    lds_barrier();
-    if (sh.flag[0]) {
-        if (tid == 0) { o[0] = sx; o[1] = sy; o[2] = tx; o[3] = ty; out_n[n] = 2; }
-        return;
-    }
-    // (2) snap both ends (envs.py:2489-2490)
-    snap_sources(sh, S, 2, whole_wg());
+    const int tid = threadIdx.x, lane = tid & 63;
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w), cells = (h + 2) * pw;
     // (3) GridGraph._spfa (pyx:69-114) from the snapped source, exactly: one wave, the 8 out-edges of
     // a popped vertex evaluated by lanes 0..7 (distinct heads, so in parallel), then the pushes and
@@ -2457,7 +2475,7 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
     const float INFR = (float)(2 * H * W);
     for (int k = tid; k < cells; k += NT) { dist[k] = INFR; parent[k] = -1; inq[k] = 0; }
     lds_barrier();
-    const bool src_ok = sh.src_ok[0] && sh.src_ok[1];
+    const bool src_ok = run_spfa;
     const int su = (sh.src_s[0][0] - sh.i0 + 1) * pw + (sh.src_s[0][1] - sh.j0 + 1);
     const int tv = (sh.src_s[1][0] - sh.i0 + 1) * pw + (sh.src_s[1][1] - sh.j0 + 1);
     if (tid < 64 && src_ok) {
@@ -2579,7 +2597,7 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
             cnt = 1;
             for (int k = 1; k < m - 1; k++) {
                 const int a = outp[cnt - 1], b2 = sparse[k + 1];
-                if (!line_free(sh, S, a >> 16, a & 0xffff, b2 >> 16, b2 & 0xffff, false)) {
+                if (!line_free(sh, S, a >> 16, a & 0xffff, b2 >> 16, b2 & 0xffff, line_mask)) {
                     if (lane == 0) outp[cnt] = sparse[k];
                     cnt++;
                 }
@@ -2589,6 +2607,57 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
                 cnt++;
             }
         }
+        return cnt;
+    }
+    return 0;
+}
+
+__global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents,
+                                                  const simaps_env *__restrict__ envs,
+                                                  const simaps_robot *__restrict__ robots,
+                                                  const uint8_t *__restrict__ occupancy,
+                                                  const double *__restrict__ sources, const double *__restrict__ targets,
+                                                  int max_pts, double *__restrict__ out_xy, int *__restrict__ out_n)
+{
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    Shared &sh = *reinterpret_cast<Shared *>(smem);
+    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
+    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int H = cfg.H, W = cfg.W;
+    const simaps_agent ag = agents[n];
+    OccLoad<NT> occ_regs;
+    cspace_load<NT>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
+                    cfg.room_w, tid);
+    const double sx = sources[2 * n], sy = sources[2 * n + 1], tx = targets[2 * n], ty = targets[2 * n + 1];
+    if (tid == 0) {
+        const simaps_env ev = envs[ag.env];
+        sh.h = cfg.room_h;
+        sh.w = cfg.room_w;
+        sh.i0 = cfg.room_i0;
+        sh.j0 = cfg.room_j0;
+        sh.r = geo.cspace_r[robots[ev.robot_off + ag.robot].type];
+        pos_to_pix(sx, sy, H, W, sh.src_q[0][0], sh.src_q[0][1]);
+        pos_to_pix(tx, ty, H, W, sh.src_q[1][0], sh.src_q[1][1]);
+        sh.nsrc = 2;
+    }
+    lds_barrier();
+    build_cspace<NT>(S, occ_regs, sh.h, sh.w, sh.r, whole_wg());
+    double *o = out_xy + (size_t)n * max_pts * 2;
+    // (1) straight line on cspace_thin between the unsnapped pixels (envs.py:2484-2486)
+    if (tid < 64) {
+        const bool straight = line_free(sh, S, sh.src_q[0][0], sh.src_q[0][1], sh.src_q[1][0], sh.src_q[1][1], LINE_THIN);
+        if (lane == 0) sh.flag[0] = straight;
+    }
+    lds_barrier();
+    if (sh.flag[0]) {
+        if (tid == 0) { o[0] = sx; o[1] = sy; o[2] = tx; o[3] = ty; out_n[n] = 2; }
+        return;
+    }
+    // (2) snap both ends (envs.py:2489-2490)
+    snap_sources(sh, S, 2, whole_wg());
+    const int cnt = path_core(sh, S, smem, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE);
+    int *outp = reinterpret_cast<int *>(smem + OFF_DIST) + DIST_FLOATS;
+    if (tid < 64) {
         // (7) positions (envs.py:2494-2503); path[0] / path[-1] replaced by the given positions
         if (cnt < 2) {
             if (lane == 0) { o[0] = sx; o[1] = sy; o[2] = tx; o[3] = ty; out_n[n] = 2; }
@@ -2604,6 +2673,64 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
                 o[2 * k + 1] = y;
             }
             if (lane == 0) out_n[n] = cnt;
+        }
+    }
+}
+
+// GridGraph(grid).shortest_path(source, target) (shortest_paths.pyx:121-154) on raw grid cells, one
+// workgroup per (grid, source, target): the same exact SPFA / parent walk / approximate_polygon as
+// path_kernel, without the cspace, snap and straight-line steps of OccupancyMap.shortest_path, the
+// line-of-sight pruning on the grid itself, and the waypoints returned as cells (target last).
+__global__ void __launch_bounds__(NT) grid_path_kernel(int H, int W, const uint8_t *__restrict__ grids,
+                                                       const int32_t *__restrict__ sources,
+                                                       const int32_t *__restrict__ targets, int wi0, int wj0, int wh,
+                                                       int ww, int max_pts, int32_t *__restrict__ out_ij,
+                                                       int32_t *__restrict__ out_n)
+{
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    Shared &sh = *reinterpret_cast<Shared *>(smem);
+    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint8_t *grid = grids + (size_t)b * H * W;
+    const int si = sources[2 * b], sj = sources[2 * b + 1], ti = targets[2 * b], tj = targets[2 * b + 1];
+    if (tid == 0) {
+        sh.h = wh; sh.w = ww; sh.i0 = wi0; sh.j0 = wj0;
+        const bool s_in = si >= wi0 && si < wi0 + wh && sj >= wj0 && sj < wj0 + ww;
+        const bool t_in = ti >= wi0 && ti < wi0 + wh && tj >= wj0 && tj < wj0 + ww;
+        // a source outside the window or blocked has no edges (pyx:56), and a target outside the
+        // window is never reached: the parent walk stops at once and the path is [target]
+        sh.flag[0] = s_in && t_in && grid[(size_t)si * W + sj] != 0;
+        sh.src_s[0][0] = si; sh.src_s[0][1] = sj; sh.src_s[1][0] = ti; sh.src_s[1][1] = tj;
+    }
+    // free bits (grid != 0: the SPFA's vertices, pyx:47-56) and grid == 1 bits (line of sight)
+    const int nwords = (ww + 63) >> 6;
+    for (int item = wave; item < wh * 2; item += NT / 64) {
+        const int rr = item >> 1, wd = item & 1, c = wd * 64 + lane;
+        const uint8_t v = (wd < nwords && c < ww) ? grid[(size_t)(wi0 + rr) * W + wj0 + c] : (uint8_t)0;
+        const uint64_t mf = __ballot(v != 0), m1 = __ballot(v == 1);
+        if (lane == 0) {
+            if (wd == 0) { S.freeb[rr].lo = mf; S.dtab[0][rr].lo = m1; }
+            else { S.freeb[rr].hi = mf; S.dtab[0][rr].hi = m1; }
+        }
+    }
+    lds_barrier();
+    int32_t *o = out_ij + (size_t)b * max_pts * 2;
+    if (!sh.flag[0]) {
+        if (tid == 0) { o[0] = ti; o[1] = tj; out_n[b] = 1; }
+        return;
+    }
+    const int cnt = path_core(sh, S, smem, H, W, true, LINE_GRID_ONE);
+    const int *outp = reinterpret_cast<const int *>(smem + OFF_DIST) + DIST_FLOATS;
+    if (tid < 64) {
+        if (cnt > max_pts) {
+            if (lane == 0) out_n[b] = -cnt;  // caller's buffer too small
+        } else {
+            for (int k = lane; k < cnt; k += 64) {  // reversed (pyx:152): source first
+                const int pv = outp[cnt - 1 - k];
+                o[2 * k] = pv >> 16;
+                o[2 * k + 1] = pv & 0xffff;
+            }
+            if (lane == 0) out_n[b] = cnt;
         }
     }
 }
@@ -2733,6 +2860,7 @@ __global__ void __launch_bounds__(NT) ingest_kernel(simaps_config cfg, simaps_ca
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 
 namespace {
 thread_local char g_err[512] = "";
@@ -2744,6 +2872,51 @@ int fail(int code, const char *fmt, ...)
     vsnprintf(g_err, sizeof(g_err), fmt, ap);
     va_end(ap);
     return code;
+}
+
+// The process-wide device fault word (include/simaps.h SIMAPS_FAULT_*): SIMAPS_NFAULT flags in
+// fine-grained (coherent) host memory that every device can write without a copy, read by the next
+// compute call without synchronising.  Allocated on first use; never freed (process lifetime).
+std::once_flag g_fault_once;
+volatile unsigned *g_fault_host = nullptr;
+unsigned *g_fault_dev = nullptr;
+
+unsigned *fault_word()
+{
+    std::call_once(g_fault_once, [] {
+        void *h = nullptr;
+        if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
+            return;
+        memset(h, 0, 64);
+        void *d = nullptr;
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return;
+        g_fault_host = static_cast<volatile unsigned *>(h);
+        g_fault_dev = static_cast<unsigned *>(d);
+    });
+    return g_fault_dev;
+}
+
+unsigned read_faults(bool clear)
+{
+    unsigned f = 0;
+    if (!g_fault_host) return 0;
+    for (int k = 0; k < SIMAPS_NFAULT; k++)
+        if (g_fault_host[k]) {
+            f |= 1u << k;
+            if (clear) g_fault_host[k] = 0;
+        }
+    return f;
+}
+
+// Entry check of every compute call: a fault posted by an earlier launch fails this call (once).
+int pending_faults()
+{
+    if (!fault_word()) return fail(SIMAPS_EHIP, "could not allocate the host-mapped fault word");
+    const unsigned f = read_faults(true);
+    if (!f) return 0;
+    return fail(SIMAPS_EDEVICE, "an earlier launch reported device fault bits 0x%x (%s%s%s): its outputs are invalid", f,
+                f & SIMAPS_FAULT_TIMEOUT ? "barrier timeout " : "", f & SIMAPS_FAULT_ROUNDS ? "SSSP round cap " : "",
+                f & SIMAPS_FAULT_DESCRIPTOR ? "descriptor clamped" : "");
 }
 
 // Robot geometry with the reference's own expressions (envs.py:802-810, 1060, 1280, 2218-2242, 2421).
@@ -2817,6 +2990,12 @@ int simaps_debug_read_stamps(unsigned long long *host_out)
 
 const char *simaps_last_error(void) { return g_err; }
 
+int simaps_fault_status(int clear)
+{
+    if (!fault_word()) return fail(SIMAPS_EHIP, "could not allocate the host-mapped fault word");
+    return (int)read_faults(clear != 0);
+}
+
 int simaps_num_channels(const simaps_config *c, int num_robots)
 {
     if (!c) return fail(SIMAPS_EINVAL, "cfg is NULL");
@@ -2852,11 +3031,12 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
     if (cfg->use_intention_channels && (num_robots_per_env < 1 || num_robots_per_env > SIMAPS_MAX_ROBOTS))
         return fail(SIMAPS_EINVAL, "intention channels need num_robots_per_env in [1, %d]", SIMAPS_MAX_ROBOTS);
     const int C = simaps_num_channels(cfg, num_robots_per_env > 0 ? num_robots_per_env : 1);
+    if ((rc = pending_faults())) return rc;
     simaps_debug d;
     memset(&d, 0, sizeof(d));
     if (dbg) d = *dbg;
     hipLaunchKernelGGL(get_state_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, geo, agents, envs,
-                       robots, paths, occupancy, overhead, state, C, d);
+                       robots, paths, occupancy, overhead, state, C, d, g_fault_dev);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "get_state launch: %s", hipGetErrorString(e));
     return 0;
@@ -2872,9 +3052,10 @@ int simaps_sp_distance(const simaps_config *cfg, int N, const simaps_agent *agen
     if (N == 0 || Q == 0) return 0;
     if (!agents || !envs || !robots || !occupancy || !sources || !targets || !out)
         return fail(SIMAPS_EINVAL, "NULL buffer");
+    if ((rc = pending_faults())) return rc;
     const Geometry geo = make_geometry();
     hipLaunchKernelGGL(sp_distance_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, geo, agents, envs, robots,
-                       occupancy, sources, targets, Q, out);
+                       occupancy, sources, targets, Q, out, g_fault_dev);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "sp_distance launch: %s", hipGetErrorString(e));
     return 0;
@@ -2890,6 +3071,7 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
     if (N == 0) return 0;
     if (!agents || !envs || !robots || !occupancy || !sources || !targets || !out_xy || !out_count)
         return fail(SIMAPS_EINVAL, "NULL buffer");
+    if ((rc = pending_faults())) return rc;
     const Geometry geo = make_geometry();
     hipLaunchKernelGGL(path_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, geo, agents, envs, robots,
                        occupancy, sources, targets, max_points, out_xy, out_count);
@@ -2910,10 +3092,30 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
     if (N == 0) return 0;
     if (!agents || !seg_ids || !cam_params || !depth || !seg_raw || !overhead || !occupancy || !keys)
         return fail(SIMAPS_EINVAL, "NULL buffer");
+    if ((rc = pending_faults())) return rc;
     hipLaunchKernelGGL(ingest_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids, cam_params,
                        depth, seg_raw, overhead, occupancy, reinterpret_cast<unsigned long long *>(keys));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "ingest launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *sources, const int32_t *targets,
+                     int wi0, int wj0, int wh, int ww, int max_points, int32_t *out_ij, int32_t *out_count, void *stream)
+{
+    if (B < 0 || H <= 0 || W <= 0 || max_points < 1) return fail(SIMAPS_EINVAL, "bad batch / grid shape / max_points");
+    if (H > 32767 || W > 32767) return fail(SIMAPS_EINVAL, "grid %dx%d too large", H, W);
+    if (B == 0) return 0;
+    if (!grids || !sources || !targets || !out_ij || !out_count) return fail(SIMAPS_EINVAL, "NULL buffer");
+    if (wh <= 0 || ww <= 0 || wi0 < 0 || wj0 < 0 || wi0 + wh > H || wj0 + ww > W)
+        return fail(SIMAPS_EINVAL, "window outside the grid");
+    if (ww > SIMAPS_MAX_ROOM_W || wh > MAX_ROWS || (wh + 2) * ((ww + 2) | 1) > SIMAPS_MAX_ROOM_CELLS)
+        return fail(SIMAPS_EUNSUPPORTED, "window %dx%d exceeds the LDS-resident limit", wh, ww);
+    if (const int rc = pending_faults()) return rc;
+    hipLaunchKernelGGL(grid_path_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, H, W, grids, sources, targets, wi0,
+                       wj0, wh, ww, max_points, out_ij, out_count);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "grid_path launch: %s", hipGetErrorString(e));
     return 0;
 }
 
@@ -2927,8 +3129,9 @@ int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *s
         return fail(SIMAPS_EINVAL, "window outside the grid");
     if (ww > SIMAPS_MAX_ROOM_W || wh > MAX_ROWS || (wh + 2) * ((ww + 2) | 1) > SIMAPS_MAX_ROOM_CELLS)
         return fail(SIMAPS_EUNSUPPORTED, "window %dx%d exceeds the LDS-resident limit", wh, ww);
+    if (const int rc = pending_faults()) return rc;
     hipLaunchKernelGGL(sssp_grid_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, H, W, grids, sources, dists, wi0,
-                       wj0, wh, ww);
+                       wj0, wh, ww, g_fault_dev);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "sssp_grid launch: %s", hipGetErrorString(e));
     return 0;

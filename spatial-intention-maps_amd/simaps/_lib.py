@@ -27,7 +27,7 @@ ROBOT_DTYPE = np.dtype([('x', '<f8'), ('y', '<f8'), ('heading', '<f8'), ('target
                         ('history_len', '<i4')], align=True)
 ENV_DTYPE = np.dtype([('receptacle_x', '<f8'), ('receptacle_y', '<f8'), ('has_receptacle', '<i4'),
                       ('robot_off', '<i4'), ('num_robots', '<i4'), ('reserved', '<i4')], align=True)
-ABI_VERSION = 2  # include/simaps.h SIMAPS_ABI_VERSION
+ABI_VERSION = 3  # include/simaps.h SIMAPS_ABI_VERSION
 AGENT_DTYPE = np.dtype([('env', '<i4'), ('robot', '<i4'), ('map_slot', '<i4')], align=True)
 assert ROBOT_DTYPE.itemsize == 72 and ENV_DTYPE.itemsize == 32 and AGENT_DTYPE.itemsize == 12
 
@@ -61,11 +61,13 @@ class SimapsError(RuntimeError):
     pass
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
+def _load(path=LIB_PATH):
+    """Bind the C ABI of the library at `path` (the product libsimaps.so by default; tests also load
+    diagnostic builds of the same ABI through this)."""
+    if not os.path.exists(path):
         raise ImportError('libsimaps.so not found at %s -- build it with `make -C spatial-intention-maps_amd/csrc` '
-                          '(or __graft_entry__.build()); there is no CPU fallback' % LIB_PATH)
-    L = ctypes.CDLL(LIB_PATH)
+                          '(or __graft_entry__.build()); there is no CPU fallback' % path)
+    L = ctypes.CDLL(path)
     vp, i32 = ctypes.c_void_p, ctypes.c_int
     L.simaps_abi_version.restype = i32
     L.simaps_last_error.restype = ctypes.c_char_p
@@ -84,6 +86,10 @@ def _load():
     L.simaps_ingest.restype = i32
     L.simaps_sssp_grid.argtypes = [i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp]
     L.simaps_sssp_grid.restype = i32
+    L.simaps_grid_path.argtypes = [i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]
+    L.simaps_grid_path.restype = i32
+    L.simaps_fault_status.argtypes = [i32]
+    L.simaps_fault_status.restype = i32
     if L.simaps_abi_version() != ABI_VERSION:
         raise ImportError('libsimaps ABI version mismatch')
     return L
@@ -91,13 +97,37 @@ def _load():
 
 lib = _load()
 
-EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_num_channels', 'simaps_robot_mask',
-            'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest', 'simaps_sssp_grid')
+EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_fault_status', 'simaps_num_channels',
+            'simaps_robot_mask', 'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest',
+            'simaps_sssp_grid', 'simaps_grid_path')
+
+# error codes and device fault bits (include/simaps.h)
+EINVAL, EUNSUPPORTED, EHIP, EDEVICE = -1, -2, -3, -4
+FAULT_TIMEOUT, FAULT_ROUNDS, FAULT_DESCRIPTOR = 1, 2, 4
 
 
-def check(rc):
+class DeviceFault(SimapsError):
+    """A kernel reported SIMAPS_FAULT_* bits: the outputs of that launch are invalid."""
+
+
+def check(rc, L=None):
     if rc != 0:
-        raise SimapsError('libsimaps error %d: %s' % (rc, lib.simaps_last_error().decode()))
+        L = L or lib
+        cls = DeviceFault if rc == EDEVICE else SimapsError
+        raise cls('libsimaps error %d: %s' % (rc, L.simaps_last_error().decode()))
+
+
+def check_faults(L=None):
+    """Raise DeviceFault if a completed launch reported a device-side fault (clears the word).
+    Call after the stream has been synchronised (e.g. after a device->host copy of the results)."""
+    L = L or lib
+    f = L.simaps_fault_status(1)
+    if f < 0:
+        check(f, L)
+    if f:
+        raise DeviceFault('device fault bits 0x%x (%s): the outputs of a completed launch are invalid' % (
+            f, ' '.join(n for b, n in ((FAULT_TIMEOUT, 'barrier-timeout'), (FAULT_ROUNDS, 'sssp-round-cap'),
+                                       (FAULT_DESCRIPTOR, 'descriptor-clamped')) if f & b)))
 
 
 def stream_handle(stream=None):

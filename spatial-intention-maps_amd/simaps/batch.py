@@ -103,6 +103,25 @@ def _to_dev(a, device):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(device)
 
 
+def launch_stream(device, stream=None):
+    """(launch stream, current stream).  A kernel launched on a side stream first waits for the
+    current stream (where this module uploads its inputs and allocates its outputs)."""
+    cur = torch.cuda.current_stream(device)
+    s = cur if stream is None else stream
+    if s != cur:
+        s.wait_stream(cur)
+    return s, cur
+
+
+def hold(s, cur, *tensors):
+    """Keep tensors a launch on side stream `s` reads or writes alive (caching allocator) until `s`
+    has finished it.  Consumers on other streams must wait for `s` themselves (torch semantics)."""
+    if s != cur:
+        for t in tensors:
+            if t is not None:
+                t.record_stream(s)
+
+
 class StateBatch:
     """One configuration's batch of agent-state stacks, resident on `device`.
 
@@ -139,6 +158,7 @@ class StateBatch:
     def set_descriptors(self, scenes):
         """Upload a new per-step scene descriptor (poses, controller state, paths)."""
         robots, envs, ag, paths = pack_descriptors(scenes, self.agents)
+        self.scenes = scenes  # (ingest takes the camera pose from here)
         self.robots_d = _to_dev(robots, self.device)
         self.envs_d = _to_dev(envs, self.device)
         self.agents_d = _to_dev(ag, self.device)
@@ -200,7 +220,8 @@ class StateBatch:
 
     def render(self, out=None, debug=None, stream=None, slots=None):
         """Launch the fused kernel: the stacks of every agent (or of map slots `slots`, in that
-        order) into `out` (allocated if None)."""
+        order) into `out` (allocated if None).  Asynchronous on `stream` (default: the current
+        stream); with a side stream, wait for it before reading `out` on another stream."""
         agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
         if out is None:
             out = self.alloc_state(n)
@@ -216,11 +237,14 @@ class StateBatch:
                     raise ValueError('debug[%r] must be contiguous with leading dim %d on %s' % (k, n, self.device))
             dbg = _lib.Debug(*(debug[k].data_ptr() if debug.get(k) is not None else None
                                for k in ('cspace', 'sources', 'dist', 'status')))
+        s, cur = launch_stream(self.device, stream)
         _lib.check(_lib.lib.simaps_get_state(
             self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d),
             _lib.ptr(self.paths_d), _lib.ptr(self.occupancy), _lib.ptr(self.overhead), _lib.ptr(out),
             self.num_robots if self.flags['use_intention_channels'] else 0,
-            None if dbg is None else dbg, _lib.stream_handle(stream)))
+            None if dbg is None else dbg, _lib.stream_handle(s)))
+        hold(s, cur, out, agents_d, self.envs_d, self.robots_d, self.paths_d, self.occupancy, self.overhead,
+             *(debug.values() if debug else ()))
         return out
 
 
@@ -237,10 +261,11 @@ class StateBatch:
         out = torch.empty((n, Q), dtype=torch.float64, device=self.device)
         if n == 0 or Q == 0:
             return out
-        self._inflight = (src, tgt)  # alive until the next call (async launch)
+        s, cur = launch_stream(self.device, stream)
         _lib.check(_lib.lib.simaps_sp_distance(
             self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d), _lib.ptr(self.occupancy),
-            _lib.ptr(src), _lib.ptr(tgt), Q, _lib.ptr(out), _lib.stream_handle(stream)))
+            _lib.ptr(src), _lib.ptr(tgt), Q, _lib.ptr(out), _lib.stream_handle(s)))
+        hold(s, cur, src, tgt, out, agents_d, self.envs_d, self.robots_d, self.occupancy)
         return out
 
 
@@ -258,10 +283,15 @@ class StateBatch:
         cnt = torch.empty((n,), dtype=torch.int32, device=self.device)
         if n == 0:
             return []
+        s, cur = launch_stream(self.device, stream)
         _lib.check(_lib.lib.simaps_shortest_path(
             self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d), _lib.ptr(self.occupancy),
-            _lib.ptr(src), _lib.ptr(tgt), max_points, _lib.ptr(xy), _lib.ptr(cnt), _lib.stream_handle(stream)))
+            _lib.ptr(src), _lib.ptr(tgt), max_points, _lib.ptr(xy), _lib.ptr(cnt), _lib.stream_handle(s)))
+        hold(s, cur, src, tgt, xy, cnt, agents_d, self.envs_d, self.robots_d, self.occupancy)
+        if s != cur:
+            cur.wait_stream(s)
         xy, cnt = xy.cpu().numpy(), cnt.cpu().numpy()
+        _lib.check_faults()
         if (cnt < 0).any():
             raise RuntimeError('a path has %d waypoints > max_points=%d' % (-cnt.min(), max_points))
         return [[(float(x), float(y), 0) for x, y in xy[k, :cnt[k]]] for k in range(n)]
@@ -298,10 +328,11 @@ class StateBatch:
         if n == 0:
             return
         ids_d, params_d = _to_dev(ids, self.device), torch.from_numpy(params).to(self.device)
-        self._inflight = (ids_d, params_d, dep, seg)  # alive until the next call (async launch)
+        s, cur = launch_stream(self.device, stream)
         _lib.check(_lib.lib.simaps_ingest(
             self.cfg, cam, n, _lib.ptr(agents_d), _lib.ptr(ids_d), _lib.ptr(params_d), _lib.ptr(dep), _lib.ptr(seg),
-            _lib.ptr(self.overhead), _lib.ptr(self.occupancy), _lib.ptr(self._keys), _lib.stream_handle(stream)))
+            _lib.ptr(self.overhead), _lib.ptr(self.occupancy), _lib.ptr(self._keys), _lib.stream_handle(s)))
+        hold(s, cur, ids_d, params_d, dep, seg, agents_d, self.overhead, self.occupancy, self._keys)
 
 
 def sssp_grid(grids, sources, window=None, stream=None):
@@ -314,6 +345,39 @@ def sssp_grid(grids, sources, window=None, stream=None):
         window = (0, 0, H, W)
     out = torch.empty((B, H, W), dtype=torch.float32, device=grids.device)
     src = sources.to(device=grids.device, dtype=torch.int32).contiguous()
-    _lib.check(_lib.lib.simaps_sssp_grid(B, H, W, _lib.ptr(grids.contiguous()), _lib.ptr(src), _lib.ptr(out),
-                                         *[int(x) for x in window], _lib.stream_handle(stream)))
+    g = grids.contiguous()
+    s, cur = launch_stream(grids.device, stream)
+    _lib.check(_lib.lib.simaps_sssp_grid(B, H, W, _lib.ptr(g), _lib.ptr(src), _lib.ptr(out),
+                                         *[int(x) for x in window], _lib.stream_handle(s)))
+    hold(s, cur, g, src, out)
     return out
+
+
+def grid_paths(grids, sources, targets, window=None, max_points=256, stream=None):
+    """Batched GridGraph(grid).shortest_path(source, target) (pyx:121-154) on device.
+
+    grids: uint8 tensor [B, H, W] (device), sources / targets: int [B, 2] cells.  Returns B lists of
+    (row, col) waypoints, source first, exactly the reference's (same SPFA parents)."""
+    B, H, W = grids.shape
+    if window is None:
+        window = (0, 0, H, W)
+    src = torch.as_tensor(sources).to(device=grids.device, dtype=torch.int32).contiguous()
+    tgt = torch.as_tensor(targets).to(device=grids.device, dtype=torch.int32).contiguous()
+    if tuple(src.shape) != (B, 2) or tuple(tgt.shape) != (B, 2):
+        raise ValueError('sources and targets must be [%d, 2]' % B)
+    if B == 0:
+        return []
+    ij = torch.empty((B, max_points, 2), dtype=torch.int32, device=grids.device)
+    cnt = torch.empty((B,), dtype=torch.int32, device=grids.device)
+    g = grids.contiguous()
+    s, cur = launch_stream(grids.device, stream)
+    _lib.check(_lib.lib.simaps_grid_path(B, H, W, _lib.ptr(g), _lib.ptr(src), _lib.ptr(tgt), *[int(x) for x in window],
+                                         max_points, _lib.ptr(ij), _lib.ptr(cnt), _lib.stream_handle(s)))
+    hold(s, cur, g, src, tgt, ij, cnt)
+    if s != cur:
+        cur.wait_stream(s)
+    ij, cnt = ij.cpu().numpy(), cnt.cpu().numpy()
+    _lib.check_faults()
+    if (cnt < 0).any():
+        raise RuntimeError('a path has %d waypoints > max_points=%d' % (-cnt.min(), max_points))
+    return [[(int(i), int(j)) for i, j in ij[k, :cnt[k]]] for k in range(B)]

@@ -18,6 +18,7 @@ fallback: constructing either class without libsimaps.so / a GPU raises.
 import numpy as np
 import torch
 
+from . import _lib
 from . import batch as _batch
 
 
@@ -54,7 +55,6 @@ class VectorEnvObservations:
                                                    for s, o in zip(scenes, self.batch.scenes)):
                 raise ValueError('update() keeps the batch shape: same envs, same robots per env')
             self.batch.set_descriptors(scenes)
-            self.batch.scenes = scenes
         if occupancy is not None or overhead is not None:
             self.batch.set_maps(occupancy, overhead, slots)
 
@@ -73,7 +73,10 @@ class VectorEnvObservations:
                     want.append(self.slot[(e, a)])
         out = self.batch.as_hwc(self.batch.render(slots=want, stream=stream))
         if numpy:
+            if stream is not None:
+                torch.cuda.current_stream(self.batch.device).wait_stream(stream)
             out = out.cpu().numpy()
+            _lib.check_faults()  # the copy synchronised: a faulting launch raises here
         pos = {k: n for n, k in enumerate(want)}
         res = []
         for e in range(self.num_envs):
@@ -99,7 +102,14 @@ class VectorEnvObservations:
             src[k] = rec[:2]
             for q, p in enumerate(positions[e][a]):
                 tgt[k, q] = p[:2]
-        d = self.batch.shortest_path_distances(src, tgt[:, :Q], stream=stream).cpu().numpy() if Q else np.zeros((n, 0))
+        if Q:
+            d = self.batch.shortest_path_distances(src, tgt[:, :Q], stream=stream)
+            if stream is not None:
+                torch.cuda.current_stream(self.batch.device).wait_stream(stream)
+            d = d.cpu().numpy()
+            _lib.check_faults()
+        else:
+            d = np.zeros((n, 0))
         return [[[float(x) for x in d[self.slot[(e, a)], :len(positions[e][a])]] for a in range(len(positions[e]))]
                 for e in range(self.num_envs)]
 
@@ -147,7 +157,23 @@ class GridGraph:
 
     def shortest_path_image(self, source):
         """(H, W) float32 NumPy image of distances from `source` (pyx:165-167)."""
-        return self.shortest_path_images([source])[0].cpu().numpy()
+        img = self.shortest_path_images([source])[0].cpu().numpy()
+        _lib.check_faults()
+        return img
+
+    def shortest_path(self, source, target):
+        """Waypoint cells [(i, j), ...] from `source` to `target` (pyx:121-154): the SPFA parent
+        walk, approximate_polygon(tolerance=1) and line-of-sight pruning, source first."""
+        return self.shortest_paths([(source, target)])[0]
+
+    def shortest_paths(self, pairs, stream=None):
+        """Batched shortest_path over (source, target) cell pairs, one launch."""
+        pairs = [(self._check_source(s), self._check_source(t)) for s, t in pairs]
+        if not pairs:
+            return []
+        grids = self.grid.unsqueeze(0).expand(len(pairs), *self.shape).contiguous()
+        return _batch.grid_paths(grids, [p[0] for p in pairs], [p[1] for p in pairs], window=self.window,
+                                 max_points=max(256, self.shape[0] + self.shape[1]), stream=stream)
 
     def shortest_path_distance(self, source, target):
         """dists[target] from `source` as a Python float (pyx:156-163); -1 if unreachable."""

@@ -375,6 +375,49 @@ class _FakeCameraP(_FakeP):
         return w, h, None, db.copy(), raw.copy()
 
 
+def gen_grid_paths(sp):
+    """GridGraph(grid).shortest_path(source, target) (pyx:121-154) on raw cells: the reference demo
+    sample (random free / blocked pairs) and small random grids whose free cells take the values
+    1, 2 and 255 (the SPFA's vertices are grid != 0, but the line-of-sight pruning counts uint8
+    `1 - grid` != 0, i.e. any cell != 1, as blocked), with blocked, unreachable and equal ends."""
+    rs = np.random.RandomState(4242)
+    out = {}
+    demo = np.load(os.path.join(REF, 'shortest_paths', 'sample-configuration-space.npy')).astype(np.uint8)
+    free = np.argwhere(demo > 0)
+    blocked = np.argwhere(demo == 0)
+    g = sp.GridGraph(demo)
+    q = 0
+    for k in range(24):
+        s = free[rs.randint(len(free))]
+        t = (blocked if k % 8 == 7 else free)[rs.randint(len(blocked) if k % 8 == 7 else len(free))]
+        if k % 8 == 3:
+            t = s
+        out['demo_%d_src' % q] = s.astype(np.int32)
+        out['demo_%d_tgt' % q] = t.astype(np.int32)
+        out['demo_%d_path' % q] = np.array(g.shortest_path((int(s[0]), int(s[1])), (int(t[0]), int(t[1]))),
+                                           dtype=np.int32).reshape(-1, 2)
+        q += 1
+    for m in range(12):
+        h, w = int(rs.randint(8, 64)), int(rs.randint(8, 64))
+        grid = (rs.rand(h, w) > [0.15, 0.3, 0.45][m % 3]).astype(np.uint8)
+        if m % 4 == 1:  # multi-valued free cells
+            grid = grid * rs.choice(np.array([1, 1, 2, 255], dtype=np.uint8), size=(h, w))
+        grid[0, 0] = 1
+        gg = sp.GridGraph(np.ascontiguousarray(grid))
+        fr = np.argwhere(grid > 0)
+        for k in range(6):
+            s = fr[rs.randint(len(fr))] if k != 4 else np.array([rs.randint(h), rs.randint(w)])
+            t = fr[rs.randint(len(fr))] if k != 5 else np.array([rs.randint(h), rs.randint(w)])
+            key = 'rand_%d_%d' % (m, k)
+            out[key + '_src'] = s.astype(np.int32)
+            out[key + '_tgt'] = t.astype(np.int32)
+            out[key + '_path'] = np.array(gg.shortest_path((int(s[0]), int(s[1])), (int(t[0]), int(t[1]))),
+                                          dtype=np.int32).reshape(-1, 2)
+        out['rand_%d_grid' % m] = grid
+    np.savez_compressed(os.path.join(HERE, 'grid_paths.npz'), **out)
+    print('wrote grid path goldens')
+
+
 def gen_ingest(envs):
     """Observation ingest: Robot.update_map -> Mapper.update (envs.py:
     2056-2066) = Camera.capture_image point cloud (1927-1955), overhead scatter (argsort by z),
@@ -439,6 +482,8 @@ def main():
         gen_paths(envs, sp)
     if 'ingest' in which or not sys.argv[1:]:
         gen_ingest(envs)
+    if 'grid_paths' in which or not sys.argv[1:]:
+        gen_grid_paths(sp)
 
 
 if __name__ == '__main__':

@@ -18,8 +18,10 @@ def declared_symbols():
 
 
 def test_header_declares_the_abi():
-    assert declared_symbols() == sorted(['simaps_abi_version', 'simaps_last_error', 'simaps_num_channels', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest',
-                                         'simaps_robot_mask', 'simaps_get_state', 'simaps_sssp_grid'])
+    assert declared_symbols() == sorted(['simaps_abi_version', 'simaps_last_error', 'simaps_fault_status',
+                                         'simaps_num_channels', 'simaps_sp_distance', 'simaps_shortest_path',
+                                         'simaps_ingest', 'simaps_robot_mask', 'simaps_get_state', 'simaps_sssp_grid',
+                                         'simaps_grid_path'])
 
 
 def test_library_exports_every_declared_symbol():
@@ -28,7 +30,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(_lib.lib, name), name
         assert isinstance(getattr(_lib.lib, name), ctypes._CFuncPtr)
     assert set(_lib.EXPORTED) == set(declared_symbols())
-    assert _lib.lib.simaps_abi_version() == 2
+    assert _lib.lib.simaps_abi_version() == 3
 
 
 def test_struct_layouts_match_header():
@@ -70,6 +72,16 @@ def test_error_paths_do_not_launch():
     rc = _lib.lib.simaps_get_state(c, 1, None, None, None, None, None, None, None, 0, None, None)
     assert rc == -2 and b'thickness' in _lib.lib.simaps_last_error()
     assert _lib.lib.simaps_sssp_grid(1, 300, 300, None, None, None, 0, 0, 300, 300, None) == -1
+    assert _lib.lib.simaps_grid_path(1, 30, 30, None, None, None, 0, 0, 30, 30, 0, None, None, None) == -1
+    assert _lib.lib.simaps_grid_path(0, 30, 30, None, None, None, 0, 0, 30, 30, 8, None, None, None) == 0
+
+
+def test_fault_status_without_gpu():
+    """The host-mapped fault word needs a device: without one the call reports SIMAPS_EHIP
+    instead of crashing; with one the word starts clear."""
+    from simaps import _lib
+    rc = _lib.lib.simaps_fault_status(0)
+    assert rc in (0, _lib.EHIP)
 
 
 def test_statebatch_refuses_cpu_device():

@@ -201,3 +201,58 @@ def test_ingest_then_get_state_vs_oracle(V, kind):
                  s['receptacle_position'] is not None)
         assert _bitwise(ov[n], s['overhead'][a]) and np.array_equal(oc[n], s['occupancy'][a]), (e, a)
         assert _bitwise(st[n], O.agent_state(s, a)), (e, a)
+
+
+def test_gridgraph_shortest_path_reference_goldens(V):
+    """GridGraph.shortest_path (pyx:121-154) on raw cells against the reference itself: the demo
+    sample (free / blocked / equal ends) and random grids with free values 1, 2, 255 (line of sight
+    counts any cell != 1 as blocked), blocked sources, unreachable targets."""
+    synthetic, vector_env = V
+    z = G.load('grid_paths.npz')
+    demo = G.load('sssp.npz')['demo_cspace']
+    g = vector_env.GridGraph(demo)
+    keys = sorted(k[:-4] for k in z.files if k.startswith('demo_') and k.endswith('_src'))
+    got = g.shortest_paths([(tuple(z[k + '_src']), tuple(z[k + '_tgt'])) for k in keys])
+    for k, p in zip(keys, got):
+        assert np.array_equal(np.array(p, dtype=np.int32).reshape(-1, 2), z[k + '_path']), k
+    s0 = G.load('paths.npz')                                         # the 3 demo.py-sample goldens of r1
+    for q in range(3):
+        p = g.shortest_path(tuple(s0['demo_%d_src' % q]), tuple(s0['demo_%d_tgt' % q]))
+        assert np.array_equal(np.array(p).reshape(-1, 2), s0['demo_%d_path' % q]), q
+    m = 0
+    while 'rand_%d_grid' % m in z.files:
+        grid = z['rand_%d_grid' % m]
+        gg = vector_env.GridGraph(grid)
+        pairs = [(tuple(z['rand_%d_%d_src' % (m, k)]), tuple(z['rand_%d_%d_tgt' % (m, k)])) for k in range(6)]
+        for k, p in enumerate(gg.shortest_paths(pairs)):
+            assert np.array_equal(np.array(p, dtype=np.int32).reshape(-1, 2), z['rand_%d_%d_path' % (m, k)]), (m, k)
+        m += 1
+    assert m == 12
+
+
+def test_policy_input_from_device_stacks(V):
+    """device-rendered CHW stacks through policy_input.group_batches equal
+    DQNPolicy.apply_transform (ToTensor of the (96, 96, C) float32 state, policies.py:44-45) of the
+    oracle's states, bitwise, batched per robot group, with no copy of the rendered tensor."""
+    synthetic, vector_env = V
+    from simaps import policy_input
+    cfg = 'lifting_2_throwing_2-large_empty'
+    scenes = [synthetic.make_scene(cfg, 610 + e) for e in range(3)]
+    obs = vector_env.VectorEnvObservations(scenes, layout='chw')
+    awaiting = [[True, False, True, True], [True] * 4, [False, True, False, False]]
+    state = obs.get_state(awaiting=awaiting)
+    for e, s in enumerate(scenes):
+        groups = vector_env.robot_groups(s)
+        for (idx, bt), members in zip(policy_input.group_batches(state[e]), groups):
+            want = [a for j, a in enumerate(members) if awaiting[e][a]]
+            assert idx == [j for j, a in enumerate(members) if awaiting[e][a]]
+            if not want:
+                assert bt is None
+                continue
+            assert bt.is_cuda and tuple(bt.shape) == (len(want), 5, 96, 96) and bt.dtype == torch.float32
+            ref = torch.cat([policy_input.apply_transform(O.agent_state(s, a)) for a in want]).numpy()
+            assert np.array_equal(bt.cpu().numpy().view(np.int32), ref.view(np.int32))
+        # a single state is a zero-copy view of the rendered CHW tensor
+        x = state[e][0][0] if state[e][0][0] is not None else state[e][0][1]
+        t = policy_input.apply_transform(x)
+        assert t.data_ptr() == x.data_ptr() and t.is_contiguous()

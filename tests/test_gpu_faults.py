@@ -1,0 +1,130 @@
+"""GPU tests of the always-on device fault path (include/simaps.h SIMAPS_FAULT_*) and of launches
+on a side stream.
+
+A kernel that hits a condition invalidating its output -- a wave-group barrier that gave up
+waiting, the SSSP round cap, or a descriptor field clamped to this build's limits -- posts a bit
+to the library's host-mapped fault word.  simaps_fault_status reads it after a sync, and the next
+compute call fails with SIMAPS_EDEVICE, with or without debug buffers.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DIAG_LIB = os.path.join(ROOT, 'spatial-intention-maps_amd', 'simaps', 'libsimaps_diagflag.so')
+
+
+@pytest.fixture(scope='module')
+def S():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a GPU (run with -m gpu on an MI355X)')
+    from simaps import _lib, batch, synthetic
+    _lib.lib.simaps_fault_status(1)
+    yield _lib, batch, synthetic
+    _lib.lib.simaps_fault_status(1)
+
+
+def _launch(L, _lib, b, robots_d, envs_d, agents_d, paths_d, out, n):
+    return L.simaps_get_state(b.cfg, n, _lib.ptr(agents_d), _lib.ptr(envs_d), _lib.ptr(robots_d), _lib.ptr(paths_d),
+                              _lib.ptr(b.occupancy), _lib.ptr(b.overhead), _lib.ptr(out), 0, None,
+                              _lib.stream_handle())
+
+
+def _dev(batch, a, device):
+    return batch._to_dev(a, device)
+
+
+def test_clean_run_posts_no_fault(S):
+    _lib, batch, synthetic = S
+    b = batch.StateBatch([synthetic.make_scene('lifting_4-small_divider', e) for e in range(8)])
+    b.render()
+    torch.cuda.synchronize()
+    assert _lib.lib.simaps_fault_status(0) == 0
+    _lib.check_faults()
+
+
+@pytest.mark.parametrize('bad', ['num_robots', 'robot_index', 'path_length'])
+def test_descriptor_clamp_is_reported(S, bad):
+    """num_robots > SIMAPS_MAX_ROBOTS, a robot index past num_robots, or an intention path longer
+    than SIMAPS_MAX_PATH: the kernel clamps (no out-of-range LDS access) and reports it."""
+    _lib, batch, synthetic = S
+    scene = synthetic.make_scene('lifting_4-small_divider', 5)
+    b = batch.StateBatch([scene])
+    robots, envs, ag, paths = batch.pack_descriptors([scene], b.agents)
+    robots = np.concatenate([robots, np.repeat(robots[:1], 8)])       # records past num_robots exist
+    paths = np.concatenate([paths, np.repeat(paths[:1], 40, 0)])
+    if bad == 'num_robots':
+        envs['num_robots'] = 9
+    elif bad == 'robot_index':
+        ag['robot'][1] = 6
+    else:
+        robots['intention_len'][2] = 17
+    out = b.alloc_state()
+    dev = lambda a: _dev(batch, a, b.device)  # noqa: E731
+    R, E, A, P = dev(robots), dev(envs), dev(ag), torch.from_numpy(paths).to(b.device)
+    assert _launch(_lib.lib, _lib, b, R, E, A, P, out, b.N) == 0
+    torch.cuda.synchronize()
+    assert _lib.lib.simaps_fault_status(0) == _lib.FAULT_DESCRIPTOR
+    # the next compute call refuses once (and clears the word), then works again
+    assert _launch(_lib.lib, _lib, b, R, E, A, P, out, b.N) == _lib.EDEVICE
+    assert b'descriptor clamped' in _lib.lib.simaps_last_error()
+    torch.cuda.synchronize()
+    _lib.lib.simaps_fault_status(1)
+    b.render()
+    torch.cuda.synchronize()
+    assert _lib.lib.simaps_fault_status(0) == 0
+
+
+def test_barrier_timeout_flag_reaches_the_caller(S):
+    """Diagnostic build libsimaps_diagflag.so raises the barrier-timeout flag at its real site (the
+    Group::sync spin) but keeps waiting: the output is still exact, and the fault surfaces through
+    simaps_fault_status, the next call's SIMAPS_EDEVICE, and simaps._lib.check_faults."""
+    _lib, batch, synthetic = S
+    if not os.path.exists(DIAG_LIB):
+        pytest.fail('build the diagnostic library first: make -C spatial-intention-maps_amd/csrc diag')
+    L = _lib._load(DIAG_LIB)
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 40 + e) for e in range(4)]
+    b = batch.StateBatch(scenes)
+    assert L.simaps_fault_status(1) == 0
+    out = b.alloc_state()
+    assert _launch(L, _lib, b, b.robots_d, b.envs_d, b.agents_d, b.paths_d, out, b.N) == 0
+    st = b.as_hwc(out).cpu().numpy()
+    assert L.simaps_fault_status(0) & _lib.FAULT_TIMEOUT
+    # the next call refuses (and clears the word); a new launch posts the flag again
+    assert _launch(L, _lib, b, b.robots_d, b.envs_d, b.agents_d, b.paths_d, out, b.N) == _lib.EDEVICE
+    assert L.simaps_fault_status(0) == 0
+    assert _launch(L, _lib, b, b.robots_d, b.envs_d, b.agents_d, b.paths_d, out, b.N) == 0
+    torch.cuda.synchronize()
+    with pytest.raises(_lib.DeviceFault):
+        _lib.check_faults(L)
+    assert L.simaps_fault_status(0) == 0
+    for n, (e, a) in enumerate(b.agents):
+        assert np.array_equal(st[n].view(np.int32), O.agent_state(scenes[e], a).view(np.int32))
+    assert _lib.lib.simaps_fault_status(0) == 0       # the product library's word is separate
+
+
+def test_side_stream_render_matches_default_stream(S):
+    """render on a non-current stream; outputs / inputs are held for that stream and the
+    reader waits for it."""
+    _lib, batch, synthetic = S
+    from simaps import vector_env
+    scenes = [synthetic.make_scene('pushing_4-large_empty', 70 + e) for e in range(6)]
+    obs = vector_env.VectorEnvObservations(scenes, layout='chw')
+    ref = obs.batch.as_hwc(obs.batch.render()).cpu().numpy()
+    side = torch.cuda.Stream()
+    for _ in range(3):
+        st = obs.get_state(all_robots=True, numpy=True, stream=side)
+        for e, s in enumerate(scenes):
+            for g, idx in zip(st[e], vector_env.robot_groups(s)):
+                for x, a in zip(g, idx):
+                    assert np.array_equal(x.view(np.int32), ref[obs.slot[(e, a)]].view(np.int32))
+    out = obs.batch.render(stream=side)
+    torch.cuda.current_stream().wait_stream(side)
+    assert np.array_equal(obs.batch.as_hwc(out).cpu().numpy().view(np.int32), ref.view(np.int32))

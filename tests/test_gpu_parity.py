@@ -131,6 +131,51 @@ def test_full_size_lifting_4_small_divider_properties(S):
         assert _bitwise(s1[n], O.agent_state(scenes[e], a))
 
 
+def _channel_invariants(st, flags):
+    """Size-independent properties of rendered stacks (N, 96, 96, C), by channel (envs.py:2071-2113)."""
+    N = st.shape[0]
+    assert np.all(np.isfinite(st))
+    c = 0
+    assert set(np.unique(st[..., c])) <= {k / 8 for k in range(9)}      # overhead: seg codes k / 8
+    c += 1
+    if flags['use_robot_map']:
+        assert set(np.unique(st[..., c])) <= {0.0, 0.5, 1.0}
+        c += 1
+    if flags['use_distance_to_receptacle_map']:
+        c += 1
+    for k in ('use_shortest_path_to_receptacle_map', 'use_shortest_path_map'):
+        if flags[k]:                                                     # local min-subtract (envs.py:2213-2216)
+            assert np.all(st[..., c].reshape(N, -1).min(1) == 0)
+            c += 1
+    if flags['use_history_map'] or flags['use_intention_map']:
+        assert np.all(st[..., c] >= 0) and np.all(st[..., c] <= max(1.0, flags['intention_map_scale']))
+
+
+@pytest.mark.parametrize('cfg,envs', [('pushing_4-large_empty', 256), ('lifting_2_throwing_2-large_empty', 1024),
+                                      ('rescue_4-small_empty', 2048)])
+def test_full_size_baseline_configs(S, cfg, envs):
+    """The other BASELINE configs at their full single-launch sizes (1,024 / 4,096 / 8,192 stacks,
+    i.e. 4-32 workgroups per CU back to back): no device fault, status clean for every agent,
+    deterministic, channel invariants, and a seeded sample of agents bitwise against the oracle."""
+    from simaps import _lib
+    batch, K, synthetic = S
+    scenes = [synthetic.make_scene(cfg, 3000 + e) for e in range(envs)]
+    b = batch.StateBatch(scenes)
+    status = torch.full((b.N,), -1, dtype=torch.int32, device=b.device)
+    s1 = b.as_hwc(b.render(debug={'status': status})).cpu().numpy()
+    _lib.check_faults()
+    st = status.cpu().numpy()
+    assert np.all(st & 0xff == 0), 'status bits set for %d agents' % int((st & 0xff != 0).sum())
+    assert np.all(st >> 8 > 0)                                           # every agent's SSSP converged
+    s2 = b.as_hwc(b.render()).cpu().numpy()
+    assert _bitwise(s1, s2)
+    _channel_invariants(s1, scenes[0]['flags'])
+    rs = np.random.RandomState(11)
+    for n in sorted(rs.choice(b.N, 10, replace=False)) + [0, b.N - 1]:
+        e, a = b.agents[n]
+        assert _bitwise(s1[n], O.agent_state(scenes[e], a)), (cfg, n)
+
+
 def test_snap_slow_path_and_idle(S):
     """Agents pressed against walls / divider (query pixel not free -> EDT snap), all robots idle."""
     batch, K, synthetic = S

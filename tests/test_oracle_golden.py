@@ -180,3 +180,17 @@ def test_oracle_ingest_vs_reference():
                      s['receptacle_position'] is not None)
             assert np.array_equal(ov.view(np.int32), z[k + '_overhead'].view(np.int32)), k
             assert np.array_equal(oc, z[k + '_occupancy']), k
+
+
+def test_oracle_grid_shortest_path_vs_reference():
+    """GridGraph.shortest_path on raw cells (pyx:121-154): demo sample + multi-valued random grids."""
+    z = G.load('grid_paths.npz')
+    demo = G.load('sssp.npz')['demo_cspace']
+    for k in sorted(k[:-4] for k in z.files if k.startswith('demo_') and k.endswith('_src')):
+        got = np.array(O.grid_shortest_path(demo, z[k + '_src'], z[k + '_tgt'])).reshape(-1, 2)
+        assert np.array_equal(got, z[k + '_path']), k
+    for m in range(12):
+        for k in range(6):
+            key = 'rand_%d_%d' % (m, k)
+            got = np.array(O.grid_shortest_path(z['rand_%d_grid' % m], z[key + '_src'], z[key + '_tgt'])).reshape(-1, 2)
+            assert np.array_equal(got, z[key + '_path']), key
