@@ -1,12 +1,14 @@
 """Benchmark: agent-state stacks/s of the fused HIP observation path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--envs E]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--envs E | --total-envs T] [--gather R]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N ...
 
 A step = one launch rendering every agent of E envs (E x A stacks) from HBM-resident per-agent
-maps (inputs uploaded before the timed region).  Multi-GPU: each rank renders its own E envs
-(distinct seeds; weak scaling), no data-path collective; barrier + max-over-ranks timing.
+maps (inputs uploaded before the timed region).  Multi-GPU: each rank renders its own block of
+envs (distinct seeds) -- E per rank (weak scaling, default) or a contiguous share of
+--total-envs (strong scaling, BASELINE configs[3] / [4]) -- with no data-path collective; barrier
++ max-over-ranks timing.  --gather R times an optional state gather to rank 0 separately.
 Prints ONE JSON line (rank 0).
 """
 import argparse
@@ -27,32 +29,30 @@ def algorithmic_bytes_per_stack(H, W, C):
     return H * W + 136 * 136 * 4 + 96 * 96 * 4 * C
 
 
-def cpu_baseline(config, budget_s=15.0):
-    """The oracle (numpy + C SPFA restatement of the reference path; 'port') on ONE host core,
-    over as many agent stacks of the same workload as fit in ~budget_s seconds (scene generation
-    excluded)."""
-    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
-    import oracle
-    from simaps import synthetic
-    oracle.agent_state(synthetic.make_scene(config, 10_000), 0)  # warm: build / load liboracle
-    n, e, el = 0, 0, 0.0
-    while el < budget_s and e < 100_000:
-        s = synthetic.make_scene(config, e)
-        for a in range(len(s['robots'])):
-            t0 = time.perf_counter()
-            oracle.agent_state(s, a)
-            el += time.perf_counter() - t0
-            n += 1
-        e += 1
-    return {'value': n / el, 'unit': 'stacks/s', 'cores': 1, 'kind': 'port',
-            'sample': '%d agent stacks (%d envs of %s), OccupancyMap.update minus point scatter + '
-                      'Mapper.get_state via oracle/ (numpy + C SPFA), 1 thread, %.1f s' % (n, e, config, el)}
+def cpu_baseline(config, budget_s=6.0, procs=0):
+    """the oracle (numpy + C SPFA restatement of the reference path; kind
+    "port") on this host's cores -- 1 process and P single-threaded processes -- in a child process
+    tree (tools/cpu_baseline.py) that never touches the GPU.  `value` is the P-process aggregate;
+    the line also carries the 1-core rate, the CPU model and, from the dev-container calibration
+    against the reference itself (profiles/r2_cpu_calibration.json), the reference's estimated rate."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--config', config, '--budget', str(budget_s)]
+    if procs:
+        cmd += ['--procs', str(procs)]
+    out = subprocess.run(cmd, capture_output=True, text=True, check=True, timeout=600)
+    return json.loads(out.stdout.strip().splitlines()[-1])
 
 
-def rank_envs(rank, envs_per_rank):
+def rank_envs(rank, envs_per_rank, world=1, total_envs=None):
     """Env ids (= scene seeds) of one rank: a contiguous block of whole envs.
-    Weak scaling: every rank renders envs_per_rank envs, the job renders world * envs_per_rank."""
-    return list(range(rank * envs_per_rank, (rank + 1) * envs_per_rank))
+    Weak scaling (total_envs None): every rank renders envs_per_rank envs, the job world *
+    envs_per_rank.  Strong scaling: the job renders total_envs envs, split into contiguous blocks
+    whose sizes differ by at most one (the first total_envs % world ranks take one more)."""
+    if total_envs is None:
+        return list(range(rank * envs_per_rank, (rank + 1) * envs_per_rank))
+    q, r = divmod(total_envs, world)
+    lo = rank * q + min(rank, r)
+    return list(range(lo, lo + q + (1 if rank < r else 0)))
 
 
 def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu'):
@@ -88,15 +88,58 @@ def max_over_ranks(values, world, device='cpu'):
     return [float(x) for x in t.cpu()]
 
 
+def sum_over_ranks(values, world, device='cpu'):
+    """Element-wise sum of per-rank numbers (identity for world == 1)."""
+    if world == 1:
+        return list(values)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(x) for x in t.cpu()]
+
+
+def gather_states(out, reps, world, rank, return_data=False):
+    """SURVEY.md 8(e)'s optional consumer gather, timed apart from the render: every rank's rendered
+    states (padded to the largest block) to rank 0 over RCCL / xGMI, `reps` times; max over ranks.
+    (Any device: the gloo tests run it on CPU tensors.)"""
+    import torch
+    import torch.distributed as dist
+    sync = torch.cuda.synchronize if out.is_cuda else (lambda: None)
+    n = int(max_over_ranks([out.shape[0]], world, out.device)[0])
+    src = torch.zeros((n,) + tuple(out.shape[1:]), dtype=out.dtype, device=out.device)
+    src[:out.shape[0]].copy_(out)
+    dst = [torch.empty_like(src) for _ in range(world)] if rank == 0 else None
+    dist.gather(src, dst, dst=0)  # warm-up (connection setup)
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.gather(src, dst, dst=0)
+    sync()
+    dist.barrier()
+    el = max_over_ranks([time.perf_counter() - t0], world, out.device)[0] / reps
+    moved = src.numel() * src.element_size() * (world - 1)
+    stats = {'ms': el * 1e3, 'bytes_to_rank0': moved, 'GB_per_s': moved / el / 1e9, 'reps': reps,
+             'note': 'states of ranks 1..N-1 (padded to the largest block) gathered to rank 0; not in value'}
+    return (stats, dst) if return_data else stats
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument('--config', default='lifting_4-small_divider')
-    ap.add_argument('--envs', type=int, default=64, help='envs per GPU (BASELINE configs[1]: 64)')
+    ap.add_argument('--envs', type=int, default=64, help='envs per GPU, weak scaling (BASELINE configs[1]: 64)')
+    ap.add_argument('--total-envs', type=int, default=None,
+                    help='strong scaling: envs of the whole job, split over the ranks (configs[3]: 1024, [4]: 2048)')
+    ap.add_argument('--gather', type=int, default=0, metavar='REPS',
+                    help='after the timed region, time REPS gathers of every rank\'s states to rank 0 (reported '
+                         'separately, SURVEY.md 8(e))')
     ap.add_argument('--layout', default='chw', choices=['hwc', 'chw'])
-    ap.add_argument('--cpu-budget', type=float, default=15.0)
+    ap.add_argument('--cpu-budget', type=float, default=6.0, help='seconds per CPU-baseline leg and worker')
+    ap.add_argument('--cpu-procs', type=int, default=0, help='CPU-baseline processes (default: usable cores, capped)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
 
@@ -112,7 +155,10 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
 
     from simaps import batch, synthetic
-    scenes = [synthetic.make_scene(args.config, e) for e in rank_envs(rank, args.envs)]
+    strong = args.total_envs is not None
+    if strong and args.total_envs < world:
+        raise SystemExit('--total-envs must give every rank at least one env')
+    scenes = [synthetic.make_scene(args.config, e) for e in rank_envs(rank, args.envs, world, args.total_envs)]
     b = batch.StateBatch(scenes, device='cuda', layout=args.layout)
     out = b.alloc_state()
     stream = torch.cuda.current_stream()
@@ -132,36 +178,44 @@ def main():
     elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, 'cuda')
     kern_ms = max_over_ranks([ev0.elapsed_time(ev1) / args.steps], world, 'cuda')[0]
 
-    stacks_per_step = b.N * world
+    stacks_per_step = int(sum_over_ranks([b.N], world, 'cuda')[0])
     value = stacks_per_step * args.steps / elapsed
     B = algorithmic_bytes_per_stack(b.H, b.W, b.C)
     achieved = B * b.N / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    # HBM traffic comes from rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE cannot be read in-process):
+    # the committed profile of the same config / launch size / layout, labelled as such, else null
+    traffic, traffic_src = None, None
     tf = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tf):
         try:
             t = json.load(open(tf))
             if (t.get('config'), t.get('stacks_per_launch'), t.get('layout')) == (args.config, b.N, args.layout):
                 traffic = t.get('hbm_bytes_per_launch')
-        except Exception:
+                traffic_src = 'from_profile: profiles/pmc_traffic.json (%s, rocprofv3 PMC passes)' % t.get('tag')
+        except (OSError, ValueError):
             traffic = None
+    gather = gather_states(out, args.gather, world, rank) if args.gather and world > 1 else None
 
     if rank == 0:
         res = {
             'metric': METRIC,
             'value': value, 'unit': 'stacks/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+            'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True,
+            'scaling': 'strong' if strong else 'weak',
             'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic (seeded scenes, SURVEY 8(d))',
-            'config': {'workload': args.config, 'envs_per_gpu': args.envs, 'agents_per_env': len(scenes[0]['robots']),
+            'config': {'workload': args.config, 'agents_per_env': len(scenes[0]['robots']),
                        'stacks_per_step': stacks_per_step, 'grid': '%dx%d' % (b.H, b.W), 'channels': b.C,
                        'layout': args.layout, 'parallelism': 'env-sharded x%d' % world},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'traffic_source': traffic_src,
                          'kernel': 'get_state_kernel', 'kernel_ms': kern_ms,
                          'algorithmic_bytes_per_stack': B},
         }
+        res['config'].update({'total_envs': args.total_envs} if strong else {'envs_per_gpu': args.envs})
+        if gather is not None:
+            res['gather'] = gather
         if world == 1 and not args.no_cpu_baseline:
-            res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_budget)
+            res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_budget, args.cpu_procs)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -79,3 +79,52 @@ def test_rank_envs_partition():
     for world in (1, 2, 4, 8):
         ids = [e for r in range(world) for e in bench.rank_envs(r, 128)]
         assert ids == list(range(world * 128))
+
+
+def _strong_worker(rank, world, port, total, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    import bench
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        ids = bench.rank_envs(rank, None, world, total)
+        n = int(bench.sum_over_ranks([len(ids)], world)[0])
+        # stand-in "states": each env's id in a (2, 3) plane per stack, like the [N, C, 96, 96] output
+        out = torch.tensor(ids, dtype=torch.float32).repeat_interleave(2).view(-1, 1, 1).expand(-1, 2, 3).contiguous()
+        stats, dst = bench.gather_states(out, 2, world, rank, return_data=True)
+        got = None
+        if rank == 0:
+            got = torch.cat([d[:, 0, 0] for d in dst]).numpy()
+        np.save(os.path.join(out_dir, 's%d.npy' % rank),
+                np.array([len(ids), ids[0], ids[-1], n, stats['bytes_to_rank0'], stats['reps']]))
+        if rank == 0:
+            np.save(os.path.join(out_dir, 'gathered.npy'), got)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_strong_split_and_gather(tmp_path):
+    """Strong scaling (bench.py --total-envs, BASELINE configs[3] / [4]): an uneven total splits into
+    contiguous blocks (4 + 3), the job's stack count sums over ranks, and the optional state gather
+    delivers every rank's block to rank 0 (padded to the largest block)."""
+    world, total = 2, 7
+    mp.spawn(_strong_worker, args=(world, _free_port(), total, str(tmp_path)), nprocs=world, join=True)
+    s0, s1 = (np.load(os.path.join(tmp_path, 's%d.npy' % k)) for k in range(world))
+    assert list(s0[:4]) == [4, 0, 3, 7] and list(s1[:4]) == [3, 4, 6, 7]
+    assert s0[4] == s1[4] == 8 * 2 * 3 * 4 * (world - 1)   # padded block of 4 envs x 2 stacks, f32
+    g = np.load(os.path.join(tmp_path, 'gathered.npy'))
+    assert list(g) == [0, 0, 1, 1, 2, 2, 3, 3] + [4, 4, 5, 5, 6, 6, 0, 0]
+
+
+def test_rank_envs_strong_partition():
+    sys.path.insert(0, ROOT)
+    import bench
+    for total in (1024, 2048, 1025, 2047, 9):
+        for world in (1, 2, 3, 4, 8):
+            blocks = [bench.rank_envs(r, None, world, total) for r in range(world)]
+            assert [e for b in blocks for e in b] == list(range(total))
+            sizes = [len(b) for b in blocks]
+            assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
