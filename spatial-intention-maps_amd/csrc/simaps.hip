@@ -150,7 +150,7 @@ struct Group {
     int t, n;           // thread index within the group, threads in the group
     unsigned *bar;      // nullptr: the whole workgroup (__syncthreads)
     int nw;             // waves in the group
-    __device__ void sync() const
+    __device__ __forceinline__ void sync() const
     {
         if (!bar) {
             lds_barrier();

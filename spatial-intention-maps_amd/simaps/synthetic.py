@@ -56,7 +56,23 @@ CONFIGS = {
                                                 flags={'use_distance_to_receptacle_map': True,
                                                        'use_history_map': True, 'use_intention_map': True,
                                                        'use_intention_channels': True}),
+    # --- the reference's maze environments (envs.py:528-549, 577-592), config/experiments/ours/ ---
+    'lifting_4-large_doors': dict(env_name='large_doors', robot_config=[{'lifting_robot': 4}],
+                                  flags={'use_intention_map': True}, long_paths=True),
+    'lifting_4-large_tunnels': dict(env_name='large_tunnels', robot_config=[{'lifting_robot': 4}],
+                                    flags={'use_intention_map': True}, long_paths=True),
+    'lifting_4-large_rooms': dict(env_name='large_rooms', robot_config=[{'lifting_robot': 4}],
+                                  flags={'use_intention_map': True}, long_paths=True),
+    'lifting_2_throwing_2-large_doors': dict(env_name='large_doors',
+                                             robot_config=[{'lifting_robot': 2}, {'throwing_robot': 2}],
+                                             flags={'use_intention_map': True}, long_paths=True),
+    # config/experiments/comparisons/history_maps/lifting_4-large_rooms-history.yml
+    'lifting_4-large_rooms-history': dict(env_name='large_rooms', robot_config=[{'lifting_robot': 4}],
+                                          flags={'use_history_map': True}, long_paths=True),
 }
+
+MAZE_CONFIGS = ('lifting_4-large_doors', 'lifting_4-large_tunnels', 'lifting_4-large_rooms',
+                'lifting_2_throwing_2-large_doors', 'lifting_4-large_rooms-history')
 
 BASELINE_CONFIGS = ('lifting_1-small_empty', 'lifting_4-small_divider', 'pushing_4-large_empty',
                     'lifting_2_throwing_2-large_empty', 'rescue_4-small_empty')
@@ -96,9 +112,12 @@ def pixel_center_positions(H, W):
 
 
 def _obstacles(env_name, room_length, room_width, rs):
-    """Boxes of VectorEnv._get_obstacles (envs.py:515-571) + robot spawn bounds.
+    """Boxes of VectorEnv._get_obstacles (envs.py:515-571), the wall / divider corners
+    (envs.py:589-647) and the robot / cube spawn bounds.
 
-    Only the env names of the BASELINE configs (empty / divider) are generated."""
+    Returns (boxes [(x, y, x_len, y_len)], divider_corners [(x, y, heading_deg)], robot_bounds,
+    cube_bounds).  The room corners (envs.py:573-587) are added by make_scene.  The random draws
+    follow the reference's order (room_random_state: one uniform per offset)."""
     wall_thickness = 1.4
     boxes = []
     for x, y, length, width in [
@@ -107,15 +126,75 @@ def _obstacles(env_name, room_length, room_width, rs):
             (0, -room_width / 2 - wall_thickness / 2, room_length + 2 * wall_thickness, wall_thickness),
             (0, room_width / 2 + wall_thickness / 2, room_length + 2 * wall_thickness, wall_thickness)]:
         boxes.append((x, y, length, width))
-    spawn_bounds = None
+    dividers = []  # (x, y, x_len, y_len, snap_y or None)
+    spawn_bounds = cube_bounds = None
     if env_name in ('small_divider', 'small_divider_norand'):
         x_offset = rs.uniform(-0.1, 0.1) if env_name == 'small_divider' else 0.0
         divider_width, opening_width = 0.05, 0.16
-        boxes.append((x_offset, 0.0, divider_width, room_width - 2 * opening_width))
+        dividers.append((x_offset, 0.0, divider_width, room_width - 2 * opening_width, None))
         spawn_bounds = (x_offset + divider_width / 2, None, None, None)
+        cube_bounds = (None, x_offset - divider_width / 2, None, None)
+    elif env_name in ('large_doors', 'large_doors_norand', 'large_tunnels', 'large_tunnels_norand'):
+        tunnel_length = 0.05 if env_name.startswith('large_doors') else 0.25
+        x_offset = y_offset = 0.0
+        if env_name == 'large_doors':
+            x_offset, y_offset = rs.uniform(-0.05, 0.05), rs.uniform(-0.1, 0.1)
+        elif env_name == 'large_tunnels':
+            x_offset, y_offset = rs.uniform(-0.05, 0.05), rs.uniform(-0.05, 0.05)
+        tunnel_width = 0.18  # add_tunnels (envs.py:530-540)
+        tunnel_x = (room_length + tunnel_width) / 6 + x_offset
+        outer_divider_len = room_length / 2 - tunnel_x - tunnel_width / 2
+        divider_x = room_length / 2 - outer_divider_len / 2
+        middle_divider_len = 2 * (tunnel_x - tunnel_width / 2)
+        dividers.append((-divider_x, y_offset, outer_divider_len, tunnel_length, None))
+        dividers.append((0.0, y_offset, middle_divider_len, tunnel_length, None))
+        dividers.append((divider_x, y_offset, outer_divider_len, tunnel_length, None))
+        spawn_bounds = (None, None, y_offset + tunnel_length / 2, None)
+        cube_bounds = (None, None, None, y_offset - tunnel_length / 2)
+    elif env_name in ('large_rooms', 'large_rooms_norand'):
+        x_offset = y_offset = 0.0
+        if env_name == 'large_rooms':
+            x_offset, y_offset = rs.uniform(-0.05, 0.05), rs.uniform(-0.05, 0.05)
+        divider_width, opening_width = 0.05, 0.18  # add_rooms (envs.py:542-551)
+        divider_len = room_width / 2 - opening_width - divider_width / 2
+        top_divider_len = divider_len - y_offset
+        bot_divider_len = divider_len + y_offset
+        top_divider_y = room_width / 2 - opening_width - top_divider_len / 2
+        bot_divider_y = -room_width / 2 + opening_width + bot_divider_len / 2
+        dividers.append((0.0, y_offset, room_length - 2 * opening_width, divider_width, None))
+        dividers.append((x_offset, top_divider_y, divider_width, top_divider_len, y_offset + divider_width / 2))
+        dividers.append((x_offset, bot_divider_y, divider_width, bot_divider_len, y_offset - divider_width / 2))
     elif env_name not in ('small_empty', 'large_empty'):
-        raise ValueError('synthetic scenes support small_empty/small_divider/large_empty, not %r' % env_name)
-    return boxes, spawn_bounds
+        raise ValueError('unknown env_name %r' % env_name)
+    corners = []
+    for (x, y, length, width, snap_y) in dividers:  # corners between walls and dividers (envs.py:610-641)
+        boxes.append((x, y, length, width))
+        pos = None
+        if math.isclose(x - length / 2, -room_length / 2):
+            pos, hd = [(-room_length / 2, y - width / 2), (-room_length / 2, y + width / 2)], [0, 90]
+        elif math.isclose(x + length / 2, room_length / 2):
+            pos, hd = [(room_length / 2, y - width / 2), (room_length / 2, y + width / 2)], [-90, 180]
+        elif math.isclose(y - width / 2, -room_width / 2):
+            pos, hd = [(x - length / 2, -room_width / 2), (x + length / 2, -room_width / 2)], [180, 90]
+        elif math.isclose(y + width / 2, room_width / 2):
+            pos, hd = [(x - length / 2, room_width / 2), (x + length / 2, room_width / 2)], [-90, 0]
+        elif snap_y is not None:
+            pos = [(x - length / 2, snap_y), (x + length / 2, snap_y)]
+            hd = [-90, 0] if snap_y > y else [180, 90]
+        if pos is not None:
+            corners.extend((px, py, h) for (px, py), h in zip(pos, hd))
+    return boxes, corners, spawn_bounds, cube_bounds
+
+
+def _corner_mask(X, Y, cx, cy, heading_deg, w=0.1006834873):
+    """A rounded corner obstacle at corner point (cx, cy): the w x w square on the diagonal at
+    heading - 45 degrees (envs.py:583-586, 637-640) minus the quarter disk of radius w centred on
+    its far corner (the corner body's curved face)."""
+    a = math.radians(heading_deg - 45)
+    sx, sy = math.copysign(1, round(math.cos(a), 12)), math.copysign(1, round(math.sin(a), 12))
+    in_sq = (np.abs(X - cx) <= w) & (np.abs(Y - cy) <= w) & ((X - cx) * sx >= 0) & ((Y - cy) * sy >= 0)
+    ox, oy = cx + sx * w, cy + sy * w
+    return in_sq & ((X - ox) ** 2 + (Y - oy) ** 2 > w * w)
 
 
 def _random_position(rs, room_length, room_width, padding, bounds=None):
@@ -157,7 +236,8 @@ def make_scene(config_name, env_idx, seed_base=1234, observe_all=False):
     receptacle = None if is_rescue else (room_length / 2 - K.RECEPTACLE_WIDTH / 2,
                                          room_width / 2 - K.RECEPTACLE_WIDTH / 2, 0)  # envs.py:150-151
 
-    boxes, spawn_bounds = _obstacles(cfg['env_name'], room_length, room_width, rs)
+    boxes, div_corners, spawn_bounds, cube_bounds = _obstacles(cfg['env_name'], room_length, room_width, rs)
+    maze = cfg.get('long_paths', False)
     X, Y = pixel_center_positions(H, W)
     obstacle = np.zeros((H, W), dtype=bool)
     for (bx, by, bl, bw) in boxes:
@@ -173,6 +253,8 @@ def make_scene(config_name, env_idx, seed_base=1234, observe_all=False):
         in_sq = (np.abs(X - cx) <= w) & (np.abs(Y - cy) <= w) & ((X - cx) * sx >= 0) & ((Y - cy) * sy >= 0)
         ox, oy = cx + sx * w, cy + sy * w
         obstacle |= in_sq & ((X - ox) ** 2 + (Y - oy) ** 2 > w * w)
+    for (cx, cy, hd) in div_corners:
+        obstacle |= _corner_mask(X, Y, cx, cy, hd)
 
     in_room = (np.abs(X) <= room_length / 2) & (np.abs(Y) <= room_width / 2)
     seg = np.where(in_room, K.SEG_VALUES['floor'], K.SEG_VALUES['obstacle']).astype(np.float32)
@@ -181,7 +263,8 @@ def make_scene(config_name, env_idx, seed_base=1234, observe_all=False):
         rec = (np.abs(X - receptacle[0]) <= K.RECEPTACLE_WIDTH / 2) & (np.abs(Y - receptacle[1]) <= K.RECEPTACLE_WIDTH / 2)
         seg[rec & in_room & ~obstacle] = K.SEG_VALUES['receptacle']
     for _ in range(num_cubes):
-        px, py = _random_position(rs, room_length, room_width, K.CUBE_WIDTH / 2)
+        # (the BASELINE configs' scenes predate the cube spawn bounds; the maze configs use them)
+        px, py = _random_position(rs, room_length, room_width, K.CUBE_WIDTH / 2, cube_bounds if maze else None)
         cube = (np.abs(X - px) <= K.CUBE_WIDTH / 2) & (np.abs(Y - py) <= K.CUBE_WIDTH / 2)
         seg[cube & in_room & ~obstacle] = K.SEG_VALUES['cube']
 
@@ -192,7 +275,8 @@ def make_scene(config_name, env_idx, seed_base=1234, observe_all=False):
         for _ in range(count):
             px, py = _random_position(rs, room_length, room_width, geom['RADIUS'], spawn_bounds)
             heading = float(rs.uniform(-math.pi, math.pi))
-            n_wp = int(rs.randint(2, 6))
+            # maze configs: longer movement paths (doors / tunnels / rooms need more waypoints)
+            n_wp = int(rs.randint(2, 6)) if not maze else int(rs.randint(4, 12))
             wps = [(px, py, 0)]
             for _ in range(n_wp - 1):
                 wx, wy = _random_position(rs, room_length, room_width, geom['RADIUS'])

@@ -150,10 +150,13 @@ def run_agent(envs, env, scene, a):
     return out
 
 
-def gen_scenes(envs):
+def gen_scenes(envs, only=None):
     plan = [(c, 2) for c in synthetic.BASELINE_CONFIGS] + \
-           [(c, 1) for c in synthetic.CONFIGS if c not in synthetic.BASELINE_CONFIGS]
+           [(c, 1) for c in synthetic.CONFIGS if c not in synthetic.BASELINE_CONFIGS and c not in synthetic.MAZE_CONFIGS] + \
+           [(c, 2) for c in synthetic.MAZE_CONFIGS]
     for cfg, n_envs in plan:
+        if only is not None and cfg not in only:
+            continue
         arrays = {}
         for e in range(n_envs):
             scene = synthetic.make_scene(cfg, e)
@@ -375,6 +378,43 @@ class _FakeCameraP(_FakeP):
         return w, h, None, db.copy(), raw.copy()
 
 
+def gen_maze_paths(envs):
+    """Movement paths on the maze environments (large_doors / large_tunnels / large_rooms,
+    envs.py:528-551): OccupancyMap.shortest_path between random free positions on each agent's fully
+    observed map, mostly across the dividers.  Also the longest waypoint list seen, which bounds the
+    intention path (RobotController.get_intention_path, envs.py:1475-1476: at most len(path) + 1
+    points) against SIMAPS_MAX_PATH."""
+    out = {}
+    rs = np.random.RandomState(5151)
+    longest = 0
+    for cfg in ('lifting_4-large_doors', 'lifting_4-large_tunnels', 'lifting_4-large_rooms'):
+        for e in range(3):
+            scene = synthetic.make_scene(cfg, 70 + e, observe_all=True)
+            env = build_env(envs, scene)
+            rw, rl = scene['room_width'], scene['room_length']
+            H, W = scene['H'], scene['W']
+            X, Y = synthetic.pixel_center_positions(H, W)
+            points = np.stack([X, Y, np.full_like(X, 0.02)], axis=2)
+            for a in range(2):
+                m = envs.Mapper(env, env.robots[a])
+                seg = np.where(scene['occupancy'][a] == 1, K.SEG_VALUES['obstacle'], K.SEG_VALUES['floor'])
+                m.global_occupancy_map.update(points, seg, K.SEG_VALUES['obstacle'])
+                for q in range(16):
+                    src = (float(rs.uniform(-rl / 2 + 0.05, rl / 2 - 0.05)), float(rs.uniform(0.05, rw / 2 - 0.05)), 0)
+                    tgt = (float(rs.uniform(-rl / 2 + 0.05, rl / 2 - 0.05)), float(rs.uniform(-rw / 2 + 0.05, -0.05)), 0)
+                    if q % 4 == 3:
+                        src, tgt = tgt, src
+                    path = m.shortest_path(src, tgt)
+                    longest = max(longest, len(path))
+                    key = '%s_e%d_a%d_q%d' % (cfg, e, a, q)
+                    out[key + '_src'] = np.array(src[:2], dtype=np.float64)
+                    out[key + '_tgt'] = np.array(tgt[:2], dtype=np.float64)
+                    out[key + '_path'] = np.array([p[:2] for p in path], dtype=np.float64)
+    out['longest_path'] = np.array(longest, dtype=np.int32)
+    np.savez_compressed(os.path.join(HERE, 'maze_paths.npz'), **out)
+    print('wrote maze path goldens, longest path %d waypoints' % longest)
+
+
 def gen_grid_paths(sp):
     """GridGraph(grid).shortest_path(source, target) (pyx:121-154) on raw cells: the reference demo
     sample (random free / blocked pairs) and small random grids whose free cells take the values
@@ -484,6 +524,10 @@ def main():
         gen_ingest(envs)
     if 'grid_paths' in which or not sys.argv[1:]:
         gen_grid_paths(sp)
+    if 'maze' in which and 'scenes' not in which:
+        gen_scenes(envs, only=synthetic.MAZE_CONFIGS)
+    if 'maze_paths' in which or not sys.argv[1:]:
+        gen_maze_paths(envs)
 
 
 if __name__ == '__main__':

@@ -160,6 +160,35 @@ def test_shortest_path_reference_goldens(V):
     assert nontrivial >= 40
 
 
+def test_maze_paths_reference_goldens(V):
+    """Movement paths on the maze environments (large_doors / tunnels / rooms) vs the reference's
+    own OccupancyMap.shortest_path: long detours through doors and tunnels, exactly."""
+    synthetic, vector_env = V
+    from simaps import batch
+    z = G.load('maze_paths.npz')
+    groups = {}
+    for k in z.files:
+        if not k.endswith('_path') or k == 'longest_path':
+            continue
+        key = k[:-len('_path')]
+        head, q = key.rsplit('_q', 1)
+        cfg, rest = head.rsplit('_e', 1)
+        e, a = (int(x) for x in rest.split('_a'))
+        groups.setdefault(cfg, []).append((e, a, key))
+    assert len(groups) == 3
+    longest = 0
+    for cfg, items in groups.items():
+        scenes = [synthetic.make_scene(cfg, 70 + e, observe_all=True) for e in range(3)]
+        b = batch.StateBatch(scenes)
+        slots = [b.agents.index((e, a)) for e, a, _ in items]
+        got = b.shortest_paths(np.stack([z[k + '_src'] for _, _, k in items]),
+                               np.stack([z[k + '_tgt'] for _, _, k in items]), slots=slots)
+        for (e, a, key), path in zip(items, got):
+            assert np.array_equal(np.array([p[:2] for p in path]), z[key + '_path']), key
+            longest = max(longest, len(path))
+    assert longest == int(z['longest_path']) >= 5
+
+
 def test_ingest_reference_goldens(V):
     """Observation ingest through simaps_ingest vs the reference's own
     Mapper.update on the committed frames (forward-facing and overhead cameras)."""

@@ -85,7 +85,9 @@ def test_layout_chw_matches_hwc(S):
                                  'lifting_2_throwing_2-large_empty', 'rescue_4-small_empty',
                                  'lifting_4-small_divider-history', 'lifting_4-large_empty-line',
                                  'lifting_4-small_empty-circle', 'lifting_4-small_divider-spatial',
-                                 'lifting_4-large_empty-nonspatial', 'lifting_2_pushing_2-large_empty-all'])
+                                 'lifting_4-large_empty-nonspatial', 'lifting_2_pushing_2-large_empty-all',
+                                 'lifting_4-large_doors', 'lifting_4-large_tunnels', 'lifting_4-large_rooms',
+                                 'lifting_2_throwing_2-large_doors', 'lifting_4-large_rooms-history'])
 def test_oracle_parity_fresh_seeds(S, cfg):
     """Seeds never used for the goldens: every agent of 6 envs vs the (golden-pinned) oracle."""
     batch, K, synthetic = S
@@ -152,7 +154,8 @@ def _channel_invariants(st, flags):
 
 
 @pytest.mark.parametrize('cfg,envs', [('pushing_4-large_empty', 256), ('lifting_2_throwing_2-large_empty', 1024),
-                                      ('rescue_4-small_empty', 2048)])
+                                      ('rescue_4-small_empty', 2048), ('lifting_4-large_tunnels', 256),
+                                      ('lifting_4-large_rooms', 256)])
 def test_full_size_baseline_configs(S, cfg, envs):
     """The other BASELINE configs at their full single-launch sizes (1,024 / 4,096 / 8,192 stacks,
     i.e. 4-32 workgroups per CU back to back): no device fault, status clean for every agent,

@@ -194,3 +194,21 @@ def test_oracle_grid_shortest_path_vs_reference():
             key = 'rand_%d_%d' % (m, k)
             got = np.array(O.grid_shortest_path(z['rand_%d_grid' % m], z[key + '_src'], z[key + '_tgt'])).reshape(-1, 2)
             assert np.array_equal(got, z[key + '_path']), key
+
+
+def test_oracle_maze_paths_vs_reference():
+    """OccupancyMap.shortest_path on the maze environments (large_doors / tunnels / rooms) from the
+    reference itself; the longest path bounds the intention path against SIMAPS_MAX_PATH."""
+    from simaps import _lib, synthetic
+    z = G.load('maze_paths.npz')
+    assert int(z['longest_path']) + 1 <= _lib.MAX_PATH
+    keys = sorted(k[:-len('_path')] for k in z.files if k.endswith('_path') and k != 'longest_path')
+    cache = {}
+    for key in keys:
+        head, q = key.rsplit('_q', 1)
+        cfg, rest = head.rsplit('_e', 1)
+        e, a = (int(x) for x in rest.split('_a'))
+        if (cfg, e, a) not in cache:
+            cache[(cfg, e, a)] = O.AgentOracle(synthetic.make_scene(cfg, 70 + e, observe_all=True), a)
+        got = np.array(cache[(cfg, e, a)].shortest_path(z[key + '_src'], z[key + '_tgt']), dtype=np.float64)
+        assert np.array_equal(got, z[key + '_path']), key

@@ -1,0 +1,60 @@
+"""Summarise tools/sq_profile.sh passes: per-dispatch SQ / GRBM counters of get_state_kernel
+(median over dispatches, summed over XCD / SE instances), per-wave figures and the VALU-issue roof.
+
+    python tools/sq_summary.py <dir> [<dir> ...]      (gpurun_out/sq_<tag>)
+
+SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* / SQ_BUSY_CYCLES count quad-cycles
+(MI355X_MICROARCH.md, rocprofv3 PMC slots); WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES.
+VALU roof: a SIMD issues one wave64 VALU instruction per quad-cycle, so the per-SIMD VALU demand is
+SQ_INSTS_VALU / (4 SIMDs x CUs used) quad-cycles per launch; against the waves' lifetime it gives
+the fraction of the kernel the VALU pipes are busy (1.0 = VALU-issue bound).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+KERNEL = 'get_state_kernel'
+
+
+def load(d):
+    per = collections.defaultdict(float)
+    for f in sorted(glob.glob(os.path.join(d, 'pass*_counter_collection.csv'))):
+        for r in csv.DictReader(open(f)):
+            if KERNEL in r['Kernel_Name']:
+                per[(r['Counter_Name'], os.path.basename(f), r['Dispatch_Id'])] += float(r['Counter_Value'])
+    agg = collections.defaultdict(list)
+    for (c, _, _), v in per.items():
+        agg[c].append(v)
+    return {c: statistics.median(v) for c, v in agg.items()}
+
+
+def summarise(d):
+    c = load(d)
+    waves = c['SQ_WAVES']
+    wg = waves / 16
+    cus = min(wg, 256)
+    out = {'dir': d, 'counters': c, 'waves': waves}
+    per_wave = {k: c[k] / waves for k in c if k.startswith('SQ_INSTS_')}
+    out['insts_per_wave'] = per_wave
+    wave_q = c['SQ_WAVE_CYCLES'] / waves
+    out['wave_lifetime_qcycles'] = wave_q
+    out['share_of_wave_cycles'] = {k: c[k] / c['SQ_WAVE_CYCLES'] for k in
+                                   ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY', 'SQ_ACTIVE_INST_VALU',
+                                    'SQ_ACTIVE_INST_LDS', 'SQ_ACTIVE_INST_SCA', 'SQ_WAIT_INST_LDS') if k in c}
+    # per-SIMD VALU demand (quad-cycles) against the kernel span per CU (workgroups run back to back)
+    valu_per_simd = c['SQ_INSTS_VALU'] / (4 * cus)
+    span_q = wave_q * (wg / cus)
+    out['valu_roof'] = {'valu_qcycles_per_simd': valu_per_simd, 'kernel_qcycles_per_cu': span_q,
+                        'valu_busy_frac': valu_per_simd / span_q}
+    if 'SQ_LDS_BANK_CONFLICT' in c:
+        out['lds_bank_conflict_frac'] = c['SQ_LDS_BANK_CONFLICT'] / c['SQ_LDS_IDX_ACTIVE']
+    return out
+
+
+if __name__ == '__main__':
+    res = [summarise(d) for d in sys.argv[1:]]
+    print(json.dumps(res, indent=1))
