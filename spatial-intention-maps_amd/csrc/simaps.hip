@@ -48,25 +48,40 @@ using namespace simaps;
 namespace {
 
 constexpr int NT = 1024;
-#ifdef SIMAPS_PHASE_STAMPS
-// Diagnostic build only (libsimaps_prof.so): per-workgroup s_memrealtime (100 MHz) stamps.
+#if defined(SIMAPS_PHASE_STAMPS) || defined(SIMAPS_LIGHT_STAMPS)
+// Diagnostic builds only (libsimaps_prof.so): per-workgroup s_memrealtime (100 MHz) stamps.
+// SIMAPS_LIGHT_STAMPS: only a few stamps and no added barriers (code as close to the product's as a
+// stamp build gets).
 constexpr int MAX_STAMP_WG = 8192, NSTAMP = 80;
 __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
+#ifdef SIMAPS_LIGHT_STAMPS
+#ifdef SIMAPS_LIGHT_SET
+#define STAMP_ON(k) (SIMAPS_LIGHT_SET(k))
+#else
+#define STAMP_ON(k) ((k) == 0 || (k) == 7 || (k) == 8 || (k) == 11 || (k) == 13 || (k) == 60 || (k) == 61 || (k) == 62)
+#endif
+#define STAMP_BAR()
+#else
+#define STAMP_ON(k) true
+#define STAMP_BAR() lds_barrier()
+#endif
 // (a barrier first, so a stamp marks the moment the SLOWEST wave finished the previous phase)
 #define STAMP(k)                                                                                 \
     do {                                                                                         \
-        lds_barrier();                                                                         \
-        if (threadIdx.x == 0 && blockIdx.x < MAX_STAMP_WG)                                       \
-            g_stamps[blockIdx.x * NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime();              \
+        if (STAMP_ON(k)) {                                                                       \
+            STAMP_BAR();                                                                         \
+            if (threadIdx.x == 0 && blockIdx.x < MAX_STAMP_WG)                                   \
+                g_stamps[blockIdx.x * NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime();          \
+        }                                                                                        \
     } while (0)
 #define STAMP_NB(k)                                                                              \
     do {                                                                                         \
-        if ((threadIdx.x & 63) == 0 && blockIdx.x < MAX_STAMP_WG)                                \
+        if (STAMP_ON(k) && (threadIdx.x & 63) == 0 && blockIdx.x < MAX_STAMP_WG)                 \
             g_stamps[blockIdx.x * NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime();              \
     } while (0)
 #define STAMP_CLK(k) /* shader-clock counter (s_memtime): with a realtime stamp, the clock rate */  \
     do {                                                                                         \
-        if ((threadIdx.x & 63) == 0 && blockIdx.x < MAX_STAMP_WG)                                \
+        if (STAMP_ON(k) && (threadIdx.x & 63) == 0 && blockIdx.x < MAX_STAMP_WG)                 \
             g_stamps[blockIdx.x * NSTAMP + (k)] = __builtin_amdgcn_s_memtime();                  \
     } while (0)
 #else
@@ -247,8 +262,6 @@ struct Shared {
     float red[3][16];
     float nonsp[2 * SIMAPS_MAX_ROBOTS];
     RobotP rob[SIMAPS_MAX_ROBOTS];
-    int colbest[2][SIMAPS_MAX_ROOM_W];
-    int envg[2][SIMAPS_MAX_ROOM_W];  // Voronoi envelope (rect columns) per source
     unsigned bar[4][4];              // group barriers {count, generation, timeout, -}: [0] sweep track, [1] render,
                                      // [2 + s] source s's sweep waves (rounds)
     int changed[2][3];               // per source, rotating per-round "some sweep improved a cell" flags
@@ -378,6 +391,51 @@ __device__ __forceinline__ void cspace_load(OccLoad<G> &L, const uint8_t *__rest
     }
 }
 
+// Byte loads + ballots straight into S.win, CH rows of loads in flight at a time (the sweep track's
+// fallback when the dword variant's alignment bounds fail): a few registers instead of NQ + NU.
+template <int G>
+__device__ __forceinline__ void win_from_bytes(SsspScratch &S, const uint8_t *__restrict__ occ, int H, int W, int i0,
+                                               int j0, int h, int w, int t)
+{
+    constexpr int NQ = 16384 / G, NU = 1024 / G, CH = 8;
+    static_assert(NQ % CH == 0, "whole chunks");
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)occ, (short)0, H * W, 0x00020000);
+    const int lane = t & 63, wave = t >> 6;
+    const int wh = h + 2 * RMAX, ww = w + 2 * RMAX;
+    const int c = t & 127, r0 = t >> 7;
+#pragma unroll 1
+    for (int q0 = 0; q0 < NQ; q0 += CH) {
+        uint32_t v[CH];
+#pragma unroll
+        for (int k = 0; k < CH; k++) {
+            const int rr = r0 + (G / 128) * (q0 + k), gi = i0 - RMAX + rr, gj = j0 - RMAX + c;
+            const bool in = ((unsigned)rr < (unsigned)wh) & ((unsigned)c < (unsigned)ww) & ((unsigned)gi < (unsigned)H) &
+                            ((unsigned)gj < (unsigned)W);
+            v[k] = __builtin_amdgcn_raw_buffer_load_b8(rs, in ? gi * W + gj : -1, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < CH; k++) {
+            const int rr = r0 + (G / 128) * (q0 + k);
+            const uint64_t m = __ballot(v[k] != 0);
+            if (lane == 0 && rr < wh) S.win[rr][wave & 1] = m;
+        }
+    }
+    uint32_t v2[NU];
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const int rr = 8 * wave + (lane >> 3) + (G / 8) * u, cc = 128 + (lane & 7), gi = i0 - RMAX + rr, gj = j0 - RMAX + cc;
+        const bool in = ((unsigned)rr < (unsigned)wh) & ((unsigned)cc < (unsigned)ww) & ((unsigned)gi < (unsigned)H) &
+                        ((unsigned)gj < (unsigned)W);
+        v2[u] = __builtin_amdgcn_raw_buffer_load_b8(rs, in ? gi * W + gj : -1, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const int rb = 8 * wave + (G / 8) * u;
+        const uint64_t m = __ballot(v2[u] != 0);
+        if (lane < 8 && rb + lane < wh) S.win[rb + lane][2] = (m >> (8 * lane)) & 0xffu;
+    }
+}
+
 // Dword variant (the sweep track, G threads, rows 4-byte aligned in a map whose window columns lie
 // inside it): each load covers 4 window columns from the aligned column a0 = (j0 - RMAX) & ~3, so the
 // window rows land shifted by sub = (j0 - RMAX) - a0 bits, which the dilation's funnel shifts absorb.
@@ -464,21 +522,26 @@ __device__ __forceinline__ unsigned row16_or(unsigned x)
 // With dist (the get_state sweep track), the 16 lanes that compute a row's free bits also write
 // that row of every distance array (free +inf, blocked / border -inf; sssp_init_sources then sets
 // the snapped sources to 0): no separate init pass over the arrays.
+// The occupancy window comes from registers loaded earlier (L4: dword loads; L: byte loads) or, with
+// neither, is loaded here in chunks (win_from_bytes on occ / H / W / i0 / j0).
 template <int G>
-__device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L, int h, int w, int r, const Group &g,
-                                             float *dist = nullptr, int nsrc = 0, const OccLoad4<G> *L4 = nullptr)
+__device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> *L, int h, int w, int r, const Group &g,
+                                             float *dist = nullptr, int nsrc = 0, const OccLoad4<G> *L4 = nullptr,
+                                             const uint8_t *occ = nullptr, int H = 0, int W = 0, int i0 = 0, int j0 = 0)
 {
     const int t = g.t, lane = t & 63, wave = t >> 6;
     const int whM = h + 2 * RMAX, wwM = w + 2 * RMAX;
     const int sub = L4 ? L4->sub : 0;  // window bit k = column k - sub (dword loads)
     if (L4) {
         win_from_dwords<G>(S, *L4, whM, t);
+    } else if (!L) {
+        win_from_bytes<G>(S, occ, H, W, i0, j0, h, w, t);
     } else {
         const int c = t & 127, r0 = t >> 7;
 #pragma unroll
         for (int q = 0; q < OccLoad<G>::NQ; q++) {
             const int rr = r0 + (G / 128) * q;
-            const uint64_t m = __ballot(L.v[q] != 0);  // 0 outside the window (cspace_load)
+            const uint64_t m = __ballot(L->v[q] != 0);  // 0 outside the window (cspace_load)
             if (lane == 0 && rr < whM) S.win[rr][wave & 1] = m;
 #ifdef SIMAPS_PHASE_STAMPS
             if (q == 0 && t == 0) STAMP_NB(46);
@@ -490,7 +553,7 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> &L
 #pragma unroll
         for (int u = 0; u < OccLoad<G>::NU; u++) {
             const int rb = 8 * wave + (G / 8) * u, rr = rb + (lane >> 3), cc = 128 + (lane & 7);
-            const uint64_t m = __ballot(L.v2[u] != 0);
+            const uint64_t m = __ballot(L->v2[u] != 0);
             if (lane < 8 && rb + lane < whM) S.win[rb + lane][2] = (m >> (8 * lane)) & 0xffu;
         }
     }
@@ -619,68 +682,54 @@ __device__ __forceinline__ void snap_sources(Shared &sh, SsspScratch &S, int nsr
         }
     }
     g.sync();
+    if (tid == 0) STAMP_NB(76);
     bool slow = false;
     for (int s = 0; s < nsrc; s++) slow |= !sh.src_ok[s];
     if (!slow) return;
-    // pass 1 (scipy: per column along axis 0): nearest free row of each rect column, ties low
-    for (int item = tid; item < nsrc * 128; item += g.n) {  // w <= 120 columns per source
-        const int s = item >> 7, c = item & 127;
-        if (c >= w || sh.src_ok[s]) continue;
-        const int qi = sh.src_q[s][0];
-        int best = -1, bestd = 1 << 30;
-        for (int rr = 0; rr < h; rr++) {
-            if (b_test(S.freeb[rr], c)) {
-                const int d = abs(i0 + rr - qi);
-                if (d < bestd) { bestd = d; best = i0 + rr; }
-            }
-        }
-        sh.colbest[s][c] = best;
-    }
-    g.sync();
-    // pass 2 (scipy _VoronoiFT along axis 1), one lane per source
-    if ((tid & 63) == 0 && (tid >> 6) < nsrc && !sh.src_ok[tid >> 6]) {
-        const int s = tid >> 6;
-        const int qi = sh.src_q[s][0], qj = sh.src_q[s][1];
-        {
-            int *g = sh.envg[s];  // envelope (indices into rect columns)
-            int l = -1;
-            for (int c = 0; c < w; c++) {
-                const int f0 = sh.colbest[s][c];
-                if (f0 < 0) continue;
-                const long long fd = j0 + c;
-                const long long tw = (long long)f0 - qi;
-                const long long wR = tw * tw;
-                while (l >= 1) {
-                    const int c1 = g[l], c2 = g[l - 1];
-                    const long long f1d = j0 + c1;
-                    const long long a = f1d - (j0 + c2);
-                    const long long b = fd - f1d;
-                    const long long tu = (long long)sh.colbest[s][c2] - qi, tv = (long long)sh.colbest[s][c1] - qi;
-                    const long long uR = tu * tu, vR = tv * tv;
-                    const long long cc = a + b;
-                    if (cc * vR - b * uR - a * wR - a * b * cc <= 0) break;
-                    --l;
-                }
-                ++l;
-                g[l] = c;
-            }
-            if (l >= 0) {
-                const int maxl = l;
-                l = 0;
-                for (int ii = 0; ii <= qj; ii++) {
-                    long long t0 = (long long)sh.colbest[s][g[l]] - qi, t1 = (long long)(j0 + g[l]) - ii;
-                    long long d1 = t0 * t0 + t1 * t1;
-                    while (l < maxl) {
-                        t0 = (long long)sh.colbest[s][g[l + 1]] - qi;
-                        t1 = (long long)(j0 + g[l + 1]) - ii;
-                        const long long d2 = t0 * t0 + t1 * t1;
-                        if (d1 <= d2) break;
-                        d1 = d2;
-                        ++l;
+    // scipy's feature transform at the query (pass 1 along axis 0: per column the nearest free row,
+    // ties low; pass 2 along axis 1 at the query row: the lower envelope of (row - qi)^2 + (col - qj)^2,
+    // which yields the minimising column, the lowest one on a tie -- a member is dropped only if its
+    // interval is strictly empty and the query scan stops at the first member the next one does not
+    // strictly beat; checked against scipy's serial envelope code on 2 x 10^5 random cases, 1.2 x 10^4
+    // of them with ties).  One wave per source, lane l owning rect columns l and l + 64: rows are
+    // scanned outward from the query row (qr - d before qr + d: ties low), every column at once,
+    // until no column still searching can reach the best (d^2 + dc^2, column) key found so far.
+    const int lane = tid & 63, wv = tid >> 6;
+    if (wv < nsrc && !sh.src_ok[wv]) {
+        const int s = wv;
+        const int qi = __builtin_amdgcn_readfirstlane(sh.src_q[s][0]);
+        const int qj = __builtin_amdgcn_readfirstlane(sh.src_q[s][1]);
+        const int qr = qi - i0, qc = qj - j0;
+        int rowd[2] = {-1, -1}, row[2] = {0, 0};  // per column: the nearest free row's distance / row
+        int best = 0x7fffffff;                    // (d^2 + dc^2) << 7 | column: the lexicographic minimum
+        for (int d = 0; d <= h + 128; d++) {       // (|qr| is bounded by the grid; d > h + |qr| finds nothing)
+            const long long dd = (long long)d * d;
+            if (dd << 7 > (long long)best) break;  // no column still searching can reach the best key
+            const int ra = qr - d, rb = qr + d;
+            const bool va = ra >= 0 && ra < h, vb = d > 0 && rb >= 0 && rb < h;
+            if (!va && !vb && ra < 0 && rb >= h) break;  // every row visited
+            const B128 fa = va ? S.freeb[ra] : B128{0ull, 0ull};
+            const B128 fb = vb ? S.freeb[rb] : B128{0ull, 0ull};
+            for (int k = 0; k < 2; k++) {
+                const int c = lane + 64 * k;
+                if (c < w && rowd[k] < 0) {
+                    if (b_test(fa, c)) { rowd[k] = d; row[k] = ra; }
+                    else if (b_test(fb, c)) { rowd[k] = d; row[k] = rb; }
+                    if (rowd[k] >= 0) {
+                        const int key = ((d * d + (c - qc) * (c - qc)) << 7) | c;
+                        best = min(best, key);
                     }
                 }
-                sh.src_s[s][0] = sh.colbest[s][g[l]];
-                sh.src_s[s][1] = j0 + g[l];
+            }
+            for (int off = 32; off > 0; off >>= 1) best = min(best, __shfl_xor(best, off));
+        }
+        if (best != 0x7fffffff) {  // (no free cell at all: src_ok stays 0)
+            const int c = best & 127;
+            const int owner = c & 63, k = c >> 6;
+            const int r = __shfl(k ? row[1] : row[0], owner);
+            if (lane == 0) {
+                sh.src_s[s][0] = i0 + r;
+                sh.src_s[s][1] = j0 + c;
                 sh.src_ok[s] = 1;
             }
         }
@@ -1950,14 +1999,13 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
 {
     const int t = g.t, H = cfg.H, W = cfg.W;
     const int h = cfg.room_h, w = cfg.room_w;
-    OccLoad<G> occ_regs;  // issued first: they depend on the map slot only
-    OccLoad4<G> occ4;
-    const bool use4 = G == 512 && occ4_ok(H, W, cfg.room_j0);  // dword loads: 9 per thread instead of 34
+    OccLoad4<G> occ4;  // issued first: they depend on the map slot only
+    const bool use4 = occ4_ok(H, W, cfg.room_j0);  // dword loads: 9 (G = 512) / 18 (G = 256) per thread
 #ifdef SIMAPS_PHASE_STAMPS
     if (t == 0 && ag.map_slot >= 0) STAMP_NB(43);  // the agent record has landed
 #endif
-    if (use4) cspace_load4<G>(occ4, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, h, t);
-    else cspace_load<G>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, h, w, t);
+    const uint8_t *occ = occupancy + (size_t)ag.map_slot * H * W;
+    if (use4) cspace_load4<G>(occ4, occ, H, W, cfg.room_i0, cfg.room_j0, h, t);
     const simaps_robot *rb = robots + ev.robot_off;
     if (t == 0) {
         sh.h = h;
@@ -1976,7 +2024,8 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
         }
         sh.nsrc = ns;
     }
-    build_cspace<G>(S, occ_regs, h, w, geo.cspace_r[rb[ag.robot].type], g, dist, nsrc, use4 ? &occ4 : nullptr);  // (its first sync publishes sh)
+    build_cspace<G>(S, nullptr, h, w, geo.cspace_r[rb[ag.robot].type], g, dist, nsrc, use4 ? &occ4 : nullptr, occ, H, W,
+                    cfg.room_i0, cfg.room_j0);  // (its first sync publishes sh)
     if (t == 0) STAMP_NB(2);
     if (dbg.cspace) {
         for (int k = t; k < h * w; k += g.n) dbg.cspace[(size_t)n * h * w + k] = b_test(S.freeb[k / w], k % w) ? 1 : 0;
@@ -2260,6 +2309,12 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             else { o[0] = o[1] = o[2] = o[3] = -1; }
         }
     }
+#ifdef SIMAPS_DIAG_V2  // diagnostic: a global store that never executes
+    if (tid == 0 && C < 0) state[0] = 1.0f;
+#endif
+#ifdef SIMAPS_DIAG_V3  // diagnostic: a realtime read consumed by an empty asm
+    if (tid == 0) { const unsigned long long tt = __builtin_amdgcn_s_memrealtime(); asm volatile("" ::"s"(tt)); }
+#endif
     if (tid == 0) {
         const unsigned f = group_faults(sh.bar, sh.rounds, nsrc);
         post_faults(fault, f);
@@ -2354,7 +2409,7 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
         sh.nsrc = 1;
     }
     lds_barrier();
-    build_cspace<NT>(S, occ_regs, sh.h, sh.w, sh.r, whole_wg());
+    build_cspace<NT>(S, &occ_regs, sh.h, sh.w, sh.r, whole_wg());
     snap_sources(sh, S, 1, whole_wg());
     const bool src_ok = sh.src_ok[0];
     sssp(sh, S, dist, 1);  // the source's distance image (GridGraph._spfa_with_cache, pyx:116-119)
@@ -2641,7 +2696,7 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
         sh.nsrc = 2;
     }
     lds_barrier();
-    build_cspace<NT>(S, occ_regs, sh.h, sh.w, sh.r, whole_wg());
+    build_cspace<NT>(S, &occ_regs, sh.h, sh.w, sh.r, whole_wg());
     double *o = out_xy + (size_t)n * max_pts * 2;
     // (1) straight line on cspace_thin between the unsnapped pixels (envs.py:2484-2486)
     if (tid < 64) {
@@ -2980,7 +3035,7 @@ extern "C" {
 
 int simaps_abi_version(void) { return SIMAPS_ABI_VERSION; }
 
-#ifdef SIMAPS_PHASE_STAMPS
+#if defined(SIMAPS_PHASE_STAMPS) || defined(SIMAPS_LIGHT_STAMPS)
 // Diagnostic build only: copy the stamp table (uint64 [8192][NSTAMP]) to host memory.
 int simaps_debug_read_stamps(unsigned long long *host_out)
 {

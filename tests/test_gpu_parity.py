@@ -201,6 +201,34 @@ def test_snap_slow_path_and_idle(S):
         assert _bitwise(st[n], O.agent_state(scenes[e], a))
 
 
+def test_snap_ties_on_maze_walls(S):
+    """EDT snap (scipy feature transform at the query, envs.py:2523-2524) for robots standing on the
+    large_rooms / large_tunnels dividers: every robot source needs the slow path, many with
+    equidistant free cells (the lowest minimal column wins, like scipy's envelope scan)."""
+    batch, K, synthetic = S
+    rs = np.random.RandomState(17)
+    scenes = []
+    for e in range(24):
+        cfg = 'lifting_4-large_rooms' if e % 2 == 0 else 'lifting_4-large_tunnels'
+        s = synthetic.make_scene(cfg, 900 + e, observe_all=e % 3 == 0)
+        for k, r in enumerate(s['robots']):
+            if cfg.endswith('rooms'):  # on the cross walls (through the room centre), +- a few pixels
+                x, y = (rs.uniform(-0.3, 0.3), rs.randint(-3, 4) / 96.0) if k % 2 else (rs.randint(-3, 4) / 96.0, rs.uniform(-0.3, 0.3))
+            else:  # inside the tunnel walls
+                x, y = rs.uniform(-0.45, 0.45), rs.uniform(-0.1, 0.1)
+            r['position'] = (float(x), float(y), 0)
+            r['waypoint_positions'][0] = r['position']
+        scenes.append(s)
+    b = batch.StateBatch(scenes)
+    dbg = b.alloc_debug()
+    st = b.as_hwc(b.render(debug=dbg)).cpu().numpy()
+    src = dbg['sources'].cpu().numpy()
+    snapped = int((src[:, 1, :2] != src[:, 1, 2:]).any(axis=1).sum())
+    assert snapped >= 48, snapped
+    for n, (e, a) in enumerate(b.agents):
+        assert _bitwise(st[n], O.agent_state(scenes[e], a)), (n, e, a)
+
+
 def test_sssp_grid_demo_known_answer(S):
     """shortest_paths/demo.py sample: distance 136.46806 and the full image, + 12 more sources."""
     batch, K, synthetic = S

@@ -25,6 +25,7 @@ def main():
     ap.add_argument('--config', default='lifting_4-small_divider')
     ap.add_argument('--envs', type=int, default=64)
     ap.add_argument('--layout', default='chw')
+    ap.add_argument('--dump', default=None, help='save the raw per-workgroup stamp table (.npy)')
     args = ap.parse_args()
     L = _lib.lib
     L.simaps_debug_read_stamps.argtypes = [ctypes.c_void_p]
@@ -39,6 +40,8 @@ def main():
     torch.cuda.synchronize()
     assert L.simaps_debug_read_stamps(st.ctypes.data) == 0
     st = st[:b.N].astype(np.int64)
+    if args.dump:
+        np.save(args.dump, st)
     us = lambda k1, k0: float(np.median((st[:, k1] - st[:, k0]) / 100.0))  # noqa: E731
     res = {'config': args.config, 'layout': args.layout, 'N': b.N,
            'total_us_median': us(6, 0), 'span_us': float((st[:, 6].max() - st[:, 0].min()) / 100.0),
