@@ -2808,101 +2808,227 @@ __device__ __forceinline__ int np_f32_to_i32(float v)
     return (v >= -2147483648.0f && v < 2147483648.0f) ? (int)v : INT32_MIN;
 }
 
-__global__ void __launch_bounds__(NT) ingest_kernel(simaps_config cfg, simaps_camera cam,
-                                                    const simaps_agent *__restrict__ agents,
-                                                    const simaps_seg_ids *__restrict__ seg_ids,
-                                                    const double *__restrict__ cam_params,
-                                                    const float *__restrict__ depth, const int32_t *__restrict__ seg_raw,
-                                                    float *__restrict__ overhead, uint8_t *__restrict__ occupancy,
-                                                    unsigned long long *__restrict__ keys)
+// Two passes, no recomputation and no reset pass:
+//   ingest_points_kernel  grid (chunks of INGEST_PTS camera pixels, frames): each point once -- its
+//                         map pixel, its obstacle bit (occupancy byte store) and its key (monotone z
+//                         bits | camera pixel + 1 | seg code).  The keys are max-reduced per map
+//                         pixel in LDS over the chunk's bounding box of map pixels (direct-mapped,
+//                         no hashing), then ONE global 64-bit atomicMax per touched pixel of the box.
+//                         A chunk's 2048 points hit only 14-1021 distinct pixels (the near rows of a
+//                         forward camera ~30), so atomics straight from the points serialised on a
+//                         few L2 lines (547 us per 256 frames); an LDS hash table cost 22 us of
+//                         init / scan on top of the reduction (95 us).  A box larger than the LDS
+//                         window falls back to global atomics per run of equal pixels.  The seg
+//                         value (a sum of 1/8 multiples < 2, exact in f32) travels as seg * 8 in the
+//                         key's low 4 bits, so the winner's value needs no second look-up.
+//   ingest_resolve_kernel grid (map blocks, frames): one coalesced sweep of the slot's key map (16 B
+//                         per lane): a nonzero key writes overhead = code / 8 and is zeroed again.
+// HBM per frame: 8 B per camera pixel (depth + seg) + 8 B per map pixel (key sweep) + the pixel
+// writes; the atomics resolve in L2 (a frame's key map is <= 0.4 MB).
+// (measured alternatives, 256 frames: 128- / 64-thread chunks +4 / +21 us, an 8192-entry window
+// +30 us (LDS occupancy), workgroups looping over several chunks of a frame with the next chunk's
+// loads in flight +4..28 us: the per-chunk barrier chain wants many chunks in flight, not fewer)
+constexpr int INGEST_WG = 256, INGEST_PPT = 8, INGEST_PTS = INGEST_WG * INGEST_PPT;
+constexpr int INGEST_WIN = 4096;  // LDS window entries (u64 keys) over a chunk's map-pixel box
+constexpr int INGEST_MAX_WC = 1024, INGEST_MAX_ROWS = 32;  // camera width; camera rows one chunk spans
+constexpr int INGEST_RES_WG = 256, INGEST_RES_KEYS = INGEST_RES_WG * 2 * 4;  // 2 keys per load, 4 loads
+
+// Camera.capture_image's frame (envs.py:1932-1940) in float32: position, principal, up, right.
+__device__ __forceinline__ void camera_frame(const double *P, float *F)
 {
-    __shared__ float F[12];  // camera position, principal, up, right (float32)
-    const int n = blockIdx.x, tid = threadIdx.x;
-    const int H = cfg.H, W = cfg.W, Hc = cam.height_px, Wc = cam.width_px, NP = Hc * Wc;
-    const simaps_agent ag = agents[n];
-    const simaps_seg_ids ids = seg_ids[ag.env];
-    if (tid == 0) {
-        const double *P = cam_params + 9 * (size_t)n;
-        float cp[3], pr[3], cu[3], up[3], rt[3];
-        for (int c = 0; c < 3; c++) {
-            cp[c] = (float)P[c];
-            pr[c] = (float)P[3 + c] - cp[c];
-            cu[c] = (float)P[6 + c];
+    float cp[3], pr[3], cu[3], up[3], rt[3];
+    for (int c = 0; c < 3; c++) {
+        cp[c] = (float)P[c];
+        pr[c] = (float)P[3 + c] - cp[c];
+        cu[c] = (float)P[6 + c];
+    }
+    const float n1 = sqrtf(dot3f(pr, pr));
+    for (int c = 0; c < 3; c++) pr[c] = pr[c] / n1;
+    const float d = dot3f(cu, pr);
+    for (int c = 0; c < 3; c++) up[c] = cu[c] - d * pr[c];
+    const float n2 = sqrtf(dot3f(up, up));
+    for (int c = 0; c < 3; c++) up[c] = up[c] / n2;
+    rt[0] = pr[1] * up[2] - pr[2] * up[1];
+    rt[1] = pr[2] * up[0] - pr[0] * up[2];
+    rt[2] = pr[0] * up[1] - pr[1] * up[0];
+    const float n3 = sqrtf(dot3f(rt, rt));
+    for (int c = 0; c < 3; c++) {
+        F[c] = cp[c];
+        F[3 + c] = pr[c];
+        F[6 + c] = up[c];
+        F[9 + c] = rt[c] / n3;
+    }
+}
+
+__device__ __forceinline__ int wave_min(int v)
+{
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int wave_max(int v)
+{
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+// Loads of a chunk: each lane owns INGEST_PPT consecutive camera pixels (one camera row segment;
+// neighbouring pixels of the near rows land on one map pixel, so the lane max-merges runs first).
+__device__ __forceinline__ void ingest_load(const float *db, const int32_t *raw, int k0, int NP, float (&dv)[INGEST_PPT],
+                                            int (&rv)[INGEST_PPT])
+{
+    static_assert(INGEST_PPT % 4 == 0, "16-B loads per lane and array");
+    if ((NP & 3) == 0 && k0 + INGEST_PPT <= NP) {  // 16-B aligned: frames start at n * NP, k0 % 4 == 0
+        const float4 *d4 = reinterpret_cast<const float4 *>(db + k0);
+        const int4 *r4 = reinterpret_cast<const int4 *>(raw + k0);
+#pragma unroll
+        for (int v = 0; v < INGEST_PPT / 4; v++) {
+            typedef float f4 __attribute__((ext_vector_type(4)));
+            typedef int i4 __attribute__((ext_vector_type(4)));
+            const f4 d = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(d4 + v));
+            const i4 r = __builtin_nontemporal_load(reinterpret_cast<const i4 *>(r4 + v));
+            dv[4 * v] = d.x, dv[4 * v + 1] = d.y, dv[4 * v + 2] = d.z, dv[4 * v + 3] = d.w;
+            rv[4 * v] = r.x, rv[4 * v + 1] = r.y, rv[4 * v + 2] = r.z, rv[4 * v + 3] = r.w;
         }
-        const float n1 = sqrtf(dot3f(pr, pr));
-        for (int c = 0; c < 3; c++) pr[c] = pr[c] / n1;
-        const float d = dot3f(cu, pr);
-        for (int c = 0; c < 3; c++) up[c] = cu[c] - d * pr[c];
-        const float n2 = sqrtf(dot3f(up, up));
-        for (int c = 0; c < 3; c++) up[c] = up[c] / n2;
-        rt[0] = pr[1] * up[2] - pr[2] * up[1];
-        rt[1] = pr[2] * up[0] - pr[0] * up[2];
-        rt[2] = pr[0] * up[1] - pr[1] * up[0];
-        const float n3 = sqrtf(dot3f(rt, rt));
-        for (int c = 0; c < 3; c++) {
-            F[c] = cp[c];
-            F[3 + c] = pr[c];
-            F[6 + c] = up[c];
-            F[9 + c] = rt[c] / n3;
+    } else {
+#pragma unroll
+        for (int q = 0; q < INGEST_PPT; q++) {
+            dv[q] = k0 + q < NP ? db[k0 + q] : 0.0f;
+            rv[q] = k0 + q < NP ? raw[k0 + q] : 0;
         }
     }
-    __syncthreads();
-    const float c1 = (float)(cam.far_m * cam.near_m), cfar = (float)cam.far_m, cfn = (float)(cam.far_m - cam.near_m);
-    const float cx2 = (float)cam.cx2, cy2 = (float)cam.cy2;
-    const float h2 = (float)((double)H / 2), w2 = (float)((double)W / 2);
+}
+
+// grid (chunks, frames)
+__global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
+    simaps_config cfg, simaps_camera cam, const simaps_agent *__restrict__ agents,
+    const simaps_seg_ids *__restrict__ seg_ids, const double *__restrict__ cam_params,
+    const float *__restrict__ depth, const int32_t *__restrict__ seg_raw, uint8_t *__restrict__ occupancy,
+    unsigned long long *__restrict__ keys)
+{
+    __shared__ unsigned long long win[INGEST_WIN];
+    __shared__ float F[12], pxT[INGEST_MAX_WC], pyT[INGEST_MAX_ROWS];
+    __shared__ int box[4];  // min i, -max i, min j, -max j of the chunk's map pixels
+    const int n = blockIdx.y, tid = threadIdx.x;
+    const int H = cfg.H, W = cfg.W, Hc = cam.height_px, Wc = cam.width_px, NP = Hc * Wc;
     const float *db = depth + (size_t)n * NP;
     const int32_t *raw = seg_raw + (size_t)n * NP;
+    const int k0 = blockIdx.x * INGEST_PTS + tid * INGEST_PPT;
+    float dv[INGEST_PPT];
+    int rv[INGEST_PPT];
+    // issue the chunk's loads first: the per-chunk tables below hide their latency
+    ingest_load(db, raw, k0, NP, dv, rv);
+    const simaps_agent ag = agents[n];
+    const simaps_seg_ids ids = seg_ids[ag.env];
+    const float c1 = (float)(cam.far_m * cam.near_m), cfar = (float)cam.far_m, cfn = (float)(cam.far_m - cam.near_m);
+    const float cx2 = (float)cam.cx2, cy2 = (float)cam.cy2;
+    // per chunk once: the camera frame (one lane) and the pixel_x / pixel_y tables of its columns and
+    // rows (envs.py:1946-1947; the same float32 divisions every point would repeat)
+    const int row0 = (blockIdx.x * INGEST_PTS) / Wc;
+    if (tid == 0) camera_frame(cam_params + 9 * (size_t)n, F);
+    if (tid < 4) box[tid] = INT32_MAX;
+    for (int j = tid; j < Wc; j += INGEST_WG) pxT[j] = cx2 * ((float)j / (float)Wc - 0.5f);
+    if (tid < INGEST_MAX_ROWS) pyT[tid] = cy2 * (0.5f - ((float)(row0 + tid) + 1.0f) / (float)Hc);
+    const float h2 = (float)((double)H / 2), w2 = (float)((double)W / 2);
     const size_t base = (size_t)ag.map_slot * H * W;
-    // point k -> (map pixel, z key, seg); the same float32 expression in every pass
-    auto point = [&](int k, int &pix, unsigned long long &key, float &seg) {
-        const int i = k / Wc, j = k - i * Wc;
-        const float dep = c1 / (cfar - cfn * db[k]);
-        const float px = cx2 * ((float)j / (float)Wc - 0.5f);
-        const float py = cy2 * (0.5f - ((float)i + 1.0f) / (float)Hc);
-        float p[3];
-        for (int c = 0; c < 3; c++) {
-            float t = F[3 + c] + px * F[9 + c];
-            t = t + py * F[6 + c];
-            p[c] = F[c] + dep * t;
+    {
+        __syncthreads();
+        int pix[INGEST_PPT];
+        unsigned long long key[INGEST_PPT];
+        int imin = INT32_MAX, imax = -1, jmin = INT32_MAX, jmax = -1;
+        int i = k0 / Wc, j = k0 - i * Wc;
+#pragma unroll
+        for (int q = 0; q < INGEST_PPT; q++, j = (j + 1 == Wc) ? (i++, 0) : j + 1) {
+            const int k = k0 + q;
+            pix[q] = -1;
+            key[q] = 0ull;
+            if (k >= NP) continue;
+            const float dep = c1 / (cfar - cfn * dv[q]);
+            const float px = pxT[j], py = pyT[i - row0];
+            float p[3];
+            for (int cc = 0; cc < 3; cc++) {
+                float t = F[3 + cc] + px * F[9 + cc];
+                t = t + py * F[6 + cc];
+                p[cc] = F[cc] + dep * t;
+            }
+            const int r = rv[q];
+            float seg = 0.125f * (r == 0 ? 1.0f : 0.0f);
+            seg += 0.25f * ((r >= ids.min_obstacle && r <= ids.max_obstacle) ? 1.0f : 0.0f);
+            if (ids.has_receptacle) seg += 0.375f * (r == ids.receptacle ? 1.0f : 0.0f);
+            seg += 0.5f * ((r >= ids.min_cube && r <= ids.max_cube) ? 1.0f : 0.0f);
+            int pi = np_f32_to_i32(floorf(h2 - p[1] * 96.0f)), pj = np_f32_to_i32(floorf(w2 + p[0] * 96.0f));
+            pi = pi < 0 ? 0 : (pi > H - 1 ? H - 1 : pi);
+            pj = pj < 0 ? 0 : (pj > W - 1 ? W - 1 : pj);
+            pix[q] = pi * W + pj;
+            imin = min(imin, pi), imax = max(imax, pi), jmin = min(jmin, pj), jmax = max(jmax, pj);
+            if (seg == 0.25f) occupancy[base + pix[q]] = 1;  // np.isclose(seg, obstacle) (seg values are exact)
+            // np.argsort order by z: float bits made unsigned-monotone, NaN last; equal z -> later pixel
+            const unsigned zb = __float_as_uint(p[2]);
+            const unsigned zk = p[2] != p[2] ? 0xffffffffu : ((zb & 0x80000000u) ? ~zb : (zb | 0x80000000u));
+            key[q] = ((unsigned long long)zk << 32) | (((unsigned)(k + 1) << 4) | (unsigned)(seg * 8.0f));
         }
-        const int r = raw[k];
-        seg = 0.125f * (r == 0 ? 1.0f : 0.0f);
-        seg += 0.25f * ((r >= ids.min_obstacle && r <= ids.max_obstacle) ? 1.0f : 0.0f);
-        if (ids.has_receptacle) seg += 0.375f * (r == ids.receptacle ? 1.0f : 0.0f);
-        seg += 0.5f * ((r >= ids.min_cube && r <= ids.max_cube) ? 1.0f : 0.0f);
-        int pi = np_f32_to_i32(floorf(h2 - p[1] * 96.0f)), pj = np_f32_to_i32(floorf(w2 + p[0] * 96.0f));
-        pi = pi < 0 ? 0 : (pi > H - 1 ? H - 1 : pi);
-        pj = pj < 0 ? 0 : (pj > W - 1 ? W - 1 : pj);
-        pix = pi * W + pj;
-        // np.argsort order by z: float bits made unsigned-monotone, NaN last; equal z -> later pixel
-        const unsigned zb = __float_as_uint(p[2]);
-        const unsigned zk = p[2] != p[2] ? 0xffffffffu : ((zb & 0x80000000u) ? ~zb : (zb | 0x80000000u));
-        key = ((unsigned long long)zk << 32) | (unsigned)(k + 1);
-    };
-    for (int k = tid; k < NP; k += NT) {
-        int pix;
-        unsigned long long key;
-        float seg;
-        point(k, pix, key, seg);
-        if (seg == 0.25f) occupancy[base + pix] = 1;  // np.isclose(seg, obstacle) (seg values are exact)
-        atomicMax(&keys[base + pix], key);
+        // runs of one map pixel inside the lane: the run's last entry carries the run's max key
+#pragma unroll
+        for (int q = 1; q < INGEST_PPT; q++)
+            if (pix[q] == pix[q - 1] && pix[q] >= 0) {
+                key[q] = key[q] > key[q - 1] ? key[q] : key[q - 1];
+                pix[q - 1] = -1;
+            }
+        // the chunk's box of map pixels
+        imin = wave_min(imin), imax = wave_max(imax), jmin = wave_min(jmin), jmax = wave_max(jmax);
+        if ((tid & 63) == 0 && imax >= 0)
+            atomicMin(&box[0], imin), atomicMin(&box[1], -imax), atomicMin(&box[2], jmin), atomicMin(&box[3], -jmax);
+        __syncthreads();
+        const int bi = box[0], bj = box[2], bh = -box[1] - bi + 1, bw = -box[3] - bj + 1;
+        const int area = bh * bw;  // block-uniform (a chunk holds >= 1 point)
+        if (area > INGEST_WIN) {   // fallback: global atomics per run
+#pragma unroll
+            for (int q = 0; q < INGEST_PPT; q++)
+                if (pix[q] >= 0) atomicMax(&keys[base + pix[q]], key[q]);
+            return;
+        }
+        for (int e = tid; e < area; e += INGEST_WG) win[e] = 0ull;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < INGEST_PPT; q++)
+            if (pix[q] >= 0) {
+                const int pi = pix[q] / W, pj = pix[q] - pi * W;
+                atomicMax(&win[(pi - bi) * bw + (pj - bj)], key[q]);
+            }
+        __syncthreads();
+        for (int e = tid; e < area; e += INGEST_WG) {
+            const unsigned long long v = win[e];
+            if (v) {
+                const int di = e / bw;
+                atomicMax(&keys[base + (size_t)((bi + di) * W + bj + (e - di * bw))], v);
+            }
+        }
     }
-    __syncthreads();
-    for (int k = tid; k < NP; k += NT) {  // the highest point of each pixel writes its seg value
-        int pix;
-        unsigned long long key;
-        float seg;
-        point(k, pix, key, seg);
-        if (__hip_atomic_load(&keys[base + pix], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key)
-            overhead[base + pix] = seg;
-    }
-    __syncthreads();
-    for (int k = tid; k < NP; k += NT) {  // leave the scratch zeroed for the next frame
-        int pix;
-        unsigned long long key;
-        float seg;
-        point(k, pix, key, seg);
-        keys[base + pix] = 0ull;
+}
+
+__global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
+    simaps_config cfg, const simaps_agent *__restrict__ agents, float *__restrict__ overhead,
+    unsigned long long *__restrict__ keys)
+{
+    const int n = blockIdx.y, HW = cfg.H * cfg.W;
+    const size_t base = (size_t)agents[n].map_slot * HW;
+    // H * W is even for every map here (checked on the host): 16-B aligned key pairs
+    ulonglong2 *kp = reinterpret_cast<ulonglong2 *>(keys + base);
+    float2 *op = reinterpret_cast<float2 *>(overhead + base);
+    const int npair = HW / 2;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int e = blockIdx.x * (INGEST_RES_KEYS / 2) + q * INGEST_RES_WG + threadIdx.x;
+        if (e >= npair) break;
+        const ulonglong2 kv = kp[e];
+        if ((kv.x | kv.y) == 0ull) continue;
+        if (kv.x && kv.y) {
+            op[e] = make_float2((float)(kv.x & 15ull) * 0.125f, (float)(kv.y & 15ull) * 0.125f);
+        } else if (kv.x) {
+            overhead[base + 2 * e] = (float)(kv.x & 15ull) * 0.125f;
+        } else {
+            overhead[base + 2 * e + 1] = (float)(kv.y & 15ull) * 0.125f;
+        }
+        kp[e] = make_ulonglong2(0ull, 0ull);
     }
 }
 
@@ -3148,8 +3274,17 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
     if (!agents || !seg_ids || !cam_params || !depth || !seg_raw || !overhead || !occupancy || !keys)
         return fail(SIMAPS_EINVAL, "NULL buffer");
     if ((rc = pending_faults())) return rc;
-    hipLaunchKernelGGL(ingest_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids, cam_params,
-                       depth, seg_raw, overhead, occupancy, reinterpret_cast<unsigned long long *>(keys));
+    const int np = cam->height_px * cam->width_px, hw = cfg->H * cfg->W;
+    if (cam->width_px > INGEST_MAX_WC || INGEST_PTS / cam->width_px + 2 > INGEST_MAX_ROWS)
+        return fail(SIMAPS_EUNSUPPORTED, "camera width %d outside [%d, %d]", cam->width_px, INGEST_PTS / (INGEST_MAX_ROWS - 2) + 1, INGEST_MAX_WC);
+    if (np >= (1 << 28)) return fail(SIMAPS_EUNSUPPORTED, "camera frame of %d pixels (key packs pixel + 1 in 28 bits)", np);
+    if (hw % 2) return fail(SIMAPS_EUNSUPPORTED, "map of %d pixels is odd (the key sweep reads pairs)", hw);
+    if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d frames per launch (grid y <= 65535)", N);
+    hipLaunchKernelGGL(ingest_points_kernel, dim3((np + INGEST_PTS - 1) / INGEST_PTS, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids,
+                       cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys));
+    hipLaunchKernelGGL(ingest_resolve_kernel, dim3((hw / 2 + INGEST_RES_KEYS / 2 - 1) / (INGEST_RES_KEYS / 2), N),
+                       dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg, agents, overhead,
+                       reinterpret_cast<unsigned long long *>(keys));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "ingest launch: %s", hipGetErrorString(e));
     return 0;

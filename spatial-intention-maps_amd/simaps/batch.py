@@ -304,6 +304,11 @@ class StateBatch:
         point cloud that updates the robot's overhead and occupancy maps in place on the device.
         camera: 'forward' (use_partial_observations) or 'overhead'; seg_ids: per-env dict of body ids
         (default: the synthetic scenes' ids).  The camera pose comes from the current descriptor."""
+        self.launch_ingest(self.prepare_ingest(depth, seg_raw, camera, slots, seg_ids), stream)
+
+    def prepare_ingest(self, depth, seg_raw, camera='forward', slots=None, seg_ids=None):
+        """The host half of ingest(): uploads the frames and packs the camera poses / body ids once;
+        launch_ingest() replays the device half (what tools/bench_extra.py times alone)."""
         from . import camera as cam_mod, synthetic
         spec = cam_mod.CAMERAS[camera]
         agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
@@ -325,14 +330,19 @@ class StateBatch:
         if getattr(self, '_keys', None) is None:
             self._keys = torch.zeros((self.N, self.H, self.W), dtype=torch.int64, device=self.device)
         cam = _lib.Camera(spec.height_px, spec.width_px, spec.near, spec.far, spec.cx2, spec.cy2)
-        if n == 0:
+        return {'n': n, 'cam': cam, 'agents': agents_d, 'ids': _to_dev(ids, self.device),
+                'params': torch.from_numpy(params).to(self.device), 'depth': dep, 'seg': seg}
+
+    def launch_ingest(self, prep, stream=None):
+        if prep['n'] == 0:
             return
-        ids_d, params_d = _to_dev(ids, self.device), torch.from_numpy(params).to(self.device)
         s, cur = launch_stream(self.device, stream)
         _lib.check(_lib.lib.simaps_ingest(
-            self.cfg, cam, n, _lib.ptr(agents_d), _lib.ptr(ids_d), _lib.ptr(params_d), _lib.ptr(dep), _lib.ptr(seg),
-            _lib.ptr(self.overhead), _lib.ptr(self.occupancy), _lib.ptr(self._keys), _lib.stream_handle(s)))
-        hold(s, cur, ids_d, params_d, dep, seg, agents_d, self.overhead, self.occupancy, self._keys)
+            self.cfg, prep['cam'], prep['n'], _lib.ptr(prep['agents']), _lib.ptr(prep['ids']), _lib.ptr(prep['params']),
+            _lib.ptr(prep['depth']), _lib.ptr(prep['seg']), _lib.ptr(self.overhead), _lib.ptr(self.occupancy),
+            _lib.ptr(self._keys), _lib.stream_handle(s)))
+        hold(s, cur, prep['ids'], prep['params'], prep['depth'], prep['seg'], prep['agents'], self.overhead,
+             self.occupancy, self._keys)
 
 
 def sssp_grid(grids, sources, window=None, stream=None):

@@ -232,6 +232,29 @@ def test_ingest_then_get_state_vs_oracle(V, kind):
         assert _bitwise(st[n], O.agent_state(s, a)), (e, a)
 
 
+def test_ingest_full_size_two_frames_vs_oracle(V):
+    """The BASELINE launch size (64 envs x 4 agents = 256 frames, 22 point chunks each) ingested
+    twice in a row (the second frame lands on the first's maps): every agent's overhead / occupancy
+    bitwise vs the oracle, and the key scratch back to zero after each launch."""
+    synthetic, vector_env = V
+    from simaps import batch, camera
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 400 + e) for e in range(64)]
+    b = batch.StateBatch(scenes)
+    spec = camera.CAMERAS['forward']
+    for rep in range(2):
+        frames = [synthetic.camera_images(scenes[e], a, 'forward', seed=97 * rep + 5 * e + a) for e, a in b.agents]
+        b.ingest(np.stack([f[0] for f in frames]), np.stack([f[1] for f in frames]), camera='forward')
+        assert int(b._keys.abs().sum()) == 0
+        for n, (e, a) in enumerate(b.agents):
+            s, r = scenes[e], scenes[e]['robots'][a]
+            O.ingest(s['overhead'][a], s['occupancy'][a], frames[n][0], frames[n][1],
+                     spec.params(r['position'][0], r['position'][1], r['heading']), spec, synthetic.SEG_IDS,
+                     s['receptacle_position'] is not None)
+    ov, oc = b.overhead.cpu().numpy(), b.occupancy.cpu().numpy()
+    for n, (e, a) in enumerate(b.agents):
+        assert _bitwise(ov[n], scenes[e]['overhead'][a]) and np.array_equal(oc[n], scenes[e]['occupancy'][a]), (e, a)
+
+
 def test_gridgraph_shortest_path_reference_goldens(V):
     """GridGraph.shortest_path (pyx:121-154) on raw cells against the reference itself: the demo
     sample (free / blocked / equal ends) and random grids with free values 1, 2, 255 (line of sight

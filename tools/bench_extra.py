@@ -93,6 +93,10 @@ def main():
 
 
 def bench_ingest(args):
+    """Ingest row: the two kernels alone (HIP events on the launch stream around K launches of the
+    device half, inputs resident) and end to end (host packing + upload + launch), with an HBM
+    roofline: algorithmic bytes per frame = 8 B per camera pixel (depth f32 + seg i32 read once)
+    + 5 B per map pixel (the overhead f32 / occupancy u8 maps it may rewrite)."""
     import oracle
     from simaps import camera
     scenes = [synthetic.make_scene(args.config, e) for e in range(args.envs)]
@@ -101,27 +105,51 @@ def bench_ingest(args):
     frames = [synthetic.camera_images(scenes[e], a, kind, seed=e * 8 + a) for e, a in b.agents]
     dep = torch.as_tensor(np.stack([f[0] for f in frames])).cuda()
     seg = torch.as_tensor(np.stack([f[1] for f in frames])).cuda()
-    dt = timed(lambda: b.ingest(dep, seg, camera=kind), args.steps, 3)
+    dt_e2e = timed(lambda: b.ingest(dep, seg, camera=kind), args.steps, 3)
+    prep = b.prepare_ingest(dep, seg, camera=kind)
+    for _ in range(3):
+        b.launch_ingest(prep)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    steps = max(args.steps, 50)
+    torch.cuda.synchronize()
+    e0.record(s)
+    for _ in range(steps):
+        b.launch_ingest(prep)
+    e1.record(s)
+    torch.cuda.synchronize()
+    kern_ms = e0.elapsed_time(e1) / steps
     spec = camera.CAMERAS[kind]
+    npix = spec.height_px * spec.width_px
+    alg = b.N * (8 * npix + 5 * b.H * b.W)
     n, el = 0, 0.0
     for k, (e, a) in enumerate(b.agents):
-        s = scenes[e]
-        r = s['robots'][a]
-        ov, oc = s['overhead'][a].copy(), s['occupancy'][a].copy()
+        sc = scenes[e]
+        r = sc['robots'][a]
+        ov, oc = sc['overhead'][a].copy(), sc['occupancy'][a].copy()
         t0 = time.perf_counter()
         oracle.ingest(ov, oc, frames[k][0], frames[k][1], spec.params(r['position'][0], r['position'][1], r['heading']),
-                      spec, synthetic.SEG_IDS, s['receptacle_position'] is not None)
+                      spec, synthetic.SEG_IDS, sc['receptacle_position'] is not None)
         el += time.perf_counter() - t0
         n += 1
         if el > args.cpu_budget:
             break
     print(json.dumps({'row': 'ingest', 'config': args.config, 'camera': kind, 'frames_per_launch': b.N,
-                      'points_per_frame': spec.height_px * spec.width_px, 'gpu_frames_per_s': b.N / dt,
-                      'gpu_ms_per_launch': dt * 1e3, 'cpu_oracle_frames_per_s': n / el, 'cpu_cores': 1,
+                      'points_per_frame': npix, 'gpu_frames_per_s': b.N / (kern_ms * 1e-3),
+                      'gpu_ms_per_launch': kern_ms, 'gpu_frames_per_s_end_to_end': b.N / dt_e2e,
+                      'gpu_ms_end_to_end': dt_e2e * 1e3,
+                      'roofline': {'bound': 'hbm', 'achieved': alg / (kern_ms * 1e-3) / 1e9, 'peak': 8000.0,
+                                   'unit': 'GB/s', 'frac': alg / (kern_ms * 1e-3) / 1e9 / 8000.0,
+                                   'algorithmic_bytes_per_frame': alg // b.N,
+                                   'kernels': 'ingest_points_kernel + ingest_resolve_kernel'},
+                      'cpu_oracle_frames_per_s': n / el, 'cpu_cores': 1,
                       'cpu_sample': '%d frames: capture_image points + argsort scatter + obstacle scatter' % n}),
           flush=True)
 
 
 if __name__ == '__main__':
-    main()
+    if '--ingest-only' in sys.argv:
+        sys.argv.remove('--ingest-only')
+    else:
+        main()
     bench_ingest(argparse.Namespace(config='lifting_4-small_divider', envs=64, steps=10, cpu_budget=8.0))
