@@ -2090,6 +2090,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const int n = blockIdx.x;
     const int tid = threadIdx.x;
     const int H = cfg.H, W = cfg.W;
+    if (tid == 0) STAMP_NB(77);  // kernel entry (dispatch skew)
 #ifdef SIMAPS_REPEAT  // diagnostic: run the body SIMAPS_REPEAT times (stamps keep the last, warm-cache pass)
 #pragma clang loop unroll(disable)
     for (int rep = 0; rep < SIMAPS_REPEAT + (int)(n >> 30); rep++) {

@@ -59,6 +59,9 @@ def main():
            'spread_us': {name: [float(np.percentile((st[:, k1].astype(np.int64) - st[:, 0].astype(np.int64)) / 100.0, q)) for q in (10, 50, 90, 100)]
                          for name, k1 in (('sweep_end', 7), ('render_end', 8), ('join', 4), ('total', 6))},
            'start_skew_us': float((np.percentile(st[:, 0], 100) - np.percentile(st[:, 0], 0)) / 100.0),
+           'entry_skew_us': [float(np.percentile((st[:, 77] - st[:, 77].min()) / 100.0, q)) for q in (10, 50, 90, 100)],
+           'entry_to_stamp0_us': [float(np.percentile((st[:, 0] - st[:, 77]) / 100.0, q)) for q in (10, 50, 90, 100)],
+           'end_after_first_entry_us': [float(np.percentile((st[:, 6] - st[:, 77].min()) / 100.0, q)) for q in (10, 50, 90, 100)],
            'sweep_steps_per_wave': [float(np.median(st[:, 64 + w].astype(np.int64))) for w in range(8)],
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())}}
     print(json.dumps(res, indent=1))
