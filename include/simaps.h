@@ -208,7 +208,9 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
  *   [N][Hc][Wc] int32 (body ids), cam_params [N][9] fp64 = _get_camera_params(robot pose)
  *   (position, target, up; envs.py:1962-2008), seg_ids [E] per env.  keys: uint64 [M, H, W] scratch,
  *   all zero on entry and left zero.  All DEVICE.  Points with equal z on one pixel: the later
- *   camera pixel wins (the reference's np.argsort leaves that order unspecified). */
+ *   camera pixel wins (the reference's np.argsort leaves that order unspecified).
+ *   SIMAPS_EUNSUPPORTED: camera width outside [69, 1024], Hc * Wc >= 2^28, H * W odd, N > 65535
+ *   (two launches on `stream`: a point pass with per-chunk LDS max-reduction + one key-map sweep). */
 int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, const simaps_agent *agents,
                   const simaps_seg_ids *seg_ids, const double *cam_params, const float *depth, const int32_t *seg_raw,
                   float *overhead, uint8_t *occupancy, uint64_t *keys, void *stream);
