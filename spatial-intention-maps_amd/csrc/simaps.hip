@@ -2511,7 +2511,7 @@ constexpr int PATH_MAX_PTS = 64;
 // approximate_polygon and the line-of-sight pruning on `line_mask`.  Leaves the kept waypoints in
 // outp[0, cnt) (packed (row << 16) | col, target first, i.e. before pyx:152's reversal) and returns
 // cnt in wave 0.  All threads call it.
-__device__ int path_core(Shared &sh, SsspScratch &S, char *smem, int H, int W, bool run_spfa, int line_mask)
+__device__ __forceinline__ int path_core(Shared &sh, SsspScratch &S, char *smem, int H, int W, bool run_spfa, int line_mask)
 {
     static_assert(align16((int)sizeof(SsspScratch)) + DIST_FLOATS * 5 <= UNION_BYTES, "SPFA queue + flags fit the union");
     // after the parent walk the distance + parent arrays are free: the Douglas-Peucker stack
@@ -2528,8 +2528,20 @@ __device__ int path_core(Shared &sh, SsspScratch &S, char *smem, int H, int W, b
     // (3) GridGraph._spfa (pyx:69-114) from the snapped source, exactly: one wave, the 8 out-edges of
     // a popped vertex evaluated by lanes 0..7 (distinct heads, so in parallel), then the pushes and
     // SLF swaps in edge order.  inf = 2 * H * W (pyx:38); queue as a ring (live entries <= cells).
+    // Blocked and border cells hold -inf, so `new < dist[v]` is false for them: no free-bit test per
+    // edge.  Per pop ONE round of LDS reads (dist[u], dist[v], in_queue[v], the next front) -- the
+    // front of the queue lives in a register (it is either the prefetched next entry or the vertex
+    // an SLF swap just put there), so no read waits for the previous pop's writes except the SLF
+    // front's distance, read only when a pop pushes.
     const float INFR = (float)(2 * H * W);
-    for (int k = tid; k < cells; k += NT) { dist[k] = INFR; parent[k] = -1; inq[k] = 0; }
+    if (tid == 0) STAMP_NB(2);
+    for (int k = tid; k < cells; k += NT) {
+        const int rr = k / pw, cc = k - rr * pw;  // (once per cell)
+        const bool fr = rr >= 1 && rr <= h && cc >= 1 && cc <= w && b_test(S.freeb[rr - 1], cc - 1);
+        dist[k] = fr ? INFR : -INFINITY;
+        parent[k] = -1;
+        inq[k] = 0;
+    }
     lds_barrier();
     const bool src_ok = run_spfa;
     const int su = (sh.src_s[0][0] - sh.i0 + 1) * pw + (sh.src_s[0][1] - sh.j0 + 1);
@@ -2540,39 +2552,83 @@ __device__ int path_core(Shared &sh, SsspScratch &S, char *smem, int H, int W, b
         const int dj = lane >= 8 ? 0 : lane < 2 ? (lane == 0 ? -1 : 1) : ((lane - 2) % 3) - 1;
         const float wl = (lane < 8 && di != 0 && dj != 0) ? SQRT2F : 1.0f;
         const int doff = di * pw + dj;
-        if (lane == 0) { dist[su] = 0.0f; queue[1 % cells] = su; inq[su] = 1; }
-        int head = 0, tail = 1, pops = 0;
-        while (head < tail && ++pops < (1 << 24)) {  // the guard is never reached by a correct SPFA
-            head++;
-            const int u = __builtin_amdgcn_readfirstlane(queue[head % cells]);
-            if (lane == 0) inq[u] = 0;
-            const float du = dist[u];
+        if (lane == 0) { dist[su] = 0.0f; queue[0] = su; inq[su] = 1; }
+        __builtin_amdgcn_wave_barrier();
+        int qh = 0, qt = 1, count = 1, front = su;  // live entries queue[qh .. qt) (mod cells); front == queue[qh]
+        // (the wave's stores below are made by every lane with the same address and value: no exec
+        // masking around them)
+        typedef __attribute__((address_space(3))) int lds_int;
+        typedef __attribute__((address_space(3))) uint8_t lds_u8;
+        lds_float *Ld = (lds_float *)dist;
+        lds_int *Lp = (lds_int *)parent, *Lq = (lds_int *)queue;
+        lds_u8 *Li = (lds_u8 *)inq;
+        for (int pops = 0; count > 0 && pops < (1 << 24); pops++) {  // the guard is never reached by a correct SPFA
+            const int u = front;
+            qh = qh + 1 == cells ? 0 : qh + 1;
+            count--;
+            Li[u] = 0;
             const int v = u + doff;
-            const int vr = v / pw - 1, vc = v % pw - 1;
-            const bool ok = lane < 8 && vr >= 0 && vr < h && vc >= 0 && vc < w && b_test(S.freeb[vr], vc);
+            // one round of reads (in-order LDS sees this wave's earlier writes); the ballots below
+            // consume them together
+            const int nfr = Lq[qh];  // the next front (valid if count > 0)
+            const float du = Ld[u], dv = Ld[v];
+            const int iqv = Li[v];
             const float nd = du + wl;
-            uint64_t imp = __ballot(ok && nd < dist[v]);
-            while (imp) {
-                const int k = __builtin_ctzll(imp);
-                imp &= imp - 1;
-                const int vk = __builtin_amdgcn_readlane(v, k);
-                const float ndk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), k));
-                if (lane == 0) {
-                    parent[vk] = u;
-                    dist[vk] = ndk;
-                    if (!inq[vk]) {
-                        tail++;
-                        queue[tail % cells] = vk;
-                        inq[vk] = 1;
-                        const int qa = queue[(head + 1) % cells];
-                        if (dist[vk] < dist[qa]) { queue[tail % cells] = qa; queue[(head + 1) % cells] = vk; }
+            const bool better = lane < 8 && nd < dv;
+            const uint64_t imp = __ballot(better);
+            const uint64_t notq = __ballot(iqv == 0);
+            int nf = __builtin_amdgcn_readfirstlane(nfr);
+            if (imp) {
+                if (better) { Ld[v] = nd; Lp[v] = u; }
+                uint64_t push = imp & notq;
+                if (push) {
+                    // The SLF compare of edge k's push sees the front's distance as the reference does
+                    // at that moment: lowered by this pop only if the front is the head of an earlier
+                    // edge (jf < k).  The front is never pushed (it is queued), but it may be relaxed.
+                    const uint64_t fm = __ballot(lane < 8 && v == nf);
+                    const int jf = fm ? __builtin_ctzll(fm) : 64;
+                    float dbefore = 0.0f, dafter = 0.0f;
+                    if (count > 0) {
+                        if (jf < 64) {
+                            dbefore = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), jf));
+                            dafter = ((imp >> jf) & 1) ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), jf)) : dbefore;
+                        } else {
+                            dbefore = dafter = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(Ld[nf])));
+                        }
+                    }
+                    bool fixed = false;  // the front is a vertex pushed by this pop (distance fixed)
+                    float dfix = 0.0f;
+                    while (push) {
+                        const int k = __builtin_ctzll(push);
+                        push &= push - 1;
+                        const int vk = __builtin_amdgcn_readlane(v, k);
+                        const float ndk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), k));
+                        const int slot = qt;
+                        qt = qt + 1 == cells ? 0 : qt + 1;
+                        Li[vk] = 1;
+                        const float dfront = fixed ? dfix : (jf < k ? dafter : dbefore);
+                        if (++count == 1) {  // the queue was empty: vk is its front
+                            Lq[slot] = vk;
+                            nf = vk;
+                            fixed = true;
+                            dfix = ndk;
+                        } else if (ndk < dfront) {  // pyx:108-111: swap with the front
+                            Lq[slot] = nf;
+                            Lq[qh] = vk;
+                            nf = vk;
+                            fixed = true;
+                            dfix = ndk;
+                        } else {
+                            Lq[slot] = vk;
+                        }
                     }
                 }
-                tail = __builtin_amdgcn_readfirstlane(tail);
             }
+            front = nf;
         }
     }
     lds_barrier();
+    if (tid == 0) STAMP_NB(3);
     // (4) dense path: parents from the target back to the source (pyx:131-138), global (i, j) packed
     if (tid == 0) {
         int cnt = 0, v = tv;
@@ -2592,6 +2648,7 @@ __device__ int path_core(Shared &sh, SsspScratch &S, char *smem, int H, int W, b
     }
     lds_barrier();
     const int nd = sh.nseg;
+    if (tid == 0) STAMP_NB(4);
     // (5) approximate_polygon(dense, tolerance=1) (skimage 0.18.3 measure/_polygon.py), one wave
     uint8_t *chain = inq;
     for (int k = tid; k < nd; k += NT) chain[k] = (k == 0 || k == nd - 1) ? 1 : 0;
@@ -2637,6 +2694,7 @@ __device__ int path_core(Shared &sh, SsspScratch &S, char *smem, int H, int W, b
         }
     }
     lds_barrier();
+    if (tid == 0) STAMP_NB(5);
     // (6) line-of-sight pruning on the grid (pyx:143-150), then reversed (pyx:152)
     if (tid < 64) {
         int m = 0;  // sparse points = chain-flagged dense points, in order
@@ -2663,6 +2721,7 @@ __device__ int path_core(Shared &sh, SsspScratch &S, char *smem, int H, int W, b
                 cnt++;
             }
         }
+        if (lane == 0) STAMP_NB(6);
         return cnt;
     }
     return 0;
@@ -2680,6 +2739,7 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
     SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
     const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int H = cfg.H, W = cfg.W;
+    if (tid == 0) STAMP_NB(0);
     const simaps_agent ag = agents[n];
     OccLoad<NT> occ_regs;
     cspace_load<NT>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
@@ -2710,6 +2770,7 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
         return;
     }
     // (2) snap both ends (envs.py:2489-2490)
+    if (tid == 0) STAMP_NB(1);
     snap_sources(sh, S, 2, whole_wg());
     const int cnt = path_core(sh, S, smem, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE);
     int *outp = reinterpret_cast<int *>(smem + OFF_DIST) + DIST_FLOATS;
