@@ -2580,48 +2580,73 @@ __device__ __forceinline__ int path_core(Shared &sh, SsspScratch &S, char *smem,
             int nf = __builtin_amdgcn_readfirstlane(nfr);
             if (imp) {
                 if (better) { Ld[v] = nd; Lp[v] = u; }
-                uint64_t push = imp & notq;
+                const uint64_t push = imp & notq;
                 if (push) {
-                    // The SLF compare of edge k's push sees the front's distance as the reference does
-                    // at that moment: lowered by this pop only if the front is the head of an earlier
-                    // edge (jf < k).  The front is never pushed (it is queued), but it may be relaxed.
-                    const uint64_t fm = __ballot(lane < 8 && v == nf);
-                    const int jf = fm ? __builtin_ctzll(fm) : 64;
+                    // The pushes of this pop, in edge order, resolved lane-parallel (lanes 0-7 own the
+                    // edges).  pyx:104-111 pushes each at the tail and swaps it with the front if its
+                    // distance is below the front's at that moment, so: the front's distance seen by
+                    // edge k is F0's (lowered by this pop only if F0 is the head of an earlier edge jf <
+                    // k: F0 is queued, so never pushed, but it may be relaxed) until the first push that
+                    // beats it (js); after that it is the running minimum of the pushed distances from
+                    // js on.  A swapping push's slot receives the previous front (F0 or the previous
+                    // swapping push's vertex); the last swapper ends at the front.
+                    const int np = __popcll(push);
+                    const bool isP = (push >> lane) & 1;
+                    const int rank = __popcll(push & ((1ull << lane) - 1));
+                    uint64_t cand = push;
+                    int F0 = nf, jf = 64;
                     float dbefore = 0.0f, dafter = 0.0f;
-                    if (count > 0) {
-                        if (jf < 64) {
+                    if (count == 0) {  // the queue was empty: the first push becomes the front
+                        const int p1 = __builtin_ctzll(push);
+                        F0 = __builtin_amdgcn_readlane(v, p1);
+                        dbefore = dafter = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), p1));
+                        cand &= cand - 1;
+                    } else {
+                        const uint64_t fm = __ballot(lane < 8 && v == nf);
+                        if (fm) {
+                            jf = __builtin_ctzll(fm);
                             dbefore = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), jf));
                             dafter = ((imp >> jf) & 1) ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), jf)) : dbefore;
                         } else {
                             dbefore = dafter = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(Ld[nf])));
                         }
                     }
-                    bool fixed = false;  // the front is a vertex pushed by this pop (distance fixed)
-                    float dfix = 0.0f;
-                    while (push) {
-                        const int k = __builtin_ctzll(push);
-                        push &= push - 1;
-                        const int vk = __builtin_amdgcn_readlane(v, k);
-                        const float ndk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), k));
-                        const int slot = qt;
-                        qt = qt + 1 == cells ? 0 : qt + 1;
-                        Li[vk] = 1;
-                        const float dfront = fixed ? dfix : (jf < k ? dafter : dbefore);
-                        if (++count == 1) {  // the queue was empty: vk is its front
-                            Lq[slot] = vk;
-                            nf = vk;
-                            fixed = true;
-                            dfix = ndk;
-                        } else if (ndk < dfront) {  // pyx:108-111: swap with the front
-                            Lq[slot] = nf;
-                            Lq[qh] = vk;
-                            nf = vk;
-                            fixed = true;
-                            dfix = ndk;
-                        } else {
-                            Lq[slot] = vk;
-                        }
+                    const bool isC = (cand >> lane) & 1;
+                    const uint64_t sF0 = __ballot(isC && nd < (lane > jf ? dafter : dbefore));
+                    int content = v, newfront = F0;
+                    if (sF0) {
+                        const int js = __builtin_ctzll(sF0);
+                        // exclusive prefix minimum of nd over the candidate lanes in [js, lane) (DPP
+                        // row shifts: lanes 0-7 lie in one row)
+                        float y = (isC && lane >= js) ? nd : INFINITY;
+#define SPFA_SHR(x, n, old) __builtin_amdgcn_update_dpp((old), (x), 0x110 + (n), 0xf, 0xf, false)
+#define SPFA_SHRF(x, n) __int_as_float(SPFA_SHR(__float_as_int(x), n, (int)INF_BITS))
+                        y = fminf(y, SPFA_SHRF(y, 1));
+                        y = fminf(y, SPFA_SHRF(y, 2));
+                        y = fminf(y, SPFA_SHRF(y, 4));
+                        const float pm = SPFA_SHRF(y, 1);
+                        const bool sw = isC && (lane == js || (lane > js && nd < pm));
+                        const uint64_t swm = __ballot(sw);
+                        // the previous swapper's vertex: exclusive "last valid" scan of v over swappers
+                        int z = sw ? v : -1, zs;
+                        zs = SPFA_SHR(z, 1, -1); z = z >= 0 ? z : zs;
+                        zs = SPFA_SHR(z, 2, -1); z = z >= 0 ? z : zs;
+                        zs = SPFA_SHR(z, 4, -1); z = z >= 0 ? z : zs;
+                        const int prev = SPFA_SHR(z, 1, -1);
+#undef SPFA_SHRF
+#undef SPFA_SHR
+                        if (sw) content = prev >= 0 ? prev : F0;
+                        newfront = __builtin_amdgcn_readlane(v, 63 - __builtin_clzll(swm));
                     }
+                    if (isP) {
+                        const int slot = qt + rank < cells ? qt + rank : qt + rank - cells;
+                        Lq[slot] = content;
+                        Li[v] = 1;
+                    }
+                    if (sF0) Lq[qh] = newfront;  // after the lanes' stores (in the empty case qh is p1's slot)
+                    qt = qt + np < cells ? qt + np : qt + np - cells;
+                    count += np;
+                    nf = newfront;
                 }
             }
             front = nf;
