@@ -282,6 +282,100 @@ def test_gridgraph_shortest_path_reference_goldens(V):
     assert m == 12
 
 
+def _tie_grids(rs):
+    """Random grids that stress the exact SPFA's queue order: empty and pillar lattices (many
+    equal-length paths, so the parents -- and the waypoints -- depend on the SLF swaps), random
+    obstacles at several densities, long corridors."""
+    grids = []
+    for h, w in ((44, 92), (60, 120), (92, 92), (17, 33)):
+        g = np.ones((h, w), np.uint8)
+        grids.append(g.copy())                                  # empty: all-tie octile paths
+        p = g.copy()
+        p[2::4, 2::4] = 0                                       # pillar lattice
+        grids.append(p)
+        for dens in (0.08, 0.25, 0.4):
+            grids.append((rs.random_sample((h, w)) > dens).astype(np.uint8))
+        c = g.copy()
+        c[::6, 1:] = 0                                          # serpentine corridors
+        c[3::12, :-1] = 1
+        c[9::12, 1:] = 1
+        c[::6, 0] = 1
+        c[::12, -1] = 1
+        grids.append(c)
+    return grids
+
+
+def _dp_tie(grid, src, tgt):
+    """True if approximate_polygon (skimage 0.18.3, tolerance 1) on this path's dense points meets a
+    floating-point tie: two candidates of a split within 1e-9 of each other, or the maximum within
+    1e-9 of the tolerance.  There the reference's own choice follows the last-bit rounding of its
+    host's libm sin / cos (numpy dispatches to SIMD / SVML kernels on AVX-512 hosts), so no
+    implementation -- nor the reference on another host -- is pinned to one answer."""
+    H, W = grid.shape
+    _, par = O.spfa(grid, src)
+    u, v = src[0] * W + src[1], tgt[0] * W + tgt[1]
+    dense = [[v // W, v % W]]
+    while v != u:
+        v = int(par[v])
+        if v < 0:
+            break
+        dense.append([v // W, v % W])
+    c = np.array(dense)
+    stack = [(0, len(c) - 1)]
+    while stack:
+        s, e = stack.pop()
+        (r0, c0), (r1, c1) = c[s], c[e]
+        dr, dc = r1 - r0, c1 - c0
+        ang = -np.arctan2(dr, dc)
+        sd = c0 * np.sin(ang) + r0 * np.cos(ang)
+        seg = c[s + 1:e]
+        if len(seg) == 0:
+            continue
+        r, cc = seg[:, 0], seg[:, 1]
+        proj = ((r - r0) * dr + (cc - c0) * dc > 0) & (-(r - r1) * dr - (cc - c1) * dc > 0)
+        d = np.where(proj, np.abs(r * np.cos(ang) + cc * np.sin(ang) - sd),
+                     np.minimum(np.hypot(cc - c0, r - r0), np.hypot(cc - c1, r - r1)))
+        top = np.sort(d)[::-1]
+        if abs(top[0] - 1.0) < 1e-9 or (len(top) > 1 and top[0] - top[1] < 1e-9 and top[0] > 1.0):
+            return True
+        if top[0] > 1.0:
+            k = s + int(np.argmax(d)) + 1
+            stack += [(k, e), (s, k)]
+    return False
+
+
+def test_gridgraph_paths_fuzz_vs_oracle(V):
+    """GridGraph.shortest_path / shortest_path_image on ~1,000 (grid, source, target) cases built to
+    create equal-length-path ties, bitwise against the oracle's C restatement of pyx:69-154 (itself
+    pinned to the reference by tests/test_oracle_golden.py): the lane-parallel SLF resolution of the
+    path kernel must leave the queue order -- hence every parent -- exactly as the reference's.
+    Paths whose Douglas-Peucker split meets a floating-point tie (_dp_tie: host-libm dependent in
+    the reference itself) must agree everywhere but may differ; they are counted and bounded."""
+    synthetic, vector_env = V
+    rs = np.random.RandomState(1234)
+    n_cases = n_tie = 0
+    for gi, grid in enumerate(_tie_grids(rs)):
+        free = np.argwhere(grid != 0)
+        if len(free) < 2:
+            continue
+        gg = vector_env.GridGraph(grid)
+        srcs = [tuple(int(x) for x in free[rs.randint(len(free))]) for _ in range(4)]
+        for src in srcs:
+            img = gg.shortest_path_image(src)
+            ref = O.spfa_image(grid, src)
+            assert _bitwise(np.asarray(img, dtype=np.float32), ref.astype(np.float32)), (gi, src)
+            tgts = [tuple(int(x) for x in free[rs.randint(len(free))]) for _ in range(10)]
+            got = gg.shortest_paths([(src, t) for t in tgts])
+            for t, p in zip(tgts, got):
+                want = O.grid_shortest_path(grid, src, t)
+                n_cases += 1
+                if np.array_equal(np.array(p, dtype=np.int64).reshape(-1, 2), np.array(want, dtype=np.int64).reshape(-1, 2)):
+                    continue
+                assert _dp_tie(grid, src, t), (gi, src, t, p, want)
+                n_tie += 1
+    assert n_cases >= 900 and n_tie <= n_cases // 100, (n_cases, n_tie)
+
+
 def test_policy_input_from_device_stacks(V):
     """device-rendered CHW stacks through policy_input.group_batches equal
     DQNPolicy.apply_transform (ToTensor of the (96, 96, C) float32 state, policies.py:44-45) of the
