@@ -174,7 +174,7 @@ def test_full_size_baseline_configs(S, cfg, envs):
     assert _bitwise(s1, s2)
     _channel_invariants(s1, scenes[0]['flags'])
     rs = np.random.RandomState(11)
-    for n in sorted(rs.choice(b.N, 10, replace=False)) + [0, b.N - 1]:
+    for n in sorted(rs.choice(b.N, 46, replace=False)) + [0, b.N - 1]:
         e, a = b.agents[n]
         assert _bitwise(s1[n], O.agent_state(scenes[e], a)), (cfg, n)
 
