@@ -53,41 +53,50 @@ def _history_path_reversed(r):
 def pack_descriptors(scenes, agents):
     """Host-side packing of the per-step scene descriptor into the C structs.
 
-    scenes: list of scene dicts (simaps.synthetic format); agents: list of (env_idx, robot_idx)."""
-    n_rob = sum(len(s['robots']) for s in scenes)
+    scenes: list of scene dicts (simaps.synthetic format); agents: list of (env_idx, robot_idx).
+    Column-wise: one numpy assignment per struct field and one concatenation of all path points
+    (a per-robot, per-field loop cost ~4.6 ms for 64 envs x 4 robots, 150x the kernel)."""
+    nr = [len(s['robots']) for s in scenes]
+    if nr and max(nr) > _lib.MAX_ROBOTS:
+        raise ValueError('at most %d robots per env' % _lib.MAX_ROBOTS)
+    rl = [r for s in scenes for r in s['robots']]
+    n_rob = len(rl)
     robots = np.zeros(n_rob, dtype=_lib.ROBOT_DTYPE)
     envs = np.zeros(len(scenes), dtype=_lib.ENV_DTYPE)
-    paths = []
-    k = 0
-    for e, s in enumerate(scenes):
-        if len(s['robots']) > _lib.MAX_ROBOTS:
-            raise ValueError('at most %d robots per env' % _lib.MAX_ROBOTS)
-        envs[e]['robot_off'] = k
-        envs[e]['num_robots'] = len(s['robots'])
-        rec = s['receptacle_position']
-        envs[e]['has_receptacle'] = rec is not None
-        if rec is not None:
-            envs[e]['receptacle_x'], envs[e]['receptacle_y'] = rec[0], rec[1]
-        for r in s['robots']:
-            R = robots[k]
-            R['x'], R['y'] = r['position'][0], r['position'][1]
-            R['heading'] = r['heading']
-            R['target_x'], R['target_y'] = r['target_ee'][0], r['target_ee'][1]
-            R['type'] = _lib.TYPE_IDS[r['type']]
-            R['group_index'] = r['group_index']
-            R['lifting'] = int(r.get('lift_state') == 'lifting')
-            R['idle'] = int(bool(r['idle']))
-            for name, pts in (('intention', _intention_path(r)), ('history', _history_path_reversed(r))):
-                if len(pts) > _lib.MAX_PATH:
-                    raise ValueError('path longer than %d points' % _lib.MAX_PATH)
-                R[name + '_off'] = len(paths)
-                R[name + '_len'] = len(pts)
-                paths.extend((float(p[0]), float(p[1])) for p in pts)
-            k += 1
+    envs['num_robots'] = nr
+    envs['robot_off'] = np.concatenate([[0], np.cumsum(nr)[:-1]]) if nr else []
+    recs = [s['receptacle_position'] for s in scenes]
+    envs['has_receptacle'] = [rec is not None for rec in recs]
+    envs['receptacle_x'] = [rec[0] if rec is not None else 0.0 for rec in recs]
+    envs['receptacle_y'] = [rec[1] if rec is not None else 0.0 for rec in recs]
+    if n_rob:
+        robots['x'] = [r['position'][0] for r in rl]
+        robots['y'] = [r['position'][1] for r in rl]
+        robots['heading'] = [r['heading'] for r in rl]
+        robots['target_x'] = [r['target_ee'][0] for r in rl]
+        robots['target_y'] = [r['target_ee'][1] for r in rl]
+        robots['type'] = [_lib.TYPE_IDS[r['type']] for r in rl]
+        robots['group_index'] = [r['group_index'] for r in rl]
+        robots['lifting'] = [r.get('lift_state') == 'lifting' for r in rl]
+        robots['idle'] = [bool(r['idle']) for r in rl]
+    # per robot: its intention path, then its reversed history path (envs.py:1475-1479, 2318)
+    pts = []
+    for r in rl:
+        pts.append(_intention_path(r))
+        pts.append(_history_path_reversed(r))
+    lens = np.array([len(p) for p in pts], dtype=np.int64).reshape(-1, 2) if pts else np.zeros((0, 2), np.int64)
+    if len(lens) and lens.max() > _lib.MAX_PATH:
+        raise ValueError('path longer than %d points' % _lib.MAX_PATH)
+    offs = np.concatenate([[0], np.cumsum(lens.ravel())[:-1]]).reshape(-1, 2) if len(lens) else lens
+    if n_rob:
+        robots['intention_off'], robots['intention_len'] = offs[:, 0], lens[:, 0]
+        robots['history_off'], robots['history_len'] = offs[:, 1], lens[:, 1]
+    flat = [q for p in pts for q in p]
+    paths = np.array([(q[0], q[1]) for q in flat] if flat else [(0.0, 0.0)], dtype=np.float64).reshape(-1, 2)
     ag = np.zeros(len(agents), dtype=_lib.AGENT_DTYPE)
-    for n, (e, a) in enumerate(agents):
-        ag[n]['env'], ag[n]['robot'], ag[n]['map_slot'] = e, a, n
-    paths = np.array(paths if paths else [(0.0, 0.0)], dtype=np.float64).reshape(-1, 2)
+    if len(agents):
+        ea = np.asarray(agents, dtype=np.int64).reshape(-1, 2)
+        ag['env'], ag['robot'], ag['map_slot'] = ea[:, 0], ea[:, 1], np.arange(len(agents))
     return robots, envs, ag, paths
 
 
