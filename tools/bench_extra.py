@@ -92,6 +92,26 @@ def main():
                       'cpu_sample': '%d paths incl. each agent\'s cspace / EDT / SPFA' % n}), flush=True)
 
 
+def bench_dropin_step(args):
+    """The drop-in's host + device cost of one observation step: VectorEnvObservations.update(new
+    scene descriptors) + get_state() (device tensors, every robot), synchronised -- what a training
+    loop pays per step beside its simulator (the bench line times the kernel alone)."""
+    from simaps import vector_env
+    scenes = [synthetic.make_scene(args.config, e) for e in range(args.envs)]
+    obs = vector_env.VectorEnvObservations(scenes, layout='chw')
+
+    def step():
+        obs.update(scenes=scenes)
+        obs.get_state()
+        torch.cuda.synchronize()
+    dt = timed(step, max(args.steps, 50), 5)
+    n = sum(len(s['robots']) for s in scenes)
+    print(json.dumps({'row': 'dropin_step', 'config': args.config, 'stacks_per_step': n,
+                      'ms_per_step': dt * 1e3, 'stacks_per_s_end_to_end': n / dt,
+                      'note': 'update(scenes) + get_state() + synchronize, host packing and uploads included'}),
+          flush=True)
+
+
 def bench_ingest(args):
     """Ingest row: the two kernels alone (HIP events on the launch stream around K launches of the
     device half, inputs resident) and end to end (host packing + upload + launch), with an HBM
@@ -152,4 +172,5 @@ if __name__ == '__main__':
         sys.argv.remove('--ingest-only')
     else:
         main()
+        bench_dropin_step(argparse.Namespace(config='lifting_4-small_divider', envs=64, steps=50))
     bench_ingest(argparse.Namespace(config='lifting_4-small_divider', envs=64, steps=10, cpu_budget=8.0))
