@@ -171,7 +171,8 @@ class StateBatch:
         self.robots_d = _to_dev(robots, self.device)
         self.envs_d = _to_dev(envs, self.device)
         self.agents_d = _to_dev(ag, self.device)
-        self._subsets = {}
+        if not hasattr(self, '_subsets'):
+            self._subsets = {}  # subset agent lists depend on self.agents only: kept across steps
         self.paths_d = torch.from_numpy(paths).to(self.device)
 
     def set_maps(self, occupancy=None, overhead=None, slots=None):
@@ -196,14 +197,18 @@ class StateBatch:
         """Device agent list rendering only map slots `slots` (indices into self.agents), e.g. the
         robots awaiting a new action (envs.py:322-323).  Cached per distinct subset."""
         key = tuple(int(k) for k in slots)
+        if len(key) == self.N and key == tuple(range(self.N)):
+            return self.agents_d, self.N  # every agent, in order
         d = self._subsets.get(key)
         if d is None:
+            ks = np.asarray(key, dtype=np.int64)
+            if len(ks) and (ks.min() < 0 or ks.max() >= self.N):
+                raise IndexError('map slot %d outside [0, %d)' % (int(ks[(ks < 0) | (ks >= self.N)][0]), self.N))
+            ea = np.asarray(self.agents, dtype=np.int64).reshape(-1, 2)[ks] if len(ks) else np.zeros((0, 2), np.int64)
             ag = np.zeros(len(key), dtype=_lib.AGENT_DTYPE)
-            for n, k in enumerate(key):
-                if not 0 <= k < self.N:
-                    raise IndexError('map slot %d outside [0, %d)' % (k, self.N))
-                ag[n]['env'], ag[n]['robot'] = self.agents[k]
-                ag[n]['map_slot'] = k
+            ag['env'], ag['robot'], ag['map_slot'] = ea[:, 0], ea[:, 1], ks
+            if len(self._subsets) >= 64:  # awaiting patterns vary per step: keep the cache bounded
+                self._subsets.clear()
             d = self._subsets[key] = _to_dev(ag, self.device)
         return d, len(key)
 

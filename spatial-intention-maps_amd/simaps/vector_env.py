@@ -78,9 +78,10 @@ class VectorEnvObservations:
             out = out.cpu().numpy()
             _lib.check_faults()  # the copy synchronised: a faulting launch raises here
         pos = {k: n for n, k in enumerate(want)}
+        rows = out if numpy else out.unbind(0)  # one C++ call for all views (per-item indexing: ~10 us each)
         res = []
         for e in range(self.num_envs):
-            res.append([[out[pos[self.slot[(e, a)]]] if self.slot[(e, a)] in pos else None for a in g]
+            res.append([[rows[pos[self.slot[(e, a)]]] if self.slot[(e, a)] in pos else None for a in g]
                         for g in self.groups[e]])
         return res
 
