@@ -64,6 +64,12 @@ def main():
            'end_after_first_entry_us': [float(np.percentile((st[:, 6] - st[:, 77].min()) / 100.0, q)) for q in (10, 50, 90, 100)],
            'sweep_steps_per_wave': [float(np.median(st[:, 64 + w].astype(np.int64))) for w in range(8)],
            'rounds': {'median': float(np.median(st[:, 10])), 'max': int(st[:, 10].max()), 'min': int(st[:, 10].min())}}
+    # SSSP edge relaxations per stack -- every cell of a swept line evaluates its 3
+    # incoming edges; wave w of source s sweeps direction (w + 2 s) & 3 (0 / 1: lines of w cells)
+    h, w = b.cfg.room_h, b.cfg.room_w
+    per_wave = np.median(st[:, 64:72].astype(np.float64), axis=0)
+    res['sssp_relaxations_per_stack'] = float(sum(n * (w if ((k + 2 * (k >> 2)) & 3) < 2 else h) * 3
+                                                  for k, n in enumerate(per_wave)))
     print(json.dumps(res, indent=1))
 
 
