@@ -55,6 +55,18 @@ def test_get_state_structure_and_awaiting_subset(V, layout):
                 assert _bitwise(x.cpu().numpy(), O.agent_state(s, a))
 
 
+def test_get_state_nobody_awaiting(V):
+    """A step where no robot awaits an action: every entry None, nothing launched, and the next
+    step renders normally."""
+    synthetic, vector_env = V
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 510 + e) for e in range(2)]
+    obs = vector_env.VectorEnvObservations(scenes)
+    st = obs.get_state(awaiting=[[False] * 4, [False] * 4], numpy=True)
+    assert [[x is None for g in env for x in g] for env in st] == [[True] * 4, [True] * 4]
+    st = obs.get_state(awaiting=[[False, True, False, False], [False] * 4], numpy=True)
+    assert st[1][0] == [None] * 4 and _bitwise(st[0][0][1], O.agent_state(scenes[0], 1))
+
+
 def test_update_descriptors_and_maps(V):
     synthetic, vector_env = V
     cfg = 'lifting_4-small_divider'

@@ -229,6 +229,38 @@ def test_snap_ties_on_maze_walls(S):
         assert _bitwise(st[n], O.agent_state(scenes[e], a)), (n, e, a)
 
 
+def test_edge_poses_and_degenerate_paths(S):
+    """The fp64 index rules at their edges: headings on exact multiples of 45 deg (and +-pi, +-0,
+    whole degrees), positions on pixel boundaries (position_to_pixel_indices floors exactly there,
+    envs.py:2391-2397), zero-length path segments and a waypoint index at the end of the path."""
+    batch, K, synthetic = S
+    rs = np.random.RandomState(23)
+    heads = [k * np.pi / 4 for k in range(-4, 5)] + [-0.0, np.radians(30.0), np.radians(-135.0), np.radians(1.0),
+                                                     1e-12, -1e-12, np.nextafter(np.pi, 0.0)]
+    k = 0
+    for c, cfg in enumerate(['lifting_4-small_divider', 'rescue_4-small_empty', 'lifting_4-large_empty-line',
+                             'lifting_2_pushing_2-large_empty-all']):
+        scenes = [synthetic.make_scene(cfg, 700 + 2 * c + e) for e in range(2)]
+        for s in scenes:
+            H, W = s['H'], s['W']
+            for r in s['robots']:
+                j, i = rs.randint(W // 2 - 30, W // 2 + 30), rs.randint(H // 2 - 15, H // 2 + 15)
+                x, y = (j - W / 2) / 96.0, (H / 2 - i) / 96.0   # on a pixel corner
+                if k % 3 == 1:
+                    x = np.nextafter(x, -1.0)                     # just below it
+                r['position'] = (float(x), float(y), 0)
+                r['heading'] = float(heads[k % len(heads)])
+                r['idle'] = False
+                wps = [r['position']] * 2 + list(r['waypoint_positions'][1:])
+                r['waypoint_positions'] = wps
+                r['waypoint_index'] = len(wps) - 1 if k % 2 else 1
+                k += 1
+        b = batch.StateBatch(scenes)
+        st = b.as_hwc(b.render()).cpu().numpy()
+        for n, (e, a) in enumerate(b.agents):
+            _check_state(st[n], O.agent_state(scenes[e], a), scenes[e]['flags'], len(scenes[e]['robots']))
+
+
 def test_sssp_grid_demo_known_answer(S):
     """shortest_paths/demo.py sample: distance 136.46806 and the full image, + 12 more sources."""
     batch, K, synthetic = S
