@@ -139,6 +139,8 @@ class StateBatch:
     the reference's index order as a zero-copy view either way."""
 
     def __init__(self, scenes, agents=None, device='cuda', layout='chw'):
+        if not scenes:
+            raise ValueError('a StateBatch needs at least one scene')
         s0 = scenes[0]
         for s in scenes:
             if (s['H'], s['W'], s['room_width'], s['room_length']) != (s0['H'], s0['W'], s0['room_width'], s0['room_length']) \

@@ -151,6 +151,8 @@ class GridGraph:
         if todo:
             grids = self.grid.unsqueeze(0).expand(len(todo), *self.shape).contiguous()
             imgs = _batch.sssp_grid(grids, torch.tensor(todo, dtype=torch.int32), window=self.window, stream=stream)
+            if stream is not None:  # cached images are read on the current stream by later calls
+                torch.cuda.current_stream(self.device).wait_stream(stream)
             for k, s in enumerate(todo):
                 self._cache[s] = imgs[k]
         return torch.stack([self._cache[s] for s in srcs]) if srcs else \

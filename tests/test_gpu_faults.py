@@ -128,3 +128,19 @@ def test_side_stream_render_matches_default_stream(S):
     out = obs.batch.render(stream=side)
     torch.cuda.current_stream().wait_stream(side)
     assert np.array_equal(obs.batch.as_hwc(out).cpu().numpy().view(np.int32), ref.view(np.int32))
+
+
+def test_gridgraph_side_stream_cache(S):
+    """GridGraph images computed on a side stream are cached and read back on the current stream."""
+    _lib, batch, synthetic = S
+    from simaps import vector_env
+    import goldens as G
+    g = G.load('sssp.npz')
+    gg = vector_env.GridGraph(g['demo_cspace'])
+    side = torch.cuda.Stream()
+    srcs = [(75, 156)] + [tuple(int(x) for x in p) for p in g['demo_sources']]
+    imgs = gg.shortest_path_images(srcs, stream=side)
+    assert np.array_equal(imgs[0].cpu().numpy().view(np.int32), g['demo_image'].view(np.int32))
+    assert gg.shortest_path_distance((75, 156), (131, 112)) == float(g['demo_distance'])
+    for q, s in enumerate(srcs[1:]):
+        assert np.array_equal(gg.shortest_path_image(s).view(np.int32), O.spfa_image(g['demo_cspace'], s).view(np.int32))
