@@ -2908,17 +2908,19 @@ __device__ __forceinline__ int np_f32_to_i32(float v)
 //                         window falls back to global atomics per run of equal pixels.  The seg
 //                         value (a sum of 1/8 multiples < 2, exact in f32) travels as seg * 8 in the
 //                         key's low 4 bits, so the winner's value needs no second look-up.
-//   ingest_resolve_kernel grid (map blocks, frames): one coalesced sweep of the slot's key map (16 B
-//                         per lane): a nonzero key writes overhead = code / 8 and is zeroed again.
-// HBM per frame: 8 B per camera pixel (depth + seg) + 8 B per map pixel (key sweep) + the pixel
-// writes; the atomics resolve in L2 (a frame's key map is <= 0.4 MB).
+//                         Each chunk also stores its box (boxes[n][chunk]).
+//   ingest_resolve_kernel 8 workgroups per frame: a sweep of the frame's box of the slot's key map
+//                         (not the whole map: a forward camera touches ~10 % of it): a nonzero key
+//                         writes overhead = code / 8 and is zeroed again; the box is reset.
+// HBM per frame: 8 B per camera pixel (depth + seg) + 8 B per pixel of the box (key sweep) + the
+// pixel writes; the atomics resolve in L2 (a frame's key map is <= 0.4 MB).
 // (measured alternatives, 256 frames: 128- / 64-thread chunks +4 / +21 us, an 8192-entry window
 // +30 us (LDS occupancy), workgroups looping over several chunks of a frame with the next chunk's
 // loads in flight +4..28 us: the per-chunk barrier chain wants many chunks in flight, not fewer)
 constexpr int INGEST_WG = 256, INGEST_PPT = 8, INGEST_PTS = INGEST_WG * INGEST_PPT;
 constexpr int INGEST_WIN = 4096;  // LDS window entries (u64 keys) over a chunk's map-pixel box
 constexpr int INGEST_MAX_WC = 1024, INGEST_MAX_ROWS = 32;  // camera width; camera rows one chunk spans
-constexpr int INGEST_RES_WG = 256, INGEST_RES_KEYS = INGEST_RES_WG * 2 * 4;  // 2 keys per load, 4 loads
+constexpr int INGEST_RES_WG = 256, INGEST_RES_U = 8, INGEST_RES_G = 8;  // resolve: 8 workgroups per frame, 8 keys per thread in flight
 
 // Camera.capture_image's frame (envs.py:1932-1940) in float32: position, principal, up, right.
 __device__ __forceinline__ void camera_frame(const double *P, float *F)
@@ -2990,7 +2992,7 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     simaps_config cfg, simaps_camera cam, const simaps_agent *__restrict__ agents,
     const simaps_seg_ids *__restrict__ seg_ids, const double *__restrict__ cam_params,
     const float *__restrict__ depth, const int32_t *__restrict__ seg_raw, uint8_t *__restrict__ occupancy,
-    unsigned long long *__restrict__ keys)
+    unsigned long long *__restrict__ keys, unsigned *__restrict__ boxes)
 {
     __shared__ unsigned long long win[INGEST_WIN];
     __shared__ float F[12], pxT[INGEST_MAX_WC], pyT[INGEST_MAX_ROWS];
@@ -3067,6 +3069,9 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
         __syncthreads();
         const int bi = box[0], bj = box[2], bh = -box[1] - bi + 1, bw = -box[3] - bj + 1;
         const int area = bh * bw;  // block-uniform (a chunk holds >= 1 point)
+        if (tid == 0)  // the chunk's box of map pixels [i0, i1) x [j0, j1), for the resolve sweep
+            reinterpret_cast<uint4 *>(boxes)[(size_t)n * gridDim.x + blockIdx.x] =
+                make_uint4((unsigned)bi, (unsigned)(bi + bh), (unsigned)bj, (unsigned)(bj + bw));
         if (area > INGEST_WIN) {   // fallback: global atomics per run
 #pragma unroll
             for (int q = 0; q < INGEST_PPT; q++)
@@ -3092,30 +3097,44 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     }
 }
 
+// grid (INGEST_RES_G, frames): the frame's box of touched map pixels (the union of the point
+// pass's chunk boxes) in INGEST_RES_WG * INGEST_RES_U pixel chunks dealt round-robin over the
+// frame's workgroups
 __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
     simaps_config cfg, const simaps_agent *__restrict__ agents, float *__restrict__ overhead,
-    unsigned long long *__restrict__ keys)
+    unsigned long long *__restrict__ keys, const unsigned *__restrict__ boxes, int nch)
 {
-    const int n = blockIdx.y, HW = cfg.H * cfg.W;
-    const size_t base = (size_t)agents[n].map_slot * HW;
-    // H * W is even for every map here (checked on the host): 16-B aligned key pairs
-    ulonglong2 *kp = reinterpret_cast<ulonglong2 *>(keys + base);
-    float2 *op = reinterpret_cast<float2 *>(overhead + base);
-    const int npair = HW / 2;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int e = blockIdx.x * (INGEST_RES_KEYS / 2) + q * INGEST_RES_WG + threadIdx.x;
-        if (e >= npair) break;
-        const ulonglong2 kv = kp[e];
-        if ((kv.x | kv.y) == 0ull) continue;
-        if (kv.x && kv.y) {
-            op[e] = make_float2((float)(kv.x & 15ull) * 0.125f, (float)(kv.y & 15ull) * 0.125f);
-        } else if (kv.x) {
-            overhead[base + 2 * e] = (float)(kv.x & 15ull) * 0.125f;
-        } else {
-            overhead[base + 2 * e + 1] = (float)(kv.y & 15ull) * 0.125f;
+    __shared__ int fbox[4];
+    const int n = blockIdx.y, tid = threadIdx.x, W = cfg.W;
+    if (tid < 64) {  // the first wave merges the chunk boxes
+        int a = INT32_MAX, bb = 0, cc = INT32_MAX, d = 0;
+        for (int k = tid; k < nch; k += 64) {
+            const uint4 c = reinterpret_cast<const uint4 *>(boxes)[(size_t)n * nch + k];
+            a = min(a, (int)c.x), bb = max(bb, (int)c.y), cc = min(cc, (int)c.z), d = max(d, (int)c.w);
         }
-        kp[e] = make_ulonglong2(0ull, 0ull);
+        a = wave_min(a), bb = wave_max(bb), cc = wave_min(cc), d = wave_max(d);
+        if (tid == 0) fbox[0] = a, fbox[1] = bb, fbox[2] = cc, fbox[3] = d;
+    }
+    __syncthreads();
+    const uint4 b = make_uint4(fbox[0], fbox[1], fbox[2], fbox[3]);
+    const int i0 = (int)b.x, j0 = (int)b.z, bw = (int)b.w - j0, area = ((int)b.y - i0) * bw;
+    const size_t base = (size_t)agents[n].map_slot * cfg.H * W + (size_t)i0 * W + j0;
+    constexpr int CH = INGEST_RES_WG * INGEST_RES_U;
+    for (int e0 = blockIdx.x * CH; e0 < area; e0 += INGEST_RES_G * CH) {
+        size_t idx[INGEST_RES_U];
+        unsigned long long kv[INGEST_RES_U];
+#pragma unroll
+        for (int u = 0; u < INGEST_RES_U; u++) {
+            const int e = e0 + u * INGEST_RES_WG + tid, r = e / bw;
+            idx[u] = base + (size_t)r * W + (e - r * bw);
+            kv[u] = e < area ? keys[idx[u]] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < INGEST_RES_U; u++)
+            if (kv[u]) {
+                overhead[idx[u]] = (float)(kv[u] & 15ull) * 0.125f;
+                keys[idx[u]] = 0ull;
+            }
     }
 }
 
@@ -3350,7 +3369,7 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
 
 int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, const simaps_agent *agents,
                   const simaps_seg_ids *seg_ids, const double *cam_params, const float *depth, const int32_t *seg_raw,
-                  float *overhead, uint8_t *occupancy, uint64_t *keys, void *stream)
+                  float *overhead, uint8_t *occupancy, uint64_t *keys, uint32_t *boxes, void *stream)
 {
     int rc = check_cfg(cfg);
     if (rc) return rc;
@@ -3358,20 +3377,19 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
         return fail(SIMAPS_EINVAL, "bad camera");
     if (N < 0) return fail(SIMAPS_EINVAL, "N < 0");
     if (N == 0) return 0;
-    if (!agents || !seg_ids || !cam_params || !depth || !seg_raw || !overhead || !occupancy || !keys)
+    if (!agents || !seg_ids || !cam_params || !depth || !seg_raw || !overhead || !occupancy || !keys || !boxes)
         return fail(SIMAPS_EINVAL, "NULL buffer");
     if ((rc = pending_faults())) return rc;
-    const int np = cam->height_px * cam->width_px, hw = cfg->H * cfg->W;
+    const int np = cam->height_px * cam->width_px;
     if (cam->width_px > INGEST_MAX_WC || INGEST_PTS / cam->width_px + 2 > INGEST_MAX_ROWS)
         return fail(SIMAPS_EUNSUPPORTED, "camera width %d outside [%d, %d]", cam->width_px, INGEST_PTS / (INGEST_MAX_ROWS - 2) + 1, INGEST_MAX_WC);
     if (np >= (1 << 28)) return fail(SIMAPS_EUNSUPPORTED, "camera frame of %d pixels (key packs pixel + 1 in 28 bits)", np);
-    if (hw % 2) return fail(SIMAPS_EUNSUPPORTED, "map of %d pixels is odd (the key sweep reads pairs)", hw);
     if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d frames per launch (grid y <= 65535)", N);
-    hipLaunchKernelGGL(ingest_points_kernel, dim3((np + INGEST_PTS - 1) / INGEST_PTS, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids,
-                       cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys));
-    hipLaunchKernelGGL(ingest_resolve_kernel, dim3((hw / 2 + INGEST_RES_KEYS / 2 - 1) / (INGEST_RES_KEYS / 2), N),
-                       dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg, agents, overhead,
-                       reinterpret_cast<unsigned long long *>(keys));
+    const int nch = (np + INGEST_PTS - 1) / INGEST_PTS;  // point-pass chunks per frame
+    hipLaunchKernelGGL(ingest_points_kernel, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids,
+                       cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes);
+    hipLaunchKernelGGL(ingest_resolve_kernel, dim3(INGEST_RES_G, N), dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg, agents, overhead,
+                       reinterpret_cast<unsigned long long *>(keys), boxes, nch);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "ingest launch: %s", hipGetErrorString(e));
     return 0;

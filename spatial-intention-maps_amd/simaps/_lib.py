@@ -82,7 +82,7 @@ def _load(path=LIB_PATH):
     L.simaps_sp_distance.restype = i32
     L.simaps_shortest_path.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.simaps_shortest_path.restype = i32
-    L.simaps_ingest.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(Camera), i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.simaps_ingest.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(Camera), i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.simaps_ingest.restype = i32
     L.simaps_sssp_grid.argtypes = [i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp]
     L.simaps_sssp_grid.restype = i32

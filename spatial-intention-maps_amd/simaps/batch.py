@@ -329,6 +329,8 @@ class StateBatch:
         spec = cam_mod.CAMERAS[camera]
         agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
         idx = list(range(self.N)) if slots is None else [int(k) for k in slots]
+        if len(set(idx)) != len(idx):
+            raise ValueError('one frame per map slot and launch (slots repeat)')
         dep = torch.as_tensor(depth).to(device=self.device, dtype=torch.float32).contiguous()
         seg = torch.as_tensor(seg_raw).to(device=self.device, dtype=torch.int32).contiguous()
         want = (n, spec.height_px, spec.width_px)
@@ -345,6 +347,9 @@ class StateBatch:
             ids[e]['has_receptacle'] = sc['receptacle_position'] is not None
         if getattr(self, '_keys', None) is None:
             self._keys = torch.zeros((self.N, self.H, self.W), dtype=torch.int64, device=self.device)
+        nbox = n * -(-spec.height_px * spec.width_px // 2048) * 4  # per chunk of 2048 camera pixels
+        if getattr(self, '_boxes', None) is None or self._boxes.numel() < nbox:
+            self._boxes = torch.empty((nbox,), dtype=torch.int32, device=self.device)
         cam = _lib.Camera(spec.height_px, spec.width_px, spec.near, spec.far, spec.cx2, spec.cy2)
         return {'n': n, 'cam': cam, 'agents': agents_d, 'ids': _to_dev(ids, self.device),
                 'params': torch.from_numpy(params).to(self.device), 'depth': dep, 'seg': seg}
@@ -356,9 +361,9 @@ class StateBatch:
         _lib.check(_lib.lib.simaps_ingest(
             self.cfg, prep['cam'], prep['n'], _lib.ptr(prep['agents']), _lib.ptr(prep['ids']), _lib.ptr(prep['params']),
             _lib.ptr(prep['depth']), _lib.ptr(prep['seg']), _lib.ptr(self.overhead), _lib.ptr(self.occupancy),
-            _lib.ptr(self._keys), _lib.stream_handle(s)))
+            _lib.ptr(self._keys), _lib.ptr(self._boxes), _lib.stream_handle(s)))
         hold(s, cur, prep['ids'], prep['params'], prep['depth'], prep['seg'], prep['agents'], self.overhead,
-             self.occupancy, self._keys)
+             self.occupancy, self._keys, self._boxes)
 
 
 def sssp_grid(grids, sources, window=None, stream=None):

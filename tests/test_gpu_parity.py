@@ -290,8 +290,8 @@ def test_sssp_grid_random(S):
 
 @pytest.mark.parametrize('mode', ['random', 'eighths_and_negzero'])
 def test_overhead_values_outside_seg_codes(S, mode):
-    """The overhead crop is staged in LDS as k/8 byte codes (every SEG_VALUES entry); any other
-    value must switch that agent to the exact HBM gather path."""
+    """Overhead maps holding values other than the SEG_VALUES codes k/8 (random floats, -0.0, a code
+    the scene's seg values never use): the overhead channel gathers them unchanged, bit for bit."""
     batch, K, synthetic = S
     rs = np.random.RandomState(11)
     scenes = [synthetic.make_scene('lifting_4-small_divider', 900 + e) for e in range(4)]
