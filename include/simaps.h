@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SIMAPS_ABI_VERSION 3
+#define SIMAPS_ABI_VERSION 4
 
 /* error codes */
 #define SIMAPS_OK 0
@@ -207,12 +207,19 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
  *   agents[n].map_slot), from depth [N][Hc][Wc] float32 (pybullet depth buffer) and seg_raw
  *   [N][Hc][Wc] int32 (body ids), cam_params [N][9] fp64 = _get_camera_params(robot pose)
  *   (position, target, up; envs.py:1962-2008), seg_ids [E] per env.  keys: uint64 [M, H, W]
- *   scratch, all zero on entry and left zero; boxes: uint32 [N, ceil(Hc * Wc / 2048), 4] scratch
- *   (any contents).  The frames' map slots must be distinct.  All DEVICE.  Points with equal z on one pixel: the later camera pixel wins (the
- *   reference's np.argsort leaves that order unspecified).
+ *   scratch, all zero on entry and left zero; boxes: uint32 [N, simaps_ingest_chunks(Hc, Wc), 4]
+ *   scratch (any contents).  The frames' map slots must be distinct.  All DEVICE.  Points with
+ *   equal z on one pixel: the later camera pixel wins (the reference's np.argsort leaves that
+ *   order unspecified).
  *   SIMAPS_EUNSUPPORTED: camera width outside [69, 1024], Hc * Wc >= 2^28, N > 65535
- *   (two launches on `stream`: a point pass with per-chunk LDS max-reduction that also records each
- *   chunk's box of touched map pixels, then one sweep of each frame's box). */
+ *   (two launches on `stream`: a point pass over chunks of 2048 camera pixels with per-chunk LDS
+ *   max-reduction that also records each chunk's box of touched map pixels, then one sweep of each
+ *   frame's box). */
+
+/* Point-pass chunks (2048 camera pixels each) per frame of an Hc x Wc camera: the boxes scratch of
+ *   simaps_ingest holds 4 uint32 per chunk and frame.  SIMAPS_EINVAL for a non-positive size. */
+int simaps_ingest_chunks(int height_px, int width_px);
+
 int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, const simaps_agent *agents,
                   const simaps_seg_ids *seg_ids, const double *cam_params, const float *depth, const int32_t *seg_raw,
                   float *overhead, uint8_t *occupancy, uint64_t *keys, uint32_t *boxes, void *stream);

@@ -2918,6 +2918,7 @@ __device__ __forceinline__ int np_f32_to_i32(float v)
 // +30 us (LDS occupancy), workgroups looping over several chunks of a frame with the next chunk's
 // loads in flight +4..28 us: the per-chunk barrier chain wants many chunks in flight, not fewer)
 constexpr int INGEST_WG = 256, INGEST_PPT = 8, INGEST_PTS = INGEST_WG * INGEST_PPT;
+__host__ __device__ constexpr int ingest_chunks(int hc, int wc) { return (hc * wc + INGEST_PTS - 1) / INGEST_PTS; }
 constexpr int INGEST_WIN = 4096;  // LDS window entries (u64 keys) over a chunk's map-pixel box
 constexpr int INGEST_MAX_WC = 1024, INGEST_MAX_ROWS = 32;  // camera width; camera rows one chunk spans
 constexpr int INGEST_RES_WG = 256, INGEST_RES_U = 8, INGEST_RES_G = 8;  // resolve: 8 workgroups per frame, 8 keys per thread in flight
@@ -3367,6 +3368,12 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
     return 0;
 }
 
+int simaps_ingest_chunks(int height_px, int width_px)
+{
+    if (height_px <= 0 || width_px <= 0) return fail(SIMAPS_EINVAL, "bad camera size");
+    return ingest_chunks(height_px, width_px);
+}
+
 int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, const simaps_agent *agents,
                   const simaps_seg_ids *seg_ids, const double *cam_params, const float *depth, const int32_t *seg_raw,
                   float *overhead, uint8_t *occupancy, uint64_t *keys, uint32_t *boxes, void *stream)
@@ -3385,7 +3392,7 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
         return fail(SIMAPS_EUNSUPPORTED, "camera width %d outside [%d, %d]", cam->width_px, INGEST_PTS / (INGEST_MAX_ROWS - 2) + 1, INGEST_MAX_WC);
     if (np >= (1 << 28)) return fail(SIMAPS_EUNSUPPORTED, "camera frame of %d pixels (key packs pixel + 1 in 28 bits)", np);
     if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d frames per launch (grid y <= 65535)", N);
-    const int nch = (np + INGEST_PTS - 1) / INGEST_PTS;  // point-pass chunks per frame
+    const int nch = ingest_chunks(cam->height_px, cam->width_px);  // point-pass chunks per frame
     hipLaunchKernelGGL(ingest_points_kernel, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids,
                        cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes);
     hipLaunchKernelGGL(ingest_resolve_kernel, dim3(INGEST_RES_G, N), dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg, agents, overhead,

@@ -27,7 +27,7 @@ ROBOT_DTYPE = np.dtype([('x', '<f8'), ('y', '<f8'), ('heading', '<f8'), ('target
                         ('history_len', '<i4')], align=True)
 ENV_DTYPE = np.dtype([('receptacle_x', '<f8'), ('receptacle_y', '<f8'), ('has_receptacle', '<i4'),
                       ('robot_off', '<i4'), ('num_robots', '<i4'), ('reserved', '<i4')], align=True)
-ABI_VERSION = 3  # include/simaps.h SIMAPS_ABI_VERSION
+ABI_VERSION = 4  # include/simaps.h SIMAPS_ABI_VERSION
 AGENT_DTYPE = np.dtype([('env', '<i4'), ('robot', '<i4'), ('map_slot', '<i4')], align=True)
 assert ROBOT_DTYPE.itemsize == 72 and ENV_DTYPE.itemsize == 32 and AGENT_DTYPE.itemsize == 12
 
@@ -84,6 +84,8 @@ def _load(path=LIB_PATH):
     L.simaps_shortest_path.restype = i32
     L.simaps_ingest.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(Camera), i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.simaps_ingest.restype = i32
+    L.simaps_ingest_chunks.argtypes = [i32, i32]
+    L.simaps_ingest_chunks.restype = i32
     L.simaps_sssp_grid.argtypes = [i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp]
     L.simaps_sssp_grid.restype = i32
     L.simaps_grid_path.argtypes = [i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]
@@ -98,7 +100,7 @@ def _load(path=LIB_PATH):
 lib = _load()
 
 EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_fault_status', 'simaps_num_channels',
-            'simaps_robot_mask', 'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest',
+            'simaps_robot_mask', 'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest', 'simaps_ingest_chunks',
             'simaps_sssp_grid', 'simaps_grid_path')
 
 # error codes and device fault bits (include/simaps.h)

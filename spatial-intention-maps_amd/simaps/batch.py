@@ -347,7 +347,10 @@ class StateBatch:
             ids[e]['has_receptacle'] = sc['receptacle_position'] is not None
         if getattr(self, '_keys', None) is None:
             self._keys = torch.zeros((self.N, self.H, self.W), dtype=torch.int64, device=self.device)
-        nbox = n * -(-spec.height_px * spec.width_px // 2048) * 4  # per chunk of 2048 camera pixels
+        nch = _lib.lib.simaps_ingest_chunks(spec.height_px, spec.width_px)  # point-pass chunks per frame
+        if nch < 0:
+            _lib.check(nch)
+        nbox = n * nch * 4
         if getattr(self, '_boxes', None) is None or self._boxes.numel() < nbox:
             self._boxes = torch.empty((nbox,), dtype=torch.int32, device=self.device)
         cam = _lib.Camera(spec.height_px, spec.width_px, spec.near, spec.far, spec.cx2, spec.cy2)

@@ -20,7 +20,7 @@ def declared_symbols():
 def test_header_declares_the_abi():
     assert declared_symbols() == sorted(['simaps_abi_version', 'simaps_last_error', 'simaps_fault_status',
                                          'simaps_num_channels', 'simaps_sp_distance', 'simaps_shortest_path',
-                                         'simaps_ingest', 'simaps_robot_mask', 'simaps_get_state', 'simaps_sssp_grid',
+                                         'simaps_ingest', 'simaps_ingest_chunks', 'simaps_robot_mask', 'simaps_get_state', 'simaps_sssp_grid',
                                          'simaps_grid_path'])
 
 
@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(_lib.lib, name), name
         assert isinstance(getattr(_lib.lib, name), ctypes._CFuncPtr)
     assert set(_lib.EXPORTED) == set(declared_symbols())
-    assert _lib.lib.simaps_abi_version() == 3
+    assert _lib.lib.simaps_abi_version() == 4
 
 
 def test_struct_layouts_match_header():
