@@ -3,7 +3,7 @@ through the C ABI in one launch per configuration and compared bitwise with the 
 workers in a process pool; the nonspatial intention channels within 1e-7, like the GPU tests).
 Seeds 5000+ are used by no test.  Prints one JSON line per configuration and a total.
 
-    python tools/fuzz_states.py [envs_per_config] [procs]
+    python tools/fuzz_states.py [envs_per_config] [procs] [--perturb]
 """
 import json
 import os
@@ -24,16 +24,42 @@ CONFIGS = ['lifting_1-small_empty', 'lifting_4-small_divider', 'pushing_4-large_
 SEED0 = 5000
 
 
+def perturbed_scene(cfg, e, perturb):
+    """make_scene(cfg, SEED0 + e); with perturb, robots anywhere in the room but 2 cm from its edge
+    (next to walls, on dividers: the snap slow path), headings half the time on exact multiples of
+    45 deg (+-pi, -0.0 included), positions half the time on pixel corners, random idle flags, and
+    one shortest_path_map_scale per configuration from {-0.5, 0, 0.25, 3}."""
+    from simaps import synthetic
+    s = synthetic.make_scene(cfg, SEED0 + e)
+    if not perturb:
+        return s
+    rs = np.random.RandomState(SEED0 + 7919 * e + 1)
+    rl, rw, H, W = s['room_length'], s['room_width'], s['H'], s['W']
+    for r in s['robots']:
+        x, y = rs.uniform(-rl / 2 + 0.02, rl / 2 - 0.02), rs.uniform(-rw / 2 + 0.02, rw / 2 - 0.02)
+        if rs.rand() < 0.5:
+            x, y = (np.floor(W / 2 + x * 96) - W / 2) / 96.0, (H / 2 - np.floor(H / 2 - y * 96)) / 96.0
+        r['position'] = (float(x), float(y), 0)
+        r['waypoint_positions'] = [r['position']] + list(r['waypoint_positions'][1:])
+        r['heading'] = float(rs.choice([-np.pi, np.pi, -0.0, 0.0, np.pi / 4, -3 * np.pi / 4, np.pi / 2])
+                             if rs.rand() < 0.5 else rs.uniform(-np.pi, np.pi))
+        r['idle'] = bool(rs.rand() < 0.25)
+    scale = [-0.5, 0.0, 0.25, 3.0][sum(map(ord, cfg)) % 4]
+    s['flags'] = dict(s['flags'], shortest_path_map_scale=scale)
+    return s
+
+
 def _oracle(job):
     import oracle as O
-    from simaps import synthetic
-    cfg, e, a = job
-    return O.agent_state(synthetic.make_scene(cfg, SEED0 + e), a)
+    cfg, e, a, perturb = job
+    return O.agent_state(perturbed_scene(cfg, e, perturb), a)
 
 
 def main():
-    envs = int(sys.argv[1]) if len(sys.argv) > 1 else 16
-    procs = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+    args = [a for a in sys.argv[1:] if not a.startswith('--')]
+    perturb = '--perturb' in sys.argv
+    envs = int(args[0]) if len(args) > 0 else 16
+    procs = int(args[1]) if len(args) > 1 else 16
     import torch
     from simaps import batch, synthetic
     from test_gpu_parity import _nonspatial_slice
@@ -41,11 +67,11 @@ def main():
     with get_context('spawn').Pool(procs) as pool:
         for cfg in CONFIGS:
             t0 = time.time()
-            scenes = [synthetic.make_scene(cfg, SEED0 + e) for e in range(envs)]
+            scenes = [perturbed_scene(cfg, e, perturb) for e in range(envs)]
             b = batch.StateBatch(scenes)
             st = b.as_hwc(b.render()).cpu().numpy()
             torch.cuda.synchronize()
-            refs = pool.map(_oracle, [(cfg, e, a) for e, a in b.agents], chunksize=4)
+            refs = pool.map(_oracle, [(cfg, e, a, perturb) for e, a in b.agents], chunksize=4)
             nb = 0
             for n, (e, a) in enumerate(b.agents):
                 ns = _nonspatial_slice(scenes[e]['flags'], len(scenes[e]['robots']))
@@ -59,11 +85,15 @@ def main():
                                          np.ascontiguousarray(ref[..., m]).view(np.int32))
                           and np.abs(got[..., ns] - ref[..., ns]).max() <= 1e-7)
                 nb += not ok
+            # negative control: the checker must see a difference between two different agents
+            control = len(b.agents) < 2 or not np.array_equal(st[0].view(np.int32), refs[1].view(np.int32))
+            assert control, 'checker is vacuous'
             total += len(b.agents)
             bad += nb
-            print(json.dumps({'config': cfg, 'stacks': len(b.agents), 'mismatches': nb, 's': round(time.time() - t0, 1)}),
-                  flush=True)
-    print(json.dumps({'total_stacks': total, 'mismatches': bad, 'seeds': [SEED0, SEED0 + envs - 1]}), flush=True)
+            print(json.dumps({'config': cfg, 'stacks': len(b.agents), 'mismatches': nb, 's': round(time.time() - t0, 1),
+                              'perturbed': perturb}), flush=True)
+    print(json.dumps({'total_stacks': total, 'mismatches': bad, 'seeds': [SEED0, SEED0 + envs - 1], 'perturbed': perturb}),
+          flush=True)
 
 
 if __name__ == '__main__':
