@@ -2416,23 +2416,53 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
     sssp(sh, S, dist, 1);  // the source's distance image (GridGraph._spfa_with_cache, pyx:116-119)
     if (tid == 0) post_faults(fault, group_faults(sh.bar, sh.rounds, 1));
     const int pw = sssp_pitch(sh.w);
-    for (int q0 = 0; q0 < Q; q0 += 2) {  // targets snapped two at a time (snap_sources' slots)
-        const int nq = Q - q0 < 2 ? Q - q0 : 2;
-        if (tid < nq) {
-            const double *t = targets + 2 * ((size_t)n * Q + q0 + tid);
-            pos_to_pix(t[0], t[1], H, W, sh.src_q[tid][0], sh.src_q[tid][1]);
+    // dists[target] (pyx:156-163) as a Python float / LOCAL_MAP_PIXELS_PER_METER; unreachable -> -1
+    // (pyx:110-112)
+    auto lookup = [&](int si, int sj) {
+        float d = -1.0f;
+        if (src_ok) {
+            const float v = dist[(si - sh.i0 + 1) * pw + (sj - sh.j0 + 1)];
+            if (v != INFINITY) d = v;
         }
-        lds_barrier();
-        snap_sources(sh, S, nq, whole_wg());
-        if (tid < nq) {
-            float d = -1.0f;  // dists[target] (pyx:156-163); unreachable -> -1 (pyx:110-112)
-            if (src_ok && sh.src_ok[tid]) {
-                const float v = dist[(sh.src_s[tid][0] - sh.i0 + 1) * pw + (sh.src_s[tid][1] - sh.j0 + 1)];
-                if (v != INFINITY) d = v;
+        return (double)d / PPM;
+    };
+    uint64_t &slow_mask = sh.dirty[0][0][0];  // (the SSSP's dirty masks are free now)
+    for (int c0 = 0; c0 < Q; c0 += 64) {
+        // wave 0, one lane per target: a free target pixel is its own snapped cell (EDT distance 0)
+        const int cn = Q - c0 < 64 ? Q - c0 : 64;
+        if (tid < 64) {
+            bool slow = false;
+            if (tid < cn) {
+                const double *t = targets + 2 * ((size_t)n * Q + c0 + tid);
+                int qi, qj;
+                pos_to_pix(t[0], t[1], H, W, qi, qj);
+                const int qr = qi - sh.i0, qc = qj - sh.j0;
+                if (qr >= 0 && qr < sh.h && qc >= 0 && qc < sh.w && b_test(S.freeb[qr], qc))
+                    out[(size_t)n * Q + c0 + tid] = lookup(qi, qj);
+                else
+                    slow = true;
             }
-            out[(size_t)n * Q + q0 + tid] = (double)d / PPM;  // Python float / LOCAL_MAP_PIXELS_PER_METER
+            const uint64_t m = __ballot(slow);
+            if (tid == 0) slow_mask = m;
         }
         lds_barrier();
+        // the others through the EDT feature transform, two at a time (snap_sources' slots)
+        for (uint64_t m = slow_mask; m;) {
+            int q[2] = {0, 0}, nq = 0;
+            while (m && nq < 2) {
+                q[nq++] = c0 + __builtin_ctzll(m);
+                m &= m - 1;
+            }
+            if (tid < nq) {
+                const double *t = targets + 2 * ((size_t)n * Q + q[tid]);
+                pos_to_pix(t[0], t[1], H, W, sh.src_q[tid][0], sh.src_q[tid][1]);
+            }
+            lds_barrier();
+            snap_sources(sh, S, nq, whole_wg());
+            if (tid < nq) out[(size_t)n * Q + q[tid]] = sh.src_ok[tid] ? lookup(sh.src_s[tid][0], sh.src_s[tid][1]) : -1.0 / PPM;
+            lds_barrier();
+        }
+        if (c0 + 64 < Q) lds_barrier();  // every wave has read slow_mask before the next chunk rewrites it
     }
 }
 

@@ -128,6 +128,26 @@ def test_sp_distance_reference_goldens(V):
         assert np.array_equal(got, want), cfg
 
 
+def test_sp_distance_many_targets_vs_oracle(V):
+    """130 targets per agent (three chunks of the kernel's lane-parallel fast snap), a third of them
+    in walls / the divider / outside the room (the EDT slow path), some robots standing in walls."""
+    synthetic, vector_env = V
+    from simaps import batch
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 80 + e) for e in range(3)]
+    rs = np.random.RandomState(9)
+    for s in scenes:
+        s['robots'][0]['position'] = (0.0, rs.uniform(-0.2, 0.2), 0)   # on the divider
+    b = batch.StateBatch(scenes)
+    Q = 130
+    src = np.array([scenes[e]['robots'][a]['position'][:2] for e, a in b.agents])
+    tgt = np.stack([rs.uniform(-0.3, 0.3, (b.N, Q)), rs.uniform(-0.3, 0.3, (b.N, Q))], -1)
+    tgt[:, ::3, 0] = rs.choice([0.0, -0.5, 0.5, 0.55], (b.N, len(range(0, Q, 3))))  # divider, walls, outside
+    got = b.shortest_path_distances(src, tgt).cpu().numpy()
+    for n, (e, a) in enumerate(b.agents):
+        ao = O.AgentOracle(scenes[e], a)
+        assert got[n].tolist() == [ao.shortest_path_distance(src[n], t) for t in tgt[n]], (e, a)
+
+
 def test_distance_to_receptacle_dropin(V):
     synthetic, vector_env = V
     scenes = [synthetic.make_scene('lifting_2_throwing_2-large_empty', 70 + e) for e in range(3)]
