@@ -2939,9 +2939,9 @@ __device__ __forceinline__ int np_f32_to_i32(float v)
 //                         value (a sum of 1/8 multiples < 2, exact in f32) travels as seg * 8 in the
 //                         key's low 4 bits, so the winner's value needs no second look-up.
 //                         Each chunk also stores its box (boxes[n][chunk]).
-//   ingest_resolve_kernel 8 workgroups per frame: a sweep of the frame's box of the slot's key map
-//                         (not the whole map: a forward camera touches ~10 % of it): a nonzero key
-//                         writes overhead = code / 8 and is zeroed again; the box is reset.
+//   ingest_resolve_kernel 8 workgroups per frame: a sweep of the frame's box (the union of its chunk
+//                         boxes) of the slot's key map, not the whole map (a forward camera's box is
+//                         ~34 % of it): a nonzero key writes overhead = code / 8 and is zeroed again.
 // HBM per frame: 8 B per camera pixel (depth + seg) + 8 B per pixel of the box (key sweep) + the
 // pixel writes; the atomics resolve in L2 (a frame's key map is <= 0.4 MB).
 // (measured alternatives, 256 frames: 128- / 64-thread chunks +4 / +21 us, an 8192-entry window
