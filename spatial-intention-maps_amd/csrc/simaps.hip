@@ -2935,7 +2935,7 @@ __device__ __forceinline__ int np_f32_to_i32(float v)
 //                         forward camera ~30), so atomics straight from the points serialised on a
 //                         few L2 lines (547 us per 256 frames); an LDS hash table cost 22 us of
 //                         init / scan on top of the reduction (95 us).  A box larger than the LDS
-//                         window falls back to global atomics per run of equal pixels.  The seg
+//                         window uses a direct-mapped (pixel tag, key) table in the same LDS.  The seg
 //                         value (a sum of 1/8 multiples < 2, exact in f32) travels as seg * 8 in the
 //                         key's low 4 bits, so the winner's value needs no second look-up.
 //                         Each chunk also stores its box (boxes[n][chunk]).
@@ -3103,10 +3103,34 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
         if (tid == 0)  // the chunk's box of map pixels [i0, i1) x [j0, j1), for the resolve sweep
             reinterpret_cast<uint4 *>(boxes)[(size_t)n * gridDim.x + blockIdx.x] =
                 make_uint4((unsigned)bi, (unsigned)(bi + bh), (unsigned)bj, (unsigned)(bj + bw));
-        if (area > INGEST_WIN) {   // fallback: global atomics per run
+        if (area > INGEST_WIN) {
+            // box past the window (a forward camera's far rows: ~2-3 points per pixel, spread wide;
+            // global atomics per run instead measured 3 us more per 256 frames):
+            // a direct-mapped table of HS (pixel tag, key) slots in the window's LDS.
+            // Each pixel's tag is written by its points (any one wins); points whose pixel owns the
+            // slot max-reduce there, the others (collisions) go straight to the global key map;
+            // then one global atomic per used slot.
+            constexpr int HS = INGEST_WIN * 2 / 3;  // keys (8 B) + tags (4 B) in the 32 KB window
+            unsigned long long *hk = win;
+            int *ht = reinterpret_cast<int *>(win + HS);
+            for (int e = tid; e < HS; e += INGEST_WG) hk[e] = 0ull, ht[e] = -1;
+            __syncthreads();
 #pragma unroll
             for (int q = 0; q < INGEST_PPT; q++)
-                if (pix[q] >= 0) atomicMax(&keys[base + pix[q]], key[q]);
+                if (pix[q] >= 0) ht[(unsigned)pix[q] % HS] = pix[q];
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < INGEST_PPT; q++)
+                if (pix[q] >= 0) {
+                    const int h = (unsigned)pix[q] % HS;
+                    if (ht[h] == pix[q]) atomicMax(&hk[h], key[q]);
+                    else atomicMax(&keys[base + pix[q]], key[q]);
+                }
+            __syncthreads();
+            for (int e = tid; e < HS; e += INGEST_WG) {
+                const unsigned long long v = hk[e];
+                if (v) atomicMax(&keys[base + ht[e]], v);
+            }
             return;
         }
         for (int e = tid; e < area; e += INGEST_WG) win[e] = 0ull;
