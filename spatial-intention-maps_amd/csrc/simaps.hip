@@ -3440,13 +3440,13 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
     if (N == 0) return 0;
     if (!agents || !seg_ids || !cam_params || !depth || !seg_raw || !overhead || !occupancy || !keys || !boxes)
         return fail(SIMAPS_EINVAL, "NULL buffer");
-    if ((rc = pending_faults())) return rc;
     const int np = cam->height_px * cam->width_px;
     if (cam->width_px > INGEST_MAX_WC || INGEST_PTS / cam->width_px + 2 > INGEST_MAX_ROWS)
         return fail(SIMAPS_EUNSUPPORTED, "camera width %d outside [%d, %d]", cam->width_px, INGEST_PTS / (INGEST_MAX_ROWS - 2) + 1, INGEST_MAX_WC);
     if (np >= (1 << 28)) return fail(SIMAPS_EUNSUPPORTED, "camera frame of %d pixels (key packs pixel + 1 in 28 bits)", np);
     if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d frames per launch (grid y <= 65535)", N);
     const int nch = ingest_chunks(cam->height_px, cam->width_px);  // point-pass chunks per frame
+    if ((rc = pending_faults())) return rc;  // (after the argument checks: they need no device)
     hipLaunchKernelGGL(ingest_points_kernel, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids,
                        cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes);
     hipLaunchKernelGGL(ingest_resolve_kernel, dim3(INGEST_RES_G, N), dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg, agents, overhead,

@@ -89,3 +89,24 @@ def test_statebatch_refuses_cpu_device():
     from simaps import batch, synthetic
     with pytest.raises(ValueError):
         batch.StateBatch([synthetic.make_scene('lifting_1-small_empty', 0)], device='cpu')
+
+
+def test_ingest_chunk_count_and_argument_checks():
+    """simaps_ingest_chunks sizes the boxes scratch (one entry per 2048 camera pixels); simaps_ingest
+    refuses bad cameras, NULL buffers and unsupported widths before any launch."""
+    import ctypes
+    from simaps import _lib, batch, camera, synthetic
+    L = _lib.lib
+    for h, w in ((156, 277), (156, 156), (1, 1), (64, 32)):
+        assert L.simaps_ingest_chunks(h, w) == -(-h * w // 2048)
+    assert L.simaps_ingest_chunks(0, 277) == _lib.EINVAL
+    c = batch.make_config(synthetic.config_flags('lifting_4-small_divider'), 0.5, 1.0)
+    spec = camera.CAMERAS['forward']
+    cam = _lib.Camera(spec.height_px, spec.width_px, spec.near, spec.far, spec.cx2, spec.cy2)
+    assert L.simaps_ingest(c, cam, 0, *([None] * 9), None) == 0                     # nothing to do
+    assert L.simaps_ingest(c, cam, 1, *([None] * 9), None) == _lib.EINVAL           # NULL buffers
+    bad = _lib.Camera(spec.height_px, spec.width_px, spec.far, spec.near, spec.cx2, spec.cy2)
+    assert L.simaps_ingest(c, bad, 1, *([None] * 9), None) == _lib.EINVAL           # near >= far
+    p = ctypes.c_void_p(8)  # never dereferenced: the width check comes first
+    wide = _lib.Camera(8, 2000, spec.near, spec.far, spec.cx2, spec.cy2)
+    assert L.simaps_ingest(c, wide, 1, *([p] * 9), None) == _lib.EUNSUPPORTED
