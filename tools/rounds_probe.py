@@ -1,3 +1,6 @@
+"""SSSP round counts per agent (the debug status word: rounds << 8) of a config's batch, and the
+launch time with and without the debug outputs.  Diagnostic only.
+    python tools/rounds_probe.py CONFIG ENVS"""
 import sys, os, time
 sys.path.insert(0, 'spatial-intention-maps_amd')
 import numpy as np, torch
