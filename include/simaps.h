@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SIMAPS_ABI_VERSION 4
+#define SIMAPS_ABI_VERSION 5
 
 /* error codes */
 #define SIMAPS_OK 0
@@ -69,6 +69,15 @@ extern "C" {
 #define SIMAPS_ENC_BINARY 1
 #define SIMAPS_ENC_LINE 2
 #define SIMAPS_ENC_CIRCLE 3
+
+/* rotate_rounding: scipy.ndimage.rotate (envs.py:2206, 2267) computes out_center = M @ ((S-1)/2)
+ * through numpy matmul -> BLAS dgemv, whose rounding depends on the numpy/OpenBLAS build and the host
+ * CPU: fma(M[r][0], a0, M[r][1] * a1) on some (numpy 2.2 here, the round-1 builder host), the plain
+ * M[r][0] * a0 + M[r][1] * a1 on others (numpy 1.26.4 / OpenBLAS 0.3.23 on an AVX-512 Xeon).  About
+ * 4 % of headings give a different sample grid.  Pick the form of the host the reference runs on
+ * (simaps.constants.host_rotate_rounding() measures it). */
+#define SIMAPS_ROT_FMA 0
+#define SIMAPS_ROT_PLAIN 1
 
 /* limits of this build */
 #define SIMAPS_MAX_ROBOTS 8      /* robots per env */
@@ -127,7 +136,7 @@ typedef struct simaps_config {
     int32_t use_intention_channels;
     int32_t intention_channel_spatial; /* 1 = 'spatial', 0 = 'nonspatial' */
     int32_t layout_chw;             /* 0: state is [N,96,96,C] (reference HWC), 1: [N,C,96,96] */
-    int32_t reserved;
+    int32_t rotate_rounding;        /* SIMAPS_ROT_*: how the host BLAS rounds scipy.ndimage.rotate's out_center */
     double distance_to_receptacle_map_scale;
     double shortest_path_map_scale;
     double intention_map_scale;

@@ -51,7 +51,7 @@ def lib():
         L.oracle_sindg.restype = ctypes.c_double
         L.oracle_cosdg.argtypes = [ctypes.c_double]
         L.oracle_cosdg.restype = ctypes.c_double
-        L.oracle_rotate_params.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
+        L.oracle_rotate_params.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         L.oracle_rotate_params.restype = None
         _lib = L
     return _lib
@@ -205,22 +205,25 @@ def edt_indices(img):
     return ft
 
 
-def rotate_params(n, angle):
+def rotate_params(n, angle, rounding='fma'):
     """scipy.ndimage.rotate(reshape=True) geometry for an n x n input (scipy interpolation.py:909-930).
 
     Returns (S0, S1, (c, s), offset) -- see oracle_rotate_params in oracle_c.c for the exact
-    rounding (out_center pinned to the oracle host's BLAS FMA by tests/golden/rotate.npz)."""
+    rounding.  rounding: how the host BLAS dgemv rounds out_center, 'fma' (pinned by
+    tests/golden/rotate.npz) or 'plain' (tests/golden/rotate_plain.npz)."""
+    if rounding not in ('fma', 'plain'):
+        raise ValueError('rounding must be fma or plain')
     out = (ctypes.c_double * 6)()
-    lib().oracle_rotate_params(int(n), float(angle), out)
+    lib().oracle_rotate_params(int(n), float(angle), int(rounding == 'plain'), out)
     return int(out[0]), int(out[1]), (out[2], out[3]), (out[4], out[5])
 
 
-def rotate_index_map(n, angle):
+def rotate_index_map(n, angle, rounding='fma'):
     """Order-0 rotate as an index map: (src_i, src_j, valid) arrays of the output shape.
 
     Output pixel o takes input[floor(src + 0.5)] when 0 <= src <= n-1 on both axes, else cval,
     src = (o0*M[r][0] + o1*M[r][1]) + offset[r] (scipy ni_interpolation.c geometric transform)."""
-    S0, S1, (c, s), (f0, f1) = rotate_params(n, angle)
+    S0, S1, (c, s), (f0, f1) = rotate_params(n, angle, rounding)
     o0 = np.arange(S0, dtype=np.float64)[:, None]
     o1 = np.arange(S1, dtype=np.float64)[None, :]
     src0 = (o0 * c + o1 * s) + f0
@@ -231,11 +234,11 @@ def rotate_index_map(n, angle):
     return i0, i1, valid
 
 
-def rotate(img, angle):
+def rotate(img, angle, rounding='fma'):
     """scipy.ndimage.rotate(img, angle, order=0) (reshape=True, cval=0) for square img."""
     n = img.shape[0]
     assert img.shape == (n, n)
-    i0, i1, valid = rotate_index_map(n, angle)
+    i0, i1, valid = rotate_index_map(n, angle, rounding)
     out = np.zeros(i0.shape, dtype=img.dtype)
     out[valid] = img[i0[valid], i1[valid]]
     return out
@@ -384,6 +387,7 @@ class AgentOracle:
         self.occupancy = scene['occupancy'][agent]
         self.overhead_wo = scene['overhead'][agent]
         self.receptacle = scene['receptacle_position']
+        self.rounding = scene.get('rotate_rounding', 'fma')  # host BLAS out_center rounding (oracle_c.c)
         self._update()
 
     # OccupancyMap.update (envs.py:2445-2460), minus the point scatter (occupancy is the input)
@@ -443,7 +447,7 @@ class AgentOracle:
         angle = 90 - math.degrees(self.robot['heading'])
         pi, pj = position_to_pixel_indices(self.robot['position'][0], self.robot['position'][1], global_map.shape)
         crop = global_map[pi - cw // 2:pi + cw // 2, pj - cw // 2:pj + cw // 2]
-        rc = rotate(crop, angle)
+        rc = rotate(crop, angle, self.rounding)
         return rc[rc.shape[0] // 2 - LW // 2:rc.shape[0] // 2 + LW // 2,
                   rc.shape[1] // 2 - LW // 2:rc.shape[1] // 2 + LW // 2]
 
@@ -464,7 +468,7 @@ class AgentOracle:
                     vis = robot_mask('lifting_robot', show_lifted_cube=True).copy()
                 else:
                     vis *= np.float32(0.5)
-            rot = rotate(vis, math.degrees(r['heading']) - 90)
+            rot = rotate(vis, math.degrees(r['heading']) - 90, self.rounding)
             pi, pj = position_to_pixel_indices(r['position'][0], r['position'][1], self.shape)
             si, sj = pi - rot.shape[0] // 2, pj - rot.shape[1] // 2
             gm[si:si + rot.shape[0], sj:sj + rot.shape[1]] = np.maximum(

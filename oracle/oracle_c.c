@@ -220,12 +220,17 @@ double oracle_cosdg(double x) { return dg_core(x, 1); }
  * scipy.ndimage.rotate(reshape=True) geometry for an n x n input (scipy interpolation.py:909-930)
  *   out_bounds = M @ [[0,0,n,n],[0,n,0,n]] -> S = int(ptp + 0.5)        (plain products/sums)
  *   out_center = M @ ((S - 1) / 2)                                        (numpy matmul -> BLAS
- *       dgemv: pinned by tests/golden/rotate.npz to fma(M[r][0], a0, M[r][1] * a1), i.e. the
- *       OpenBLAS FMA kernel of the oracle host; the non-fused form mismatches ~half the angles)
+ *       dgemv, whose rounding is a property of the host's numpy / OpenBLAS build:
+ *       plain == 0: fma(M[r][0], a0, M[r][1] * a1) -- the FMA kernel (numpy 2.2.6 here; the
+ *                   round-1 builder host's numpy 1.26.4), pinned by tests/golden/rotate.npz;
+ *       plain == 1: M[r][0] * a0 + M[r][1] * a1 -- numpy 1.26.4 / OpenBLAS 0.3.23 on this
+ *                   AVX-512 Xeon, pinned by tests/golden/rotate_plain.npz.
+ *       Each form matches its host on every golden angle and the other on only ~50-55 % of
+ *       them, ~4 % of random headings giving a different sample grid.)
  *   offset = (n - 1) / 2 - out_center
  * out: {S0, S1, c, s, off0, off1}
  * ------------------------------------------------------------------------------------------ */
-void oracle_rotate_params(int n, double angle, double *out)
+void oracle_rotate_params(int n, double angle, int plain, double *out)
 {
     double c = oracle_cosdg(angle), s = oracle_sindg(angle);
     double iy = n, ix = n;
@@ -240,8 +245,8 @@ void oracle_rotate_params(int n, double angle, double *out)
     }
     long S0 = (long)(mx0 - mn0 + 0.5), S1 = (long)(mx1 - mn1 + 0.5);
     double a0 = (double)(S0 - 1) / 2, a1 = (double)(S1 - 1) / 2;
-    double oc0 = fma(c, a0, s * a1);
-    double oc1 = fma(-s, a0, c * a1);
+    double oc0 = plain ? c * a0 + s * a1 : fma(c, a0, s * a1);
+    double oc1 = plain ? -s * a0 + c * a1 : fma(-s, a0, c * a1);
     double inc = (double)(n - 1) / 2;
     out[0] = (double)S0; out[1] = (double)S1; out[2] = c; out[3] = s;
     out[4] = inc - oc0; out[5] = inc - oc1;

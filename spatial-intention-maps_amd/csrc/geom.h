@@ -81,14 +81,15 @@ SIMAPS_HD double dg_core(double x, bool want_cos)
 // ---- scipy.ndimage.rotate(input n x n, angle, order=0, reshape=True) geometry ------------------
 // scipy interpolation.py (1.7.1) 909-930; output pixel o samples input[floor(src + 0.5)] iff
 // 0 <= src <= n-1 on both axes (else cval 0), src_r = (o0 * M[r][0] + o1 * M[r][1]) + off_r.
-// out_center = M @ ((S-1)/2) goes through numpy matmul -> BLAS dgemv, whose rounding on the
-// oracle host is fma(M[r][0], a0, M[r][1] * a1) (pinned by tests/golden/rotate.npz).
+// out_center = M @ ((S-1)/2) goes through numpy matmul -> BLAS dgemv, whose rounding depends on the
+// host's numpy / OpenBLAS build: fma(M[r][0], a0, M[r][1] * a1) (plain = false; pinned by
+// tests/golden/rotate.npz) or M[r][0] * a0 + M[r][1] * a1 (plain = true; tests/golden/rotate_plain.npz).
 struct Rot {
     double c, s, f0, f1;
     int S0, S1;
 };
 
-SIMAPS_HD Rot rot_params(int n, double angle)
+SIMAPS_HD Rot rot_params(int n, double angle, bool plain)
 {
     Rot R;
     const double c = dg_core(angle, true), s = dg_core(angle, false);
@@ -105,8 +106,8 @@ SIMAPS_HD Rot rot_params(int n, double angle)
     R.S0 = (int)(mx0 - mn0 + 0.5);
     R.S1 = (int)(mx1 - mn1 + 0.5);
     const double a0 = (double)(R.S0 - 1) / 2, a1 = (double)(R.S1 - 1) / 2;
-    const double oc0 = fma(c, a0, s * a1);
-    const double oc1 = fma(-s, a0, c * a1);
+    const double oc0 = plain ? c * a0 + s * a1 : fma(c, a0, s * a1);
+    const double oc1 = plain ? -s * a0 + c * a1 : fma(-s, a0, c * a1);
     const double inc = (double)(n - 1) / 2;
     R.c = c;
     R.s = s;

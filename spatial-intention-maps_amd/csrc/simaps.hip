@@ -2151,7 +2151,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         }
         if (t == 64) {
             const simaps_robot &me = rb[ag.robot];
-            sh.rot = rot_params(CROP, 90.0 - me.heading * RAD_TO_DEG);
+            sh.rot = rot_params(CROP, 90.0 - me.heading * RAD_TO_DEG, cfg.rotate_rounding == SIMAPS_ROT_PLAIN);
             pos_to_pix(me.x, me.y, H, W, sh.pi, sh.pj);
             STAMP_NB(72);
         }
@@ -2162,7 +2162,7 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             if ((cfg.use_intention_map && r.intention_len > SIMAPS_MAX_PATH) ||
                 (cfg.use_history_map && r.history_len > SIMAPS_MAX_PATH))  // cut to SIMAPS_MAX_PATH points
                 __hip_atomic_store(&sh.bar[0][3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const Rot R = rot_params(LW, r.heading * RAD_TO_DEG - 90.0);
+            const Rot R = rot_params(LW, r.heading * RAD_TO_DEG - 90.0, cfg.rotate_rounding == SIMAPS_ROT_PLAIN);
             P.c = R.c; P.s = R.s; P.f0 = R.f0; P.f1 = R.f1; P.S0 = R.S0; P.S1 = R.S1;
             int pi, pj;
             pos_to_pix(r.x, r.y, H, W, pi, pj);
@@ -3314,6 +3314,8 @@ int check_cfg(const simaps_config *c)
     if (c->intention_map_line_thickness < 1 || c->intention_map_line_thickness > 2)
         return fail(SIMAPS_EUNSUPPORTED, "intention_map_line_thickness must be 1 or 2");
     if (c->intention_map_scale < 0) return fail(SIMAPS_EUNSUPPORTED, "negative intention_map_scale");
+    if (c->rotate_rounding != SIMAPS_ROT_FMA && c->rotate_rounding != SIMAPS_ROT_PLAIN)
+        return fail(SIMAPS_EINVAL, "bad rotate_rounding %d", c->rotate_rounding);
     return 0;
 }
 }  // namespace

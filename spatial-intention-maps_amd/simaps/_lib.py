@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get('SIMAPS_LIB', os.path.join(HERE, 'libsimaps.so'))
 LIFTING, PUSHING, THROWING, RESCUE = 0, 1, 2, 3
 TYPE_IDS = {'lifting_robot': LIFTING, 'pushing_robot': PUSHING, 'throwing_robot': THROWING, 'rescue_robot': RESCUE}
 ENC_IDS = {'ramp': 0, 'binary': 1, 'line': 2, 'circle': 3}
+ROT_IDS = {'fma': 0, 'plain': 1}  # SIMAPS_ROT_* (include/simaps.h)
 MAX_ROBOTS = 8
 MAX_PATH = 16
 
@@ -27,7 +28,7 @@ ROBOT_DTYPE = np.dtype([('x', '<f8'), ('y', '<f8'), ('heading', '<f8'), ('target
                         ('history_len', '<i4')], align=True)
 ENV_DTYPE = np.dtype([('receptacle_x', '<f8'), ('receptacle_y', '<f8'), ('has_receptacle', '<i4'),
                       ('robot_off', '<i4'), ('num_robots', '<i4'), ('reserved', '<i4')], align=True)
-ABI_VERSION = 4  # include/simaps.h SIMAPS_ABI_VERSION
+ABI_VERSION = 5  # include/simaps.h SIMAPS_ABI_VERSION
 AGENT_DTYPE = np.dtype([('env', '<i4'), ('robot', '<i4'), ('map_slot', '<i4')], align=True)
 assert ROBOT_DTYPE.itemsize == 72 and ENV_DTYPE.itemsize == 32 and AGENT_DTYPE.itemsize == 12
 
@@ -47,7 +48,7 @@ class Config(ctypes.Structure):
         'H', 'W', 'room_i0', 'room_j0', 'room_h', 'room_w', 'use_robot_map', 'use_distance_to_receptacle_map',
         'use_shortest_path_to_receptacle_map', 'use_shortest_path_map', 'use_intention_map',
         'intention_map_encoding', 'intention_map_line_thickness', 'use_history_map', 'use_intention_channels',
-        'intention_channel_spatial', 'layout_chw', 'reserved')] + \
+        'intention_channel_spatial', 'layout_chw', 'rotate_rounding')] + \
         [(n, ctypes.c_double) for n in ('distance_to_receptacle_map_scale', 'shortest_path_map_scale',
                                          'intention_map_scale', 'intention_channel_nonspatial_scale')]
 

@@ -15,7 +15,12 @@ from . import _lib
 from . import constants as K
 
 
-def make_config(flags, room_width, room_length, layout='hwc'):
+def make_config(flags, room_width, room_length, layout='hwc', rotate_rounding='fma'):
+    """simaps_config of one configuration.  rotate_rounding: 'fma' / 'plain', how the host the
+    reference runs on rounds scipy.ndimage.rotate's out_center (include/simaps.h SIMAPS_ROT_*;
+    K.host_rotate_rounding() measures it)."""
+    if rotate_rounding not in _lib.ROT_IDS:
+        raise ValueError('rotate_rounding must be one of %s' % sorted(_lib.ROT_IDS))
     H, W = K.padded_room_shape(room_width, room_length)
     i0, j0, h, w = K.room_rect(room_width, room_length)
     c = _lib.Config()
@@ -31,6 +36,7 @@ def make_config(flags, room_width, room_length, layout='hwc'):
     c.use_intention_channels = int(bool(flags['use_intention_channels']))
     c.intention_channel_spatial = int(flags['intention_channel_encoding'] == 'spatial')
     c.layout_chw = 1 if layout == 'chw' else 0
+    c.rotate_rounding = _lib.ROT_IDS[rotate_rounding]
     c.distance_to_receptacle_map_scale = float(flags['distance_to_receptacle_map_scale'])
     c.shortest_path_map_scale = float(flags['shortest_path_map_scale'])
     c.intention_map_scale = float(flags['intention_map_scale'])
@@ -58,12 +64,19 @@ def pack_descriptors(scenes, agents):
     envs['has_receptacle'] = [rec is not None for rec in recs]
     envs['receptacle_x'] = [rec[0] if rec is not None else 0.0 for rec in recs]
     envs['receptacle_y'] = [rec[1] if rec is not None else 0.0 for rec in recs]
+    # A robot that has not acted yet (Robot.__init__ / reset, envs.py:828-832, 958-963; controller
+    # 1373-1376) has target_end_effector_position / waypoint_positions / waypoint_index = None and is
+    # idle; the reference never reads them for an idle robot (envs.py:2305, 2363, 2371), so it packs
+    # with no target and empty paths (the kernel skips idle robots the same way).
+    for r in rl:
+        if not r['idle'] and (r['target_ee'] is None or r['waypoint_positions'] is None or r['waypoint_index'] is None):
+            raise ValueError('a robot that is not idle needs target_ee, waypoint_positions and waypoint_index')
     if n_rob:
         robots['x'] = [r['position'][0] for r in rl]
         robots['y'] = [r['position'][1] for r in rl]
         robots['heading'] = [r['heading'] for r in rl]
-        robots['target_x'] = [r['target_ee'][0] for r in rl]
-        robots['target_y'] = [r['target_ee'][1] for r in rl]
+        robots['target_x'] = [r['target_ee'][0] if r['target_ee'] is not None else 0.0 for r in rl]
+        robots['target_y'] = [r['target_ee'][1] if r['target_ee'] is not None else 0.0 for r in rl]
         robots['type'] = [_lib.TYPE_IDS[r['type']] for r in rl]
         robots['group_index'] = [r['group_index'] for r in rl]
         robots['lifting'] = [r.get('lift_state') == 'lifting' for r in rl]
@@ -74,6 +87,9 @@ def pack_descriptors(scenes, agents):
     flat, lens = [], []
     for r in rl:
         pos, wps, idx, tgt = r['position'], r['waypoint_positions'], r['waypoint_index'], r['target_ee']
+        if tgt is None or wps is None or idx is None:  # idle, never acted: no paths
+            lens += (0, 0)
+            continue
         mid = wps[idx:-1]
         flat += (pos[0], pos[1])
         for q in mid:
@@ -143,8 +159,8 @@ class StateBatch:
         s0 = scenes[0]
         for s in scenes:
             if (s['H'], s['W'], s['room_width'], s['room_length']) != (s0['H'], s0['W'], s0['room_width'], s0['room_length']) \
-                    or s['flags'] != s0['flags']:
-                raise ValueError('one StateBatch holds one configuration (grid + flags)')
+                    or s['flags'] != s0['flags'] or s.get('rotate_rounding', 'fma') != s0.get('rotate_rounding', 'fma'):
+                raise ValueError('one StateBatch holds one configuration (grid + flags + rotate rounding)')
         if agents is None:
             agents = [(e, a) for e, s in enumerate(scenes) for a in range(len(s['robots']))]
         self.scenes, self.agents, self.device = scenes, list(agents), resolve_device(device)
@@ -152,7 +168,8 @@ class StateBatch:
             raise ValueError('StateBatch renders on a GPU device (got %s); there is no CPU path' % self.device)
         self.flags = s0['flags']
         self.H, self.W = s0['H'], s0['W']
-        self.cfg = make_config(self.flags, s0['room_width'], s0['room_length'], layout)
+        self.cfg = make_config(self.flags, s0['room_width'], s0['room_length'], layout,
+                               s0.get('rotate_rounding', 'fma'))
         self.num_robots = len(s0['robots'])
         if self.flags['use_intention_channels'] and any(len(s['robots']) != self.num_robots for s in scenes):
             raise ValueError('intention channels need the same robot count in every env of a batch')

@@ -108,3 +108,36 @@ def room_dims(env_name):
     if env_name.startswith('large'):
         return 1.0, 1.0, 20
     return 1.0, 0.5, 10
+
+
+# scipy.ndimage.rotate (envs.py:2206, 2267) computes out_center = rot_matrix @ ((S - 1) / 2) with
+# numpy matmul -> BLAS dgemv (scipy/ndimage/interpolation.py:928 in scipy 1.7.1).  Whether that
+# dgemv fuses M[r][0] * a0 into the second product's sum (an FMA kernel) is a property of the
+# numpy / OpenBLAS build and the host CPU, and it decides the sample grid of ~4 % of headings.
+ROTATE_ROUNDINGS = ('fma', 'plain')
+
+
+def host_rotate_rounding():
+    """'fma' or 'plain': how THIS process's numpy rounds rot_matrix @ v, i.e. what
+    scipy.ndimage.rotate does on this host.  Measured on rotation matrices / half-integer
+    vectors of the same shape as rotate's, with exact rational arithmetic for the two candidate
+    forms; raises if the host follows neither."""
+    from fractions import Fraction
+    import numpy as np
+    rs = np.random.RandomState(2206)
+    votes = {'fma': 0, 'plain': 0}
+    n = 0
+    for t in rs.uniform(-math.pi, math.pi, 256):
+        c, s = math.cos(t), math.sin(t)
+        a = np.array([float(rs.randint(60, 200)) / 2, float(rs.randint(60, 200)) / 2])
+        got = np.array([[c, s], [-s, c]]) @ a
+        for r, (m0, m1) in enumerate(((c, s), (-s, c))):
+            n += 1
+            votes['fma'] += float(got[r]) == float(Fraction(m0) * Fraction(a[0]) + Fraction(m1 * a[1]))
+            votes['plain'] += float(got[r]) == m0 * a[0] + m1 * a[1]
+    for k in ROTATE_ROUNDINGS:
+        if votes[k] == n:
+            return k
+    raise RuntimeError('numpy matmul rounds rot_matrix @ v in neither the fused nor the plain form '
+                       '(%d / %d / %d): the drop-in cannot reproduce this host\'s scipy.ndimage.rotate' % (
+                           votes['fma'], votes['plain'], n))

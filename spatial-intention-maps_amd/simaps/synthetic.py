@@ -316,6 +316,22 @@ def make_scene(config_name, env_idx, seed_base=1234, observe_all=False):
     }
 
 
+def never_acted(scene, robots=None):
+    """A copy of `scene` whose robots `robots` (all if None) have not acted yet: the state
+    Robot.__init__ / Robot.reset leave until the robot's first store_new_action (envs.py:828-832,
+    958-963; RobotController.__init__ 1373-1376) -- controller idle, waypoint_positions,
+    target_end_effector_position and waypoint_index None, LiftingRobot.lift_state 'ready'
+    (envs.py:1175).  All robots: what VectorEnv.reset() renders (envs.py:214-222)."""
+    out = dict(scene)
+    out['robots'] = [dict(r) for r in scene['robots']]
+    for k, r in enumerate(out['robots']):
+        if robots is None or k in robots:
+            r.update(idle=True, waypoint_positions=None, waypoint_index=None, target_ee=None)
+            if r['type'] == 'lifting_robot':
+                r['lift_state'] = 'ready'
+    return out
+
+
 def intention_path(robot):
     """RobotController.get_intention_path (envs.py:1475-1476)."""
     idx = robot['waypoint_index']

@@ -23,8 +23,11 @@ def scene_cases():
         e = 0
         while 'e%d_scene' % e in z.files:
             scene = json.loads(str(z['e%d_scene' % e]))
-            scene['robots'] = [dict(r, position=tuple(r['position']), target_ee=tuple(r['target_ee']),
-                                    waypoint_positions=[tuple(p) for p in r['waypoint_positions']])
+            # (robots that have not acted yet carry None paths / target: the reset goldens)
+            scene['robots'] = [dict(r, position=tuple(r['position']),
+                                    target_ee=None if r['target_ee'] is None else tuple(r['target_ee']),
+                                    waypoint_positions=None if r['waypoint_positions'] is None else
+                                    [tuple(p) for p in r['waypoint_positions']])
                                for r in scene['robots']]
             if scene['receptacle_position'] is not None:
                 scene['receptacle_position'] = tuple(scene['receptacle_position'])

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(_lib.lib, name), name
         assert isinstance(getattr(_lib.lib, name), ctypes._CFuncPtr)
     assert set(_lib.EXPORTED) == set(declared_symbols())
-    assert _lib.lib.simaps_abi_version() == 4
+    assert _lib.lib.simaps_abi_version() == 5
 
 
 def test_struct_layouts_match_header():

@@ -4,6 +4,11 @@ from types import SimpleNamespace
 
 import numpy as np
 
+import json
+
+import pytest
+
+import goldens as G
 from simaps import batch, reference_adapter, synthetic
 
 
@@ -11,7 +16,7 @@ class _Robot:
     def __init__(self, r, occ, ovh):
         self.group_index = r['group_index']
         self._pos, self._h = r['position'], r['heading']
-        self.waypoint_positions = list(r['waypoint_positions'])
+        self.waypoint_positions = None if r['waypoint_positions'] is None else list(r['waypoint_positions'])
         self.target_end_effector_position = r['target_ee']
         self.controller = SimpleNamespace(waypoint_index=r['waypoint_index'], state='idle' if r['idle'] else 'moving')
         self.mapper = SimpleNamespace(global_overhead_map_without_robots=ovh,
@@ -95,3 +100,61 @@ def test_pack_descriptors_bytes_match_per_robot_packing():
         agents = [(e, a) for e, s in enumerate(scenes) for a in range(len(s['robots']))][::-1][:-2]
         for got, want in zip(batch.pack_descriptors(scenes, agents), _pack_per_robot(scenes, agents)):
             assert got.dtype == want.dtype and got.tobytes() == want.tobytes(), cfg
+
+
+def test_scene_from_env_reset_and_not_yet_acted_robots():
+    """VectorEnv.reset() state (envs.py:214-222): every robot idle with waypoint_positions /
+    target_end_effector_position / controller.waypoint_index None (envs.py:828-832, 958-963,
+    1373-1376) -- and the mixed state after it.  The adapter passes None through and the packer
+    gives those robots no paths."""
+    base = synthetic.make_scene('lifting_4-small_divider', 5)
+    for sc in (synthetic.never_acted(base), synthetic.never_acted(base, robots=[1, 2, 3])):
+        got = reference_adapter.scene_from_env(_fake_env(sc))
+        assert [r['target_ee'] for r in got['robots']] == [r['target_ee'] for r in sc['robots']]
+        agents = [(0, a) for a in range(4)]
+        x, y = batch.pack_descriptors([sc], agents), batch.pack_descriptors([got], agents)
+        assert all(p.tobytes() == q.tobytes() for p, q in zip(x, y))
+        rob = x[0]
+        never = np.array([r['waypoint_positions'] is None for r in sc['robots']])
+        assert (rob['idle'][never] == 1).all()
+        assert (rob['intention_len'][never] == 0).all() and (rob['history_len'][never] == 0).all()
+        assert (rob['target_x'][never] == 0).all()
+
+
+def test_pack_rejects_moving_robot_without_path():
+    sc = synthetic.never_acted(synthetic.make_scene('lifting_4-small_divider', 5), robots=[2])
+    sc['robots'][2]['idle'] = False
+    with pytest.raises(ValueError):
+        batch.pack_descriptors([sc], [(0, 0)])
+
+
+RESET_FILES = [f for f in G.scene_files() if '/scene_reset_' in f or '/scene_rot-' in f]
+
+
+@pytest.mark.parametrize('path', RESET_FILES, ids=[f.rsplit('/', 1)[1] for f in RESET_FILES])
+def test_adapter_on_reference_objects_matches_fixture(path):
+    """make_goldens.py ran reference_adapter.scene_from_env on the reference's OWN LiftingRobot /
+    RobotController objects (reset and never-acted robots included) and recorded what it returned:
+    that descriptor packs byte-identically to the fixture's scene, and in the reset env every robot
+    packs as idle with no paths."""
+    z = G.load(path.rsplit('/', 1)[1])
+    e = 0
+    while 'e%d_scene' % e in z.files:
+        want = json.loads(str(z['e%d_scene' % e]))
+        got = json.loads(str(z['e%d_adapter' % e]))
+        assert got['rotate_rounding'] == want['rotate_rounding']
+        for gr, wr in zip(got['robots'], want['robots']):
+            for k in ('type', 'group_index', 'idle', 'waypoint_index', 'heading'):
+                assert gr[k] == wr[k], k
+            if wr['type'] == 'lifting_robot':  # (only LiftingRobot has a lift_state, envs.py:1175)
+                assert gr['lift_state'] == wr['lift_state']
+            assert gr['position'][:2] == wr['position'][:2]
+            assert (gr['target_ee'] is None) == (wr['target_ee'] is None)
+            assert (gr['waypoint_positions'] is None) == (wr['waypoint_positions'] is None)
+        agents = [(0, a) for a in range(len(want['robots']))]
+        for p, q in zip(batch.pack_descriptors([want], agents), batch.pack_descriptors([got], agents)):
+            assert p.tobytes() == q.tobytes()
+        if '/scene_reset_' in path and e == 0:
+            rob = batch.pack_descriptors([got], agents)[0]
+            assert (rob['idle'] == 1).all() and (rob['intention_len'] == 0).all()
+        e += 1

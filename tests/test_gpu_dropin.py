@@ -434,3 +434,76 @@ def test_policy_input_from_device_stacks(V):
         x = state[e][0][0] if state[e][0][0] is not None else state[e][0][1]
         t = policy_input.apply_transform(x)
         assert t.data_ptr() == x.data_ptr() and t.is_contiguous()
+
+
+RESET_FILES = [f.rsplit('/', 1)[1] for f in G.scene_files() if '/scene_reset_' in f]
+
+
+def _golden_env(z, e, key):
+    """Scene of golden env e as the drop-in receives it: `key` = 'scene' (the fixture's own
+    descriptor) or 'adapter' (reference_adapter.scene_from_env run on the reference's objects),
+    plus every rendered agent's maps."""
+    import json
+    sc = json.loads(str(z['e%d_%s' % (e, key)]))
+    for r in sc['robots']:
+        r['position'] = tuple(r['position'])
+    if sc['receptacle_position'] is not None:
+        sc['receptacle_position'] = tuple(sc['receptacle_position'])
+    A = len(sc['robots'])
+    sc['occupancy'] = np.stack([z['e%d_a%d_occupancy' % (e, a)] for a in range(A)])
+    sc['overhead'] = np.stack([z['e%d_a%d_overhead' % (e, a)] for a in range(A)])
+    return sc
+
+
+@pytest.mark.parametrize('name', RESET_FILES)
+def test_dropin_reset_and_not_yet_acted_robots(V, name):
+    """VectorEnvObservations.get_state on the reference's reset state (env 0: every robot idle,
+    None paths / target, envs.py:214-222) and on the steps after it (env 1: robot 0 moving, the
+    others never acted), fed the descriptor the adapter read from the reference's own objects:
+    every stack bitwise equal to the reference's Mapper.get_state (tests/golden/make_goldens.py
+    gen_reset).  The reset step renders the awaiting robot only (envs.py:222, 747-752)."""
+    synthetic, vector_env = V
+    z = G.load(name)
+    scenes = [_golden_env(z, e, 'adapter') for e in range(2)]
+    flags = scenes[0]['flags']
+    nr = len(scenes[0]['robots'])
+    obs = vector_env.VectorEnvObservations(scenes, layout='hwc')
+    full = obs.get_state(all_robots=True, numpy=True)
+    for e in range(2):
+        for g, idx in zip(full[e], vector_env.robot_groups(scenes[e])):
+            for x, a in zip(g, idx):
+                ref = z['e%d_a%d_state' % (e, a)]
+                if flags['use_intention_channels'] and flags['intention_channel_encoding'] == 'nonspatial':
+                    assert np.abs(x - ref).max() <= 1e-7
+                else:
+                    assert _bitwise(x, ref), (e, a, float(np.abs(x - ref).max()))
+    awaiting = [[a == 0 for a in range(nr)], [False] * nr]
+    st = obs.get_state(awaiting=awaiting, numpy=True)
+    first = vector_env.robot_groups(scenes[0])[0][0]
+    assert st[0][0][0] is not None and first == 0
+    assert all(x is None for g in st[1] for x in g)
+    assert np.array_equal(st[0][0][0], full[0][0][0])
+
+
+@pytest.mark.parametrize('cfg', ['lifting_4-small_divider', 'pushing_4-large_empty'])
+def test_rotate_rounding_modes(V, cfg):
+    """scene_rot-plain_*: every robot at a heading where the two BLAS roundings of rotate's
+    out_center disagree, rendered by the reference on a plain-dgemv host.  The kernel in 'plain'
+    mode is bitwise equal to the reference; in 'fma' mode it differs from it and equals the
+    oracle's FMA restatement (so the switch is what makes the difference)."""
+    from simaps import batch
+    z = G.load('scene_rot-plain_%s.npz' % cfg)
+    scenes = [_golden_env(z, e, 'scene') for e in range(2)]
+    assert scenes[0]['rotate_rounding'] == 'plain'
+    b = batch.StateBatch(scenes, layout='hwc')
+    st = b.render().cpu().numpy()
+    for n, (e, a) in enumerate(b.agents):
+        assert _bitwise(st[n], z['e%d_a%d_state' % (e, a)]), (e, a)
+    fma = [dict(s, rotate_rounding='fma') for s in scenes]
+    bf = batch.StateBatch(fma, layout='hwc')
+    sf = bf.render().cpu().numpy()
+    differ = 0
+    for n, (e, a) in enumerate(bf.agents):
+        differ += not _bitwise(sf[n], z['e%d_a%d_state' % (e, a)])
+        assert _bitwise(sf[n], O.agent_state(fma[e], a)), (e, a)
+    assert differ >= len(bf.agents) // 2, differ
