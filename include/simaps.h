@@ -220,7 +220,7 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
  *   scratch (any contents).  The frames' map slots must be distinct.  All DEVICE.  Points with
  *   equal z on one pixel: the later camera pixel wins (the reference's np.argsort leaves that
  *   order unspecified).
- *   SIMAPS_EUNSUPPORTED: camera width outside [69, 1024], Hc * Wc >= 2^28, N > 65535
+ *   SIMAPS_EUNSUPPORTED: camera width outside [67, 1024], Hc * Wc >= 2^28, N > 65535
  *   (two launches on `stream`: a point pass over chunks of 2048 camera pixels with per-chunk LDS
  *   max-reduction that also records each chunk's box of touched map pixels, then one sweep of each
  *   frame's box). */

@@ -32,9 +32,11 @@
 // gathered through L2 (<= 136^2 f32 footprint), the state write (96*96*C f32).  No intermediate
 // map ever leaves the CU.
 //
-// Diagnostic-only build macros (tools/phase_profile.py with `make variant`, never the product):
-// SIMAPS_PHASE_STAMPS (per-phase s_memrealtime stamps), SIMAPS_ABL_NOSWEEP / _NORENDER (one group
-// of the split alone), SIMAPS_ABL_NOGATHER / _NOGPIX (overhead gathers / fp64 sample indices off).
+// Diagnostic-only build macros (never the product): SIMAPS_PHASE_STAMPS / SIMAPS_LIGHT_STAMPS
+// (per-phase s_memrealtime stamps, tools/phase_profile.py, `make prof`), SIMAPS_DIAG_FLAG_TIMEOUT
+// (the fault-path test build, `make diag`).  The round-1/2 ablation variants (sweeps or render
+// alone, no gathers / raster / stores, issue-priority variants) were measured and removed; their
+// results are in DESIGN.md.
 //
 // Compiled with -ffp-contract=off: every fp32/fp64 operation rounds exactly like the reference
 // (see geom.h for the one explicit fma).
@@ -79,6 +81,11 @@ __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
         if (STAMP_ON(k) && (threadIdx.x & 63) == 0 && blockIdx.x < MAX_STAMP_WG)                 \
             g_stamps[blockIdx.x * NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime();              \
     } while (0)
+#define STAMP_VAL(k, v) /* a counter instead of a time (e.g. the SPFA's pops) */             \
+    do {                                                                                         \
+        if (STAMP_ON(k) && blockIdx.x < MAX_STAMP_WG)                                            \
+            g_stamps[blockIdx.x * NSTAMP + (k)] = (unsigned long long)(v);                       \
+    } while (0)
 #define STAMP_CLK(k) /* shader-clock counter (s_memtime): with a realtime stamp, the clock rate */  \
     do {                                                                                         \
         if (STAMP_ON(k) && (threadIdx.x & 63) == 0 && blockIdx.x < MAX_STAMP_WG)                 \
@@ -90,6 +97,9 @@ __device__ unsigned long long g_stamps[MAX_STAMP_WG * NSTAMP];
     } while (0)
 #define STAMP_NB(k) \
     do {            \
+    } while (0)
+#define STAMP_VAL(k, v) \
+    do {                \
     } while (0)
 #define STAMP_CLK(k) \
     do {             \
@@ -667,7 +677,8 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> *L
 // ------------------------------------------------------------------------------------------------
 // Phase: snap the query pixels to the closest free cell (scipy EDT feature transform at q)
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void snap_sources(Shared &sh, SsspScratch &S, int nsrc, const Group &g)
+template <class SH>  // Shared (get_state / sp_distance) or PathHdr (path kernels)
+__device__ __forceinline__ void snap_sources(SH &sh, SsspScratch &S, int nsrc, const Group &g)
 {
     const int tid = g.t;
     const int h = sh.h, w = sh.w, i0 = sh.i0, j0 = sh.j0;
@@ -701,10 +712,13 @@ __device__ __forceinline__ void snap_sources(Shared &sh, SsspScratch &S, int nsr
         const int qj = __builtin_amdgcn_readfirstlane(sh.src_q[s][1]);
         const int qr = qi - i0, qc = qj - j0;
         int rowd[2] = {-1, -1}, row[2] = {0, 0};  // per column: the nearest free row's distance / row
-        int best = 0x7fffffff;                    // (d^2 + dc^2) << 7 | column: the lexicographic minimum
-        for (int d = 0; d <= h + 128; d++) {       // (|qr| is bounded by the grid; d > h + |qr| finds nothing)
+        // (d^2 + dc^2) << 7 | column: the lexicographic minimum, 64-bit (the query is clamped to the
+        // grid only, so d and dc reach the grid size)
+        long long best = 0x7fffffffffffffffll;
+        const int dmax = max(abs(qr), abs(qr - (h - 1)));  // the farthest rect row from the query row
+        for (int d = 0; d <= dmax; d++) {
             const long long dd = (long long)d * d;
-            if (dd << 7 > (long long)best) break;  // no column still searching can reach the best key
+            if (dd << 7 > best) break;  // no column still searching can reach the best key
             const int ra = qr - d, rb = qr + d;
             const bool va = ra >= 0 && ra < h, vb = d > 0 && rb >= 0 && rb < h;
             if (!va && !vb && ra < 0 && rb >= h) break;  // every row visited
@@ -716,15 +730,15 @@ __device__ __forceinline__ void snap_sources(Shared &sh, SsspScratch &S, int nsr
                     if (b_test(fa, c)) { rowd[k] = d; row[k] = ra; }
                     else if (b_test(fb, c)) { rowd[k] = d; row[k] = rb; }
                     if (rowd[k] >= 0) {
-                        const int key = ((d * d + (c - qc) * (c - qc)) << 7) | c;
+                        const long long key = (((long long)d * d + (long long)(c - qc) * (c - qc)) << 7) | c;
                         best = min(best, key);
                     }
                 }
             }
             for (int off = 32; off > 0; off >>= 1) best = min(best, __shfl_xor(best, off));
         }
-        if (best != 0x7fffffff) {  // (no free cell at all: src_ok stays 0)
-            const int c = best & 127;
+        if (best != 0x7fffffffffffffffll) {  // (no free cell at all: src_ok stays 0)
+            const int c = (int)(best & 127);
             const int owner = c & 63, k = c >> 6;
             const int r = __shfl(k ? row[1] : row[0], owner);
             if (lane == 0) {
@@ -849,11 +863,7 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw_rt)
         R0 = G[goff((J) + P)];                                                                          \
         if (CPL == 2) R1 = G[goff((J) + P) + sa];                                                       \
     } while (0)
-#ifdef SIMAPS_DIAG_PLAINSTORE  // diagnostic (wrong results): plain stores instead of LDS atomic min
-#define SWEEP_WRITE(P_, V_, R_) (*(P_) = fminf((V_), (R_)))
-#else
 #define SWEEP_WRITE(P_, V_, R_) lds_min((P_), (V_))
-#endif
     int t = 0;
     for (; t + P <= len; t += P) {
         G = gbase(t);
@@ -886,24 +896,9 @@ __device__ bool sweep_t(lds_float *__restrict__ D, int len, int span, int pw_rt)
 // Every LDS operation, wait and register of the loop lives inside the asm, which drains
 // (lgkmcnt(0)) before handing its registers back.  A DPP read of p0 / p1 follows their VALU write
 // by >= 3 VALU instructions.
-// Diagnostic variants (wrong results; per-step cost attribution with the stamp build):
-// SIMAPS_DIAG_SWA_NOMIN (no atomics), SIMAPS_DIAG_SWA_NOREAD (no prefetch reads after the prologue)
-#ifdef SIMAPS_DIAG_SWA_NOMIN
-#define SWA_DSMIN(x) ""
-#else
 #define SWA_DSMIN(x) x
-#endif
-#ifdef SIMAPS_DIAG_SWA_NOREAD
-#define SWA_DSREAD(x) ""
-#define SWA_WAIT(W) ""
-#else
 #define SWA_DSREAD(x) x
-#ifdef SIMAPS_DIAG_SWA_NOMIN
-#define SWA_WAIT(W) "s_waitcnt lgkmcnt(0)\n\t"
-#else
 #define SWA_WAIT(W) "s_waitcnt lgkmcnt(" #W ")\n\t"
-#endif
-#endif
 #define SWA_OFF(J) "((%[k0]+(" #J ")*%[kd])*%[sl4])"
 #define SWA_ROR "wave_ror:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
 #define SWA_ROL "wave_rol:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
@@ -1131,9 +1126,6 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
     const int bhi = mhi ? 127 - __builtin_clzll(mhi) : 63 - __builtin_clzll(mlo);
     const int t0 = fwd ? blo : len - 1 - bhi, tmax = fwd ? bhi : len - 1 - blo;  // step t: line fwd ? t + 1 : len - t
     if (pw == 95
-#ifdef SIMAPS_SWEEP_C
-        && false
-#endif
     ) {  // every BASELINE room is 92 columns wide (pitch 95): the asm loop with immediate offsets
         SweepOut o;
         switch (dir) {
@@ -1226,14 +1218,11 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
     const int s = wave >> 2;
     const Group gs{tid & 255, 256, sh.bar[2 + s], 4};
     int *changed = sh.changed[s];
-#ifndef SIMAPS_SHORT_PRIO
-#define SIMAPS_SHORT_PRIO 2
-#endif
     {   // issue priority over the render waves (which have slack), the longer sweeps first (VALU
         // arbitration is priority, then age)
         const int dir = (wave + 2 * s) & 3;
         if ((dir >= 2) == (w >= h)) __builtin_amdgcn_s_setprio(3);
-        else __builtin_amdgcn_s_setprio(SIMAPS_SHORT_PRIO);
+        else __builtin_amdgcn_s_setprio(2);
     }
     int steps = 0;  // lines this wave processed (diagnostics)
     for (int round = 0;; round++) {
@@ -1245,9 +1234,6 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
 #endif
         // waves go to SIMD (wave % 4): source 1's directions are rotated by 2 so that every SIMD
         // hosts one row sweep and one column sweep (the long ones would otherwise share two SIMDs)
-#ifdef SIMAPS_DIAG_ONESRC  // diagnostic (wrong results): only source 0 sweeps
-        if (s == 1) {} else
-#endif
         if (sh.src_ok[s] && sweep(dist + s * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3, sh.dirty[s], steps) && (tid & 63) == 0)
             changed[round % 3] = 1;
 #ifdef SIMAPS_PHASE_STAMPS
@@ -1709,13 +1695,9 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
     for (int k = 0; k < MAXPG; k++) {
         uint32_t v = gq_v(k);
         asm volatile("" : "+v"(v));  // nothing computed here is shared with (kept alive for) later passes
-#ifdef SIMAPS_ABL_NOGATHER
-        ovv[k] = v != 0xffffu ? 0.125f : 0.0f;
-#else
         // branch-free, 32-bit offsets (SGPR base): pixels outside the crop load cell 0, ignored later
         const int idx = (ci0 + (int)(v >> 8)) * W + (cj0 + (int)(v & 0xffu));
         ovv[k] = *reinterpret_cast<const float *>(reinterpret_cast<const char *>(ovh) + (unsigned)(v != 0xffffu ? idx : 0) * 4u);
-#endif
     }
     if (g.t == 0) STAMP_NB(42);
     // overhead / robot channels (Mapper._create_global_overhead_map / _create_global_robot_map,
@@ -1727,11 +1709,7 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
 #pragma unroll
     for (int k = 0; k < MAXPG; k++) {
         const uint32_t v = gq_v(k);
-#ifdef SIMAPS_ABL_NOROBOT  // diagnostic: no robot stamps in the overhead / robot channels
-        const unsigned m = 0;
-#else
         const unsigned m = cmap[v != 0xffffu ? (int)(v >> 8) * CROP + (int)(v & 0xffu) : CROP * CROP];
-#endif
         codes[k >> 2] |= m << (8 * (k & 3));
     }
     if (g.t == 0) STAMP_NB(14);
@@ -1745,12 +1723,8 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         const float vseg = ms ? (float)(31 - __builtin_clz(ms) + 5) * 0.125f : 0.0f;
         const float vrob = (mr & 2u) ? 1.0f : ((mr & 1u) ? 0.5f : 0.0f);
         const float vov = vseg > 0.0f ? vseg : (v != 0xffffu ? ovv[k] : 0.0f);
-#ifdef SIMAPS_ABL_NOSTORE01
-        asm volatile("" ::"v"(vov), "v"(vrob));
-#else
         rc.put(0, p, vov);
         if (cfg.use_robot_map) rc.put(1, p, vrob);
-#endif
     }
     if (g.t == 0) STAMP_NB(11);
     // sample one rasterised pass into channel c (then the tile may be reused)
@@ -1773,17 +1747,13 @@ __device__ __forceinline__ void render_maps(const RenderCtx &rc, const Group &g,
         if (!early_tile) g.sync();
         wait_scratch(sh);
         if (g.t == 0) STAMP_NB(62);
-#ifndef SIMAPS_ABL_NORASTER
         raster_lines(sh, tile, cfg, rb, paths, encs[0], true, g, early_tile);
-#endif
         if (g.t == 0) STAMP_NB(13);
         sample_pass(ch, npass == 1);
     }
     // the second history / intention pass (history + intention configs)
     if (npass > 1) {
-#ifndef SIMAPS_ABL_NORASTER
         raster_lines(sh, tile, cfg, rb, paths, encs[1], false, g);
-#endif
         sample_pass(ch + 1, true);
     }
     ch += npass;
@@ -2048,9 +2018,7 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
         STAMP_NB(3);
     }
     if (nsrc == 0) return;
-#ifndef SIMAPS_ABL_NOSWEEP  // diagnostic: render alone (distance channels wrong)
     sssp_rounds(sh, dist, nsrc, g);
-#endif
     if (nsrc == 2 && G == 512 && !dbg.dist) {
         // each source's four waves take its maximum as soon as its own rounds end (the arrays are
         // independent), overlapping the other source's remaining rounds
@@ -2091,11 +2059,6 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const int tid = threadIdx.x;
     const int H = cfg.H, W = cfg.W;
     if (tid == 0) STAMP_NB(77);  // kernel entry (dispatch skew)
-#ifdef SIMAPS_REPEAT  // diagnostic: run the body SIMAPS_REPEAT times (stamps keep the last, warm-cache pass)
-#pragma clang loop unroll(disable)
-    for (int rep = 0; rep < SIMAPS_REPEAT + (int)(n >> 30); rep++) {
-    lds_barrier();
-#endif
     simaps_agent ag = agents[n];
     // Sources of the shortest-path maps (envs.py:2071-2113 order): receptacle, then the robot.
     const int nsrc = (cfg.use_shortest_path_to_receptacle_map ? 1 : 0) + (cfg.use_shortest_path_map ? 1 : 0);
@@ -2128,9 +2091,6 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     const RenderCtx rc{cfg, sh, out, C, n};
     if ((tid >> 6) < cs_waves) {
         const Group g{tid, 64 * cs_waves, sh.bar[0], cs_waves};
-#ifdef SIMAPS_TRACK_PRIO  // diagnostic: the sweep track issues ahead of the render track
-        __builtin_amdgcn_s_setprio(SIMAPS_TRACK_PRIO);
-#endif
         if (cs_waves == 8) sweep_track<512>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g, early_tile);
         else sweep_track<256>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g, early_tile);
         STAMP_NB(7);
@@ -2139,9 +2099,6 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         const Group g{tid - 64 * cs_waves, 64 * nw, cs_waves ? sh.bar[1] : nullptr, nw};
         const int t = g.t;
         const simaps_robot *rb = robots + ev.robot_off;
-#if SIMAPS_RENDER_PRIO
-        __builtin_amdgcn_s_setprio(SIMAPS_RENDER_PRIO);
-#endif
         // ---- parameters (one lane per robot; the agent's own local rotation on another wave)
         if (t == 0) {
             sh.nr = ev.num_robots;
@@ -2223,9 +2180,6 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
         }
         if (t == 0) STAMP_NB(75);
         g.sync();
-#if SIMAPS_RENDER_PRIO && SIMAPS_RENDER_PRIO_END == 1
-        __builtin_amdgcn_s_setprio(0);
-#endif
         if (t == 0) STAMP_NB(9);
         if (segs) seg_ramp(sh, t - 320);  // (the segment table is read at raster time, many barriers later)
         if (cfg.use_intention_channels && t == 256) intention_channel_order(sh, cfg, rb);
@@ -2278,16 +2232,11 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             }
         }
         g.sync();
-#if SIMAPS_RENDER_PRIO && SIMAPS_RENDER_PRIO_END == 2
-        __builtin_amdgcn_s_setprio(0);
-#endif
         if (t == 0) STAMP_NB(1);
-#ifndef SIMAPS_ABL_NORENDER  // diagnostic: sweeps alone (output channels 0.. left unwritten)
         const float *ovh = overhead + (size_t)ag.map_slot * H * W;
         if (nw == 8) render_maps<18>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile, tail_cells, dist);
         else if (nw == 12) render_maps<12>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile, tail_cells, dist);
         else render_maps<9>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile, tail_cells, dist);
-#endif
         if (t == 0) STAMP_NB(8);
     }
     lds_barrier();
@@ -2310,12 +2259,6 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             else { o[0] = o[1] = o[2] = o[3] = -1; }
         }
     }
-#ifdef SIMAPS_DIAG_V2  // diagnostic: a global store that never executes
-    if (tid == 0 && C < 0) state[0] = 1.0f;
-#endif
-#ifdef SIMAPS_DIAG_V3  // diagnostic: a realtime read consumed by an empty asm
-    if (tid == 0) { const unsigned long long tt = __builtin_amdgcn_s_memrealtime(); asm volatile("" ::"s"(tt)); }
-#endif
     if (tid == 0) {
         const unsigned f = group_faults(sh.bar, sh.rounds, nsrc);
         post_faults(fault, f);
@@ -2328,9 +2271,6 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
     }
 #ifdef SIMAPS_PHASE_STAMPS
     if (tid == 0 && blockIdx.x < MAX_STAMP_WG) g_stamps[blockIdx.x * NSTAMP + 10] = (unsigned long long)sh.rounds;
-#endif
-#ifdef SIMAPS_REPEAT
-    }
 #endif
 }
 
@@ -2376,6 +2316,21 @@ __global__ void __launch_bounds__(NT) sssp_grid_kernel(int H, int W, const uint8
     }
 }
 
+// The robot class of agent ag with get_state_kernel's descriptor clamps (num_robots in [1,
+// SIMAPS_MAX_ROBOTS], robot index < num_robots, class < 4); `bad` = something was clamped
+// (SIMAPS_FAULT_DESCRIPTOR).
+__device__ __forceinline__ int agent_robot_type(const simaps_agent &ag, const simaps_env *envs, const simaps_robot *robots,
+                                                bool &bad)
+{
+    const simaps_env ev = envs[ag.env];
+    bad = (unsigned)(ev.num_robots - 1) >= (unsigned)SIMAPS_MAX_ROBOTS || (unsigned)ag.robot >= (unsigned)ev.num_robots;
+    const int nr = min(max(ev.num_robots, 1), SIMAPS_MAX_ROBOTS);
+    const int r = (unsigned)ag.robot < (unsigned)nr ? ag.robot : 0;
+    int type = robots[ev.robot_off + r].type;
+    if ((unsigned)type > 3u) { bad = true; type = 0; }
+    return type;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Reward lookups: OccupancyMap.shortest_path_distance (envs.py:2507-2512) from one source position to
 // Q target positions on each agent's own map (Mapper.distance_to_receptacle, envs.py:2190-2194)
@@ -2400,12 +2355,14 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
     cspace_load<NT>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
                     cfg.room_w, tid);
     if (tid == 0) {
-        const simaps_env ev = envs[ag.env];
+        bool bad;
+        const int type = agent_robot_type(ag, envs, robots, bad);
+        sh.flag[1] = bad;
         sh.h = cfg.room_h;
         sh.w = cfg.room_w;
         sh.i0 = cfg.room_i0;
         sh.j0 = cfg.room_j0;
-        sh.r = geo.cspace_r[robots[ev.robot_off + ag.robot].type];
+        sh.r = geo.cspace_r[type];
         pos_to_pix(sources[2 * n], sources[2 * n + 1], H, W, sh.src_q[0][0], sh.src_q[0][1]);
         sh.nsrc = 1;
     }
@@ -2414,7 +2371,7 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
     snap_sources(sh, S, 1, whole_wg());
     const bool src_ok = sh.src_ok[0];
     sssp(sh, S, dist, 1);  // the source's distance image (GridGraph._spfa_with_cache, pyx:116-119)
-    if (tid == 0) post_faults(fault, group_faults(sh.bar, sh.rounds, 1));
+    if (tid == 0) post_faults(fault, group_faults(sh.bar, sh.rounds, 1) | (sh.flag[1] ? SIMAPS_FAULT_DESCRIPTOR : 0u));
     const int pw = sssp_pitch(sh.w);
     // dists[target] (pyx:156-163) as a Python float / LOCAL_MAP_PIXELS_PER_METER; unreachable -> -1
     // (pyx:110-112)
@@ -2485,7 +2442,8 @@ __device__ __forceinline__ void line_pixel(int r0, int c0, int r1, int c1, int t
 }
 
 // cspace (the GridGraph grid): free iff inside the room rect and a free cspace bit
-__device__ __forceinline__ bool cs_free(const Shared &sh, const SsspScratch &S, int i, int j)
+template <class SH>
+__device__ __forceinline__ bool cs_free(const SH &sh, const SsspScratch &S, int i, int j)
 {
     const int r = i - sh.i0, c = j - sh.j0;
     return r >= 0 && r < sh.h && c >= 0 && c < sh.w && b_test(S.freeb[r], c);
@@ -2493,7 +2451,8 @@ __device__ __forceinline__ bool cs_free(const Shared &sh, const SsspScratch &S, 
 
 // cspace_thin = 1 - binary_dilation(min(room_mask, occupancy), disk(3)) (envs.py:2456): free iff no
 // in-room occupied pixel within disk(3); S.win holds the occupancy window (rect + RMAX halo).
-__device__ __forceinline__ bool thin_free(const Shared &sh, const SsspScratch &S, int i, int j)
+template <class SH>
+__device__ __forceinline__ bool thin_free(const SH &sh, const SsspScratch &S, int i, int j)
 {
     constexpr int R = 3;  // disk(ceil(HALF_WIDTH * 96)) (envs.py:2426)
     for (int dy = -R; dy <= R; dy++)
@@ -2508,9 +2467,11 @@ __device__ __forceinline__ bool thin_free(const Shared &sh, const SsspScratch &S
 }
 
 // wave-parallel: is every pixel of line (r0, c0) -> (r1, c1) free (thin ? cspace_thin : cspace)?
-// grid == 1 bits of a raw GridGraph grid (grid_path_kernel; kept in the unused dilation table):
-// the line-of-sight test of pyx:146 counts (1 - grid[rr, cc]) != 0 in uint8, i.e. any cell != 1
-__device__ __forceinline__ bool one_free(const Shared &sh, const SsspScratch &S, int i, int j)
+// grid == 1 bits of a raw GridGraph grid (grid_path_kernel; kept in S.dtab[0], which the SPFA arrays
+// do not overlay): the line-of-sight test of pyx:146 counts (1 - grid[rr, cc]) != 0 in uint8, i.e.
+// any cell != 1
+template <class SH>
+__device__ __forceinline__ bool one_free(const SH &sh, const SsspScratch &S, int i, int j)
 {
     const int r = i - sh.i0, c = j - sh.j0;
     return r >= 0 && r < sh.h && c >= 0 && c < sh.w && b_test(S.dtab[0][r], c);
@@ -2518,8 +2479,8 @@ __device__ __forceinline__ bool one_free(const Shared &sh, const SsspScratch &S,
 
 enum LineMask { LINE_CSPACE = 0, LINE_THIN = 1, LINE_GRID_ONE = 2 };
 
-__device__ __forceinline__ bool line_free(const Shared &sh, const SsspScratch &S, int r0, int c0, int r1, int c1,
-                                          int mask)
+template <class SH>
+__device__ __forceinline__ bool line_free(const SH &sh, const SsspScratch &S, int r0, int c0, int r1, int c1, int mask)
 {
     const int lane = threadIdx.x & 63;
     const int n = max(abs(r1 - r0), abs(c1 - c0)) + 1;
@@ -2533,83 +2494,130 @@ __device__ __forceinline__ bool line_free(const Shared &sh, const SsspScratch &S
     return __ballot(blocked) == 0;
 }
 
-constexpr int PATH_MAX_PTS = 64;
+// ------------------------------------------------------------------------------------------------
+// Path kernels' LDS: one 256-thread workgroup per query, its LDS sized for the room so that several
+// queries share a CU -- the exact SPFA is one wave's serial pop loop (latency-bound), so throughput
+// comes from residency.  Layout (PathLds<CELLS>):
+//   PathHdr                       query header (the Shared fields the snap / path steps read)
+//   SsspScratch                   occupancy window, free bits, dilation table (build_cspace); after
+//                                 the cspace is built only win (straight-line test), freeb and dtab[0]
+//                                 (grid == 1 bits of grid paths) stay live, and
+//   arrays at dtab[1]:            dist   f32 [CELLS]   SPFA distances (free: inf, blocked / border -inf)
+//                                 queue  u16 [CELLS]   ring of cell indices (live entries <= cells)
+//                                 pin    u8  [CELLS]   bits 0-3: 1 + direction of the parent edge (0: none),
+//                                                      bit 4: in queue
+// 7 B per cell: small rooms (46 x 95 cells) take 39 KB -> 4 queries per CU; rooms up to the
+// SIMAPS_MAX_ROOM_CELLS limit 70 KB -> 2 per CU.  (The round-2 kernels used the 158 KB get_state
+// layout, one 1024-thread query per CU.)
+// ------------------------------------------------------------------------------------------------
+#ifndef SIMAPS_POP_CAP  // the diagnostic build (tests/test_gpu_faults.py) lowers it to exercise the fault path
+#define SIMAPS_POP_CAP (1 << 24)
+#endif
+constexpr int PNT = 256;  // path workgroup: 4 waves (build_cspace needs >= 4 for its row blocks)
+constexpr int PATH_SMALL_CELLS = 4608;  // >= (44 + 2) * 95: every small_* room
+struct PathHdr {
+    int h, w, i0, j0, r, nsrc;
+    int src_q[2][2], src_s[2][2], src_ok[2];
+    int flag[2];
+    int nseg;
+    unsigned fault;  // SIMAPS_FAULT_* bits of this query
+};
+constexpr int OFF_PS = align16((int)sizeof(PathHdr));
+constexpr int OFF_PA = OFF_PS + align16((int)(offsetof(SsspScratch, dtab) + sizeof(B128) * MAX_WIN_ROWS));
+template <int CELLS>
+constexpr int path_lds_bytes()
+{
+    return align16(OFF_PA + 7 * CELLS > OFF_PS + (int)sizeof(SsspScratch) ? OFF_PA + 7 * CELLS
+                                                                           : OFF_PS + (int)sizeof(SsspScratch));
+}
+static_assert(path_lds_bytes<PATH_SMALL_CELLS>() * 4 <= 160 * 1024, "4 small-room queries per CU");
+static_assert(path_lds_bytes<SIMAPS_MAX_ROOM_CELLS>() * 2 <= 160 * 1024, "2 queries per CU at the room limit");
+static_assert(MAX_ROWS <= 256 && SIMAPS_MAX_ROOM_W <= 256, "rect cells pack as (row << 8) | col");
+
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+// pyx:30 direction order [0,-1],[0,1],[-1,-1],[-1,0],[-1,1],[1,-1],[1,0],[1,1]: cell offset of edge k
+__device__ __forceinline__ int dir_off(int k, int pw)
+{
+    const int di = k < 2 ? 0 : (k < 5 ? -1 : 1);
+    const int dj = k < 2 ? (k == 0 ? -1 : 1) : ((k - 2) % 3) - 1;
+    return di * pw + dj;
+}
 
 // Steps (3)-(6) of the movement path on the LDS-resident free bits (S.freeb) between the cells
 // sh.src_s[0] (source) and sh.src_s[1] (target), both inside the window: the exact SPFA (run_spfa:
 // the source is a free cell of the window; otherwise only the source is reached), the parent walk,
 // approximate_polygon and the line-of-sight pruning on `line_mask`.  Leaves the kept waypoints in
-// outp[0, cnt) (packed (row << 16) | col, target first, i.e. before pyx:152's reversal) and returns
-// cnt in wave 0.  All threads call it.
-__device__ __forceinline__ int path_core(Shared &sh, SsspScratch &S, char *smem, int H, int W, bool run_spfa, int line_mask)
+// outp[0, cnt) (u16 rect cells (row << 8) | col, target first, i.e. before pyx:152's reversal) and
+// returns cnt in wave 0.  All PNT threads call it.
+template <int CELLS>
+__device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr, int H, int W, bool run_spfa,
+                                         int line_mask, const uint16_t *&outp_ret)
 {
-    static_assert(align16((int)sizeof(SsspScratch)) + DIST_FLOATS * 5 <= UNION_BYTES, "SPFA queue + flags fit the union");
-    // after the parent walk the distance + parent arrays are free: the Douglas-Peucker stack
-    // (<= 2 * points ints), then the sparse points and the kept waypoints
-    float *dist = reinterpret_cast<float *>(smem + OFF_DIST);
-    int *parent = reinterpret_cast<int *>(smem + OFF_DIST) + DIST_FLOATS;
-    int *queue = reinterpret_cast<int *>(smem + OFF_UNION + align16((int)sizeof(SsspScratch)));
-    uint8_t *inq = reinterpret_cast<uint8_t *>(queue + DIST_FLOATS);  // later: chain flags
-    int *dense = queue;  // after the SPFA: the dense path
-    int *stack = reinterpret_cast<int *>(smem + OFF_DIST);
-    int *sparse = stack, *outp = stack + DIST_FLOATS;
+    float *dist = reinterpret_cast<float *>(arr);
+    uint16_t *queue = reinterpret_cast<uint16_t *>(arr + 4 * CELLS);
+    uint8_t *pin = reinterpret_cast<uint8_t *>(arr + 6 * CELLS);
+    // after the parent walk: dense path (u16 rect cells) in the queue region, chain flags in pin,
+    // the Douglas-Peucker stack (u16 pairs) in the dist region; then the sparse points and the kept
+    // waypoints (u16 each) in the dist region
+    uint16_t *dense = queue;
+    uint32_t *stack = reinterpret_cast<uint32_t *>(arr);
+    uint16_t *sparse = reinterpret_cast<uint16_t *>(arr), *outp = sparse + CELLS;
+    uint8_t *chain = pin;
+    outp_ret = outp;
     const int tid = threadIdx.x, lane = tid & 63;
     const int h = sh.h, w = sh.w, pw = sssp_pitch(w), cells = (h + 2) * pw;
     // (3) GridGraph._spfa (pyx:69-114) from the snapped source, exactly: one wave, the 8 out-edges of
     // a popped vertex evaluated by lanes 0..7 (distinct heads, so in parallel), then the pushes and
     // SLF swaps in edge order.  inf = 2 * H * W (pyx:38); queue as a ring (live entries <= cells).
     // Blocked and border cells hold -inf, so `new < dist[v]` is false for them: no free-bit test per
-    // edge.  Per pop ONE round of LDS reads (dist[u], dist[v], in_queue[v], the next front) -- the
-    // front of the queue lives in a register (it is either the prefetched next entry or the vertex
-    // an SLF swap just put there), so no read waits for the previous pop's writes except the SLF
-    // front's distance, read only when a pop pushes.
+    // edge.  Per pop ONE round of LDS reads (dist[u], dist[v], pin[v] -- lane 8's v is u itself, so
+    // its pin read is u's --, the next front) -- the front of the queue lives in a register (it is
+    // either the prefetched next entry or the vertex an SLF swap just put there), so no read waits
+    // for the previous pop's writes except the SLF front's distance, read only when a pop pushes.
     const float INFR = (float)(2 * H * W);
     if (tid == 0) STAMP_NB(2);
-    for (int k = tid; k < cells; k += NT) {
+    for (int k = tid; k < cells; k += PNT) {
         const int rr = k / pw, cc = k - rr * pw;  // (once per cell)
         const bool fr = rr >= 1 && rr <= h && cc >= 1 && cc <= w && b_test(S.freeb[rr - 1], cc - 1);
         dist[k] = fr ? INFR : -INFINITY;
-        parent[k] = -1;
-        inq[k] = 0;
+        pin[k] = 0;
     }
     lds_barrier();
-    const bool src_ok = run_spfa;
     const int su = (sh.src_s[0][0] - sh.i0 + 1) * pw + (sh.src_s[0][1] - sh.j0 + 1);
     const int tv = (sh.src_s[1][0] - sh.i0 + 1) * pw + (sh.src_s[1][1] - sh.j0 + 1);
-    if (tid < 64 && src_ok) {
-        // pyx:30 direction order [0,-1],[0,1],[-1,-1],[-1,0],[-1,1],[1,-1],[1,0],[1,1] -> lanes 0..7
-        const int di = lane >= 8 ? 0 : lane < 2 ? 0 : (lane < 5 ? -1 : 1);
-        const int dj = lane >= 8 ? 0 : lane < 2 ? (lane == 0 ? -1 : 1) : ((lane - 2) % 3) - 1;
-        const float wl = (lane < 8 && di != 0 && dj != 0) ? SQRT2F : 1.0f;
-        const int doff = di * pw + dj;
-        if (lane == 0) { dist[su] = 0.0f; queue[0] = su; inq[su] = 1; }
+    if (tid < 64 && run_spfa) {
+        const int doff = lane < 8 ? dir_off(lane, pw) : 0;
+        const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
+        const uint8_t pbits = (uint8_t)((lane + 1) | 0x10);  // a relaxed head: parent edge `lane`, queued
+        if (lane == 0) { dist[su] = 0.0f; queue[0] = (uint16_t)su; pin[su] = 0x10; }
         __builtin_amdgcn_wave_barrier();
         int qh = 0, qt = 1, count = 1, front = su;  // live entries queue[qh .. qt) (mod cells); front == queue[qh]
         // (the wave's stores below are made by every lane with the same address and value: no exec
         // masking around them)
-        typedef __attribute__((address_space(3))) int lds_int;
-        typedef __attribute__((address_space(3))) uint8_t lds_u8;
         lds_float *Ld = (lds_float *)dist;
-        lds_int *Lp = (lds_int *)parent, *Lq = (lds_int *)queue;
-        lds_u8 *Li = (lds_u8 *)inq;
-        for (int pops = 0; count > 0 && pops < (1 << 24); pops++) {  // the guard is never reached by a correct SPFA
+        lds_u16 *Lq = (lds_u16 *)queue;
+        lds_u8 *Li = (lds_u8 *)pin;
+        int pops = 0;
+        for (; count > 0 && pops < SIMAPS_POP_CAP; pops++) {  // the cap is never reached by a correct SPFA
             const int u = front;
             qh = qh + 1 == cells ? 0 : qh + 1;
             count--;
-            Li[u] = 0;
             const int v = u + doff;
             // one round of reads (in-order LDS sees this wave's earlier writes); the ballots below
             // consume them together
             const int nfr = Lq[qh];  // the next front (valid if count > 0)
             const float du = Ld[u], dv = Ld[v];
-            const int iqv = Li[v];
+            const int pv = Li[v];
             const float nd = du + wl;
             const bool better = lane < 8 && nd < dv;
             const uint64_t imp = __ballot(better);
-            const uint64_t notq = __ballot(iqv == 0);
+            const uint64_t notq = __ballot(!(pv & 0x10));
             int nf = __builtin_amdgcn_readfirstlane(nfr);
+            Li[u] = (uint8_t)(__builtin_amdgcn_readlane(pv, 8) & 0xf);  // u leaves the queue (pyx:92)
             if (imp) {
-                if (better) { Ld[v] = nd; Lp[v] = u; }
+                if (better) { Ld[v] = nd; Li[v] = pbits; }
                 const uint64_t push = imp & notq;
                 if (push) {
                     // The pushes of this pop, in edge order, resolved lane-parallel (lanes 0-7 own the
@@ -2670,10 +2678,9 @@ __device__ __forceinline__ int path_core(Shared &sh, SsspScratch &S, char *smem,
                     }
                     if (isP) {
                         const int slot = qt + rank < cells ? qt + rank : qt + rank - cells;
-                        Lq[slot] = content;
-                        Li[v] = 1;
+                        Lq[slot] = (uint16_t)content;
                     }
-                    if (sF0) Lq[qh] = newfront;  // after the lanes' stores (in the empty case qh is p1's slot)
+                    if (sF0) Lq[qh] = (uint16_t)newfront;  // after the lanes' stores (in the empty case qh is p1's slot)
                     qt = qt + np < cells ? qt + np : qt + np - cells;
                     count += np;
                     nf = newfront;
@@ -2681,41 +2688,46 @@ __device__ __forceinline__ int path_core(Shared &sh, SsspScratch &S, char *smem,
             }
             front = nf;
         }
+        if (lane == 0) {
+            STAMP_VAL(7, pops);  // (stamp build: tools/path_profile.py reports ns per pop)
+            if (count > 0) sh.fault |= SIMAPS_FAULT_ROUNDS;  // the pop cap stopped a live queue
+        }
     }
     lds_barrier();
     if (tid == 0) STAMP_NB(3);
-    // (4) dense path: parents from the target back to the source (pyx:131-138), global (i, j) packed
+    // (4) dense path: parents from the target back to the source (pyx:131-138), as rect cells
     if (tid == 0) {
         int cnt = 0, v = tv;
-        if (src_ok) {
-            dense[cnt++] = v;
+        auto pack = [&](int c) { const int rr = c / pw; return (uint16_t)(((rr - 1) << 8) | (c - rr * pw - 1)); };
+        if (run_spfa) {
+            dense[cnt++] = pack(v);
             while (v != su) {
-                v = parent[v];
-                if (v < 0) break;
-                dense[cnt++] = v;
+                const int p = pin[v] & 0xf;
+                if (!p) break;
+                v -= dir_off(p - 1, pw);
+                dense[cnt++] = pack(v);
             }
-        }
-        for (int k = 0; k < cnt; k++) {
-            const int r = dense[k] / pw - 1 + sh.i0, c = dense[k] % pw - 1 + sh.j0;
-            dense[k] = (r << 16) | c;
         }
         sh.nseg = cnt;
     }
     lds_barrier();
     const int nd = sh.nseg;
     if (tid == 0) STAMP_NB(4);
-    // (5) approximate_polygon(dense, tolerance=1) (skimage 0.18.3 measure/_polygon.py), one wave
-    uint8_t *chain = inq;
-    for (int k = tid; k < nd; k += NT) chain[k] = (k == 0 || k == nd - 1) ? 1 : 0;
+    // (5) approximate_polygon(dense, tolerance=1) (skimage 0.18.3 measure/_polygon.py), one wave, on
+    // the global (row, col) indices like the reference (the fp64 distances are not translation-exact)
+    for (int k = tid; k < nd; k += PNT) chain[k] = (k == 0 || k == nd - 1) ? 1 : 0;
     lds_barrier();
+    const int gi0 = sh.i0, gj0 = sh.j0;
     if (tid < 64 && nd > 0) {
         int sp = 0, iters = 0;
-        if (lane == 0) { stack[0] = 0; stack[1] = nd - 1; }
+        if (lane == 0) stack[0] = (uint32_t)(nd - 1) << 16;
         sp = 1;
         while (sp > 0 && ++iters <= 2 * nd) {  // each pop either splits at a new chain point or ends
             sp--;
-            const int start = stack[2 * sp], end = stack[2 * sp + 1];
-            const int r0 = dense[start] >> 16, c0 = dense[start] & 0xffff, r1 = dense[end] >> 16, c1 = dense[end] & 0xffff;
+            const uint32_t se = stack[sp];
+            const int start = (int)(se & 0xffff), end = (int)(se >> 16);
+            const int r0 = (dense[start] >> 8) + gi0, c0 = (dense[start] & 0xff) + gj0;
+            const int r1 = (dense[end] >> 8) + gi0, c1 = (dense[end] & 0xff) + gj0;
             const long dr = r1 - r0, dc = c1 - c0;
             const double ang = -atan2((double)dr, (double)dc);
             const double sn = sin(ang), cs = cos(ang);
@@ -2723,7 +2735,7 @@ __device__ __forceinline__ int path_core(Shared &sh, SsspScratch &S, char *smem,
             double best = -1.0;
             int besti = -1;
             for (int k = start + 1 + lane; k < end; k += 64) {
-                const int rr = dense[k] >> 16, cc = dense[k] & 0xffff;
+                const int rr = (dense[k] >> 8) + gi0, cc = (dense[k] & 0xff) + gj0;
                 const long dr0 = rr - r0, dc0 = cc - c0, dr1 = rr - r1, dc1 = cc - c1;
                 const bool perp = dr0 * dr + dc0 * dc > 0 && -dr1 * dr - dc1 * dc > 0;
                 double d;
@@ -2740,8 +2752,8 @@ __device__ __forceinline__ int path_core(Shared &sh, SsspScratch &S, char *smem,
             if (best > 1.0) {  // np.any(segment_dists > tolerance)
                 const int ne = besti;
                 if (lane == 0) {
-                    stack[2 * sp] = ne; stack[2 * sp + 1] = end;
-                    stack[2 * sp + 2] = start; stack[2 * sp + 3] = ne;
+                    stack[sp] = (uint32_t)ne | ((uint32_t)end << 16);
+                    stack[sp + 1] = (uint32_t)start | ((uint32_t)ne << 16);
                     chain[ne] = 1;
                 }
                 sp += 2;
@@ -2766,7 +2778,7 @@ __device__ __forceinline__ int path_core(Shared &sh, SsspScratch &S, char *smem,
             cnt = 1;
             for (int k = 1; k < m - 1; k++) {
                 const int a = outp[cnt - 1], b2 = sparse[k + 1];
-                if (!line_free(sh, S, a >> 16, a & 0xffff, b2 >> 16, b2 & 0xffff, line_mask)) {
+                if (!line_free(sh, S, (a >> 8) + gi0, (a & 0xff) + gj0, (b2 >> 8) + gi0, (b2 & 0xff) + gj0, line_mask)) {
                     if (lane == 0) outp[cnt] = sparse[k];
                     cnt++;
                 }
@@ -2782,37 +2794,40 @@ __device__ __forceinline__ int path_core(Shared &sh, SsspScratch &S, char *smem,
     return 0;
 }
 
-__global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents,
-                                                  const simaps_env *__restrict__ envs,
-                                                  const simaps_robot *__restrict__ robots,
-                                                  const uint8_t *__restrict__ occupancy,
-                                                  const double *__restrict__ sources, const double *__restrict__ targets,
-                                                  int max_pts, double *__restrict__ out_xy, int *__restrict__ out_n)
+template <int CELLS>
+__global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents,
+                                                   const simaps_env *__restrict__ envs,
+                                                   const simaps_robot *__restrict__ robots,
+                                                   const uint8_t *__restrict__ occupancy,
+                                                   const double *__restrict__ sources, const double *__restrict__ targets,
+                                                   int max_pts, double *__restrict__ out_xy, int *__restrict__ out_n,
+                                                   unsigned *fault)
 {
-    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-    Shared &sh = *reinterpret_cast<Shared *>(smem);
-    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
+    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS>()];
+    PathHdr &sh = *reinterpret_cast<PathHdr *>(smem);
+    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_PS);
     const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int H = cfg.H, W = cfg.W;
+    const Group g{tid, PNT, nullptr, PNT / 64};
     if (tid == 0) STAMP_NB(0);
     const simaps_agent ag = agents[n];
-    OccLoad<NT> occ_regs;
-    cspace_load<NT>(occ_regs, occupancy + (size_t)ag.map_slot * H * W, H, W, cfg.room_i0, cfg.room_j0, cfg.room_h,
-                    cfg.room_w, tid);
     const double sx = sources[2 * n], sy = sources[2 * n + 1], tx = targets[2 * n], ty = targets[2 * n + 1];
     if (tid == 0) {
-        const simaps_env ev = envs[ag.env];
+        bool bad;
+        const int type = agent_robot_type(ag, envs, robots, bad);
+        sh.fault = bad ? SIMAPS_FAULT_DESCRIPTOR : 0u;
         sh.h = cfg.room_h;
         sh.w = cfg.room_w;
         sh.i0 = cfg.room_i0;
         sh.j0 = cfg.room_j0;
-        sh.r = geo.cspace_r[robots[ev.robot_off + ag.robot].type];
+        sh.r = geo.cspace_r[type];
         pos_to_pix(sx, sy, H, W, sh.src_q[0][0], sh.src_q[0][1]);
         pos_to_pix(tx, ty, H, W, sh.src_q[1][0], sh.src_q[1][1]);
         sh.nsrc = 2;
     }
     lds_barrier();
-    build_cspace<NT>(S, &occ_regs, sh.h, sh.w, sh.r, whole_wg());
+    build_cspace<PNT>(S, nullptr, sh.h, sh.w, sh.r, g, nullptr, 0, nullptr, occupancy + (size_t)ag.map_slot * H * W, H,
+                      W, sh.i0, sh.j0);
     double *o = out_xy + (size_t)n * max_pts * 2;
     // (1) straight line on cspace_thin between the unsnapped pixels (envs.py:2484-2486)
     if (tid < 64) {
@@ -2821,14 +2836,17 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
     }
     lds_barrier();
     if (sh.flag[0]) {
-        if (tid == 0) { o[0] = sx; o[1] = sy; o[2] = tx; o[3] = ty; out_n[n] = 2; }
+        if (tid == 0) {
+            o[0] = sx; o[1] = sy; o[2] = tx; o[3] = ty; out_n[n] = 2;
+            post_faults(fault, sh.fault);
+        }
         return;
     }
     // (2) snap both ends (envs.py:2489-2490)
     if (tid == 0) STAMP_NB(1);
-    snap_sources(sh, S, 2, whole_wg());
-    const int cnt = path_core(sh, S, smem, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE);
-    int *outp = reinterpret_cast<int *>(smem + OFF_DIST) + DIST_FLOATS;
+    snap_sources(sh, S, 2, g);
+    const uint16_t *outp;
+    const int cnt = path_core<CELLS>(sh, S, smem + OFF_PA, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE, outp);
     if (tid < 64) {
         // (7) positions (envs.py:2494-2503); path[0] / path[-1] replaced by the given positions
         if (cnt < 2) {
@@ -2837,7 +2855,7 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
             if (lane == 0) out_n[n] = -cnt;  // caller's buffer too small
         } else {
             for (int k = lane; k < cnt; k += 64) {
-                const int pv = outp[cnt - 1 - k], pi = pv >> 16, pj = pv & 0xffff;
+                const int pv = outp[cnt - 1 - k], pi = (pv >> 8) + sh.i0, pj = (pv & 0xff) + sh.j0;
                 double x = ((pj + 0.5) - (double)W / 2) / PPM, y = ((double)H / 2 - (pi + 0.5)) / PPM;
                 if (k == 0) { x = sx; y = sy; }
                 if (k == cnt - 1) { x = tx; y = ty; }
@@ -2846,6 +2864,7 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
             }
             if (lane == 0) out_n[n] = cnt;
         }
+        if (lane == 0) post_faults(fault, sh.fault);
     }
 }
 
@@ -2853,20 +2872,22 @@ __global__ void __launch_bounds__(NT) path_kernel(simaps_config cfg, Geometry ge
 // workgroup per (grid, source, target): the same exact SPFA / parent walk / approximate_polygon as
 // path_kernel, without the cspace, snap and straight-line steps of OccupancyMap.shortest_path, the
 // line-of-sight pruning on the grid itself, and the waypoints returned as cells (target last).
-__global__ void __launch_bounds__(NT) grid_path_kernel(int H, int W, const uint8_t *__restrict__ grids,
-                                                       const int32_t *__restrict__ sources,
-                                                       const int32_t *__restrict__ targets, int wi0, int wj0, int wh,
-                                                       int ww, int max_pts, int32_t *__restrict__ out_ij,
-                                                       int32_t *__restrict__ out_n)
+template <int CELLS>
+__global__ void __launch_bounds__(PNT) grid_path_kernel(int H, int W, const uint8_t *__restrict__ grids,
+                                                        const int32_t *__restrict__ sources,
+                                                        const int32_t *__restrict__ targets, int wi0, int wj0, int wh,
+                                                        int ww, int max_pts, int32_t *__restrict__ out_ij,
+                                                        int32_t *__restrict__ out_n, unsigned *fault)
 {
-    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-    Shared &sh = *reinterpret_cast<Shared *>(smem);
-    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
+    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS>()];
+    PathHdr &sh = *reinterpret_cast<PathHdr *>(smem);
+    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_PS);
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint8_t *grid = grids + (size_t)b * H * W;
     const int si = sources[2 * b], sj = sources[2 * b + 1], ti = targets[2 * b], tj = targets[2 * b + 1];
     if (tid == 0) {
         sh.h = wh; sh.w = ww; sh.i0 = wi0; sh.j0 = wj0;
+        sh.fault = 0u;
         const bool s_in = si >= wi0 && si < wi0 + wh && sj >= wj0 && sj < wj0 + ww;
         const bool t_in = ti >= wi0 && ti < wi0 + wh && tj >= wj0 && tj < wj0 + ww;
         // a source outside the window or blocked has no edges (pyx:56), and a target outside the
@@ -2876,7 +2897,7 @@ __global__ void __launch_bounds__(NT) grid_path_kernel(int H, int W, const uint8
     }
     // free bits (grid != 0: the SPFA's vertices, pyx:47-56) and grid == 1 bits (line of sight)
     const int nwords = (ww + 63) >> 6;
-    for (int item = wave; item < wh * 2; item += NT / 64) {
+    for (int item = wave; item < wh * 2; item += PNT / 64) {
         const int rr = item >> 1, wd = item & 1, c = wd * 64 + lane;
         const uint8_t v = (wd < nwords && c < ww) ? grid[(size_t)(wi0 + rr) * W + wj0 + c] : (uint8_t)0;
         const uint64_t mf = __ballot(v != 0), m1 = __ballot(v == 1);
@@ -2891,19 +2912,20 @@ __global__ void __launch_bounds__(NT) grid_path_kernel(int H, int W, const uint8
         if (tid == 0) { o[0] = ti; o[1] = tj; out_n[b] = 1; }
         return;
     }
-    const int cnt = path_core(sh, S, smem, H, W, true, LINE_GRID_ONE);
-    const int *outp = reinterpret_cast<const int *>(smem + OFF_DIST) + DIST_FLOATS;
+    const uint16_t *outp;
+    const int cnt = path_core<CELLS>(sh, S, smem + OFF_PA, H, W, true, LINE_GRID_ONE, outp);
     if (tid < 64) {
         if (cnt > max_pts) {
             if (lane == 0) out_n[b] = -cnt;  // caller's buffer too small
         } else {
             for (int k = lane; k < cnt; k += 64) {  // reversed (pyx:152): source first
                 const int pv = outp[cnt - 1 - k];
-                o[2 * k] = pv >> 16;
-                o[2 * k + 1] = pv & 0xffff;
+                o[2 * k] = (pv >> 8) + wi0;
+                o[2 * k + 1] = (pv & 0xff) + wj0;
             }
             if (lane == 0) out_n[b] = cnt;
         }
+        if (lane == 0) post_faults(fault, sh.fault);
     }
 }
 
@@ -2951,6 +2973,11 @@ constexpr int INGEST_WG = 256, INGEST_PPT = 8, INGEST_PTS = INGEST_WG * INGEST_P
 __host__ __device__ constexpr int ingest_chunks(int hc, int wc) { return (hc * wc + INGEST_PTS - 1) / INGEST_PTS; }
 constexpr int INGEST_WIN = 4096;  // LDS window entries (u64 keys) over a chunk's map-pixel box
 constexpr int INGEST_MAX_WC = 1024, INGEST_MAX_ROWS = 32;  // camera width; camera rows one chunk spans
+// A chunk's pixels k0 .. k0 + INGEST_PTS - 1 reach camera row k0 / Wc + 1 + (INGEST_PTS - 2) / Wc at most
+// (k0 % Wc = Wc - 1): its row table index must stay below INGEST_MAX_ROWS.  Smallest such width: 67.
+constexpr bool ingest_width_ok(int wc) { return wc >= 1 && wc <= INGEST_MAX_WC && 1 + (INGEST_PTS - 2) / wc < INGEST_MAX_ROWS; }
+constexpr int ingest_min_width(int wc = 1) { return ingest_width_ok(wc) ? wc : ingest_min_width(wc + 1); }
+static_assert(ingest_min_width() == 67, "include/simaps.h documents the camera width range [67, 1024]");
 constexpr int INGEST_RES_WG = 256, INGEST_RES_U = 8, INGEST_RES_G = 8;  // resolve: 8 workgroups per frame, 8 keys per thread in flight
 
 // Camera.capture_image's frame (envs.py:1932-1940) in float32: position, principal, up, right.
@@ -3242,11 +3269,13 @@ unsigned read_faults(bool clear)
 {
     unsigned f = 0;
     if (!g_fault_host) return 0;
-    for (int k = 0; k < SIMAPS_NFAULT; k++)
-        if (g_fault_host[k]) {
-            f |= 1u << k;
-            if (clear) g_fault_host[k] = 0;
-        }
+    for (int k = 0; k < SIMAPS_NFAULT; k++) {
+        // clear with an exchange: a fault posted by a launch still in flight between a read and a
+        // separate store of 0 would be erased unreported
+        const unsigned v = clear ? __atomic_exchange_n(&g_fault_host[k], 0u, __ATOMIC_ACQ_REL)
+                                 : __atomic_load_n(&g_fault_host[k], __ATOMIC_ACQUIRE);
+        if (v) f |= 1u << k;
+    }
     return f;
 }
 
@@ -3417,8 +3446,12 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
         return fail(SIMAPS_EINVAL, "NULL buffer");
     if ((rc = pending_faults())) return rc;
     const Geometry geo = make_geometry();
-    hipLaunchKernelGGL(path_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, geo, agents, envs, robots,
-                       occupancy, sources, targets, max_points, out_xy, out_count);
+    if ((cfg->room_h + 2) * ((cfg->room_w + 2) | 1) <= PATH_SMALL_CELLS)
+        hipLaunchKernelGGL(path_kernel<PATH_SMALL_CELLS>, dim3(N), dim3(PNT), 0, (hipStream_t)stream, *cfg, geo, agents, envs,
+                           robots, occupancy, sources, targets, max_points, out_xy, out_count, g_fault_dev);
+    else
+        hipLaunchKernelGGL(path_kernel<SIMAPS_MAX_ROOM_CELLS>, dim3(N), dim3(PNT), 0, (hipStream_t)stream, *cfg, geo, agents,
+                           envs, robots, occupancy, sources, targets, max_points, out_xy, out_count, g_fault_dev);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "shortest_path launch: %s", hipGetErrorString(e));
     return 0;
@@ -3443,8 +3476,8 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
     if (!agents || !seg_ids || !cam_params || !depth || !seg_raw || !overhead || !occupancy || !keys || !boxes)
         return fail(SIMAPS_EINVAL, "NULL buffer");
     const int np = cam->height_px * cam->width_px;
-    if (cam->width_px > INGEST_MAX_WC || INGEST_PTS / cam->width_px + 2 > INGEST_MAX_ROWS)
-        return fail(SIMAPS_EUNSUPPORTED, "camera width %d outside [%d, %d]", cam->width_px, INGEST_PTS / (INGEST_MAX_ROWS - 2) + 1, INGEST_MAX_WC);
+    if (!ingest_width_ok(cam->width_px))
+        return fail(SIMAPS_EUNSUPPORTED, "camera width %d outside [%d, %d]", cam->width_px, ingest_min_width(), INGEST_MAX_WC);
     if (np >= (1 << 28)) return fail(SIMAPS_EUNSUPPORTED, "camera frame of %d pixels (key packs pixel + 1 in 28 bits)", np);
     if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d frames per launch (grid y <= 65535)", N);
     const int nch = ingest_chunks(cam->height_px, cam->width_px);  // point-pass chunks per frame
@@ -3470,8 +3503,12 @@ int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *s
     if (ww > SIMAPS_MAX_ROOM_W || wh > MAX_ROWS || (wh + 2) * ((ww + 2) | 1) > SIMAPS_MAX_ROOM_CELLS)
         return fail(SIMAPS_EUNSUPPORTED, "window %dx%d exceeds the LDS-resident limit", wh, ww);
     if (const int rc = pending_faults()) return rc;
-    hipLaunchKernelGGL(grid_path_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, H, W, grids, sources, targets, wi0,
-                       wj0, wh, ww, max_points, out_ij, out_count);
+    if ((wh + 2) * ((ww + 2) | 1) <= PATH_SMALL_CELLS)
+        hipLaunchKernelGGL(grid_path_kernel<PATH_SMALL_CELLS>, dim3(B), dim3(PNT), 0, (hipStream_t)stream, H, W, grids, sources,
+                           targets, wi0, wj0, wh, ww, max_points, out_ij, out_count, g_fault_dev);
+    else
+        hipLaunchKernelGGL(grid_path_kernel<SIMAPS_MAX_ROOM_CELLS>, dim3(B), dim3(PNT), 0, (hipStream_t)stream, H, W, grids,
+                           sources, targets, wi0, wj0, wh, ww, max_points, out_ij, out_count, g_fault_dev);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "grid_path launch: %s", hipGetErrorString(e));
     return 0;

@@ -311,20 +311,11 @@ class StateBatch:
         sources / targets [n, 2] fp64 (x, y) for map slots `slots` (all agents if None) -> list of n
         waypoint lists [(x, y, 0), ...] like the reference returns (Robot.store_new_action,
         envs.py:875-876)."""
-        agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
-        src = torch.as_tensor(sources, dtype=torch.float64).to(self.device).contiguous()
-        tgt = torch.as_tensor(targets, dtype=torch.float64).to(self.device).contiguous()
-        if tuple(src.shape) != (n, 2) or tuple(tgt.shape) != (n, 2):
-            raise ValueError('sources and targets must be [%d, 2]' % n)
-        xy = torch.empty((n, max_points, 2), dtype=torch.float64, device=self.device)
-        cnt = torch.empty((n,), dtype=torch.int32, device=self.device)
+        n = self.N if slots is None else len(slots)
         if n == 0:
             return []
         s, cur = launch_stream(self.device, stream)
-        _lib.check(_lib.lib.simaps_shortest_path(
-            self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d), _lib.ptr(self.occupancy),
-            _lib.ptr(src), _lib.ptr(tgt), max_points, _lib.ptr(xy), _lib.ptr(cnt), _lib.stream_handle(s)))
-        hold(s, cur, src, tgt, xy, cnt, agents_d, self.envs_d, self.robots_d, self.occupancy)
+        xy, cnt = self.launch_shortest_paths(sources, targets, slots, max_points, stream)
         if s != cur:
             cur.wait_stream(s)
         xy, cnt = xy.cpu().numpy(), cnt.cpu().numpy()
@@ -333,6 +324,25 @@ class StateBatch:
             raise RuntimeError('a path has %d waypoints > max_points=%d' % (-cnt.min(), max_points))
         return [[(float(x), float(y), 0) for x, y in xy[k, :cnt[k]]] for k in range(n)]
 
+
+    def launch_shortest_paths(self, sources, targets, slots=None, max_points=64, stream=None):
+        """The device half of shortest_paths(): one launch, results left on the device as
+        (xy [n, max_points, 2] fp64, count [n] int32; count = -needed if max_points is too small)."""
+        agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
+        src = torch.as_tensor(sources, dtype=torch.float64).to(self.device).contiguous()
+        tgt = torch.as_tensor(targets, dtype=torch.float64).to(self.device).contiguous()
+        if tuple(src.shape) != (n, 2) or tuple(tgt.shape) != (n, 2):
+            raise ValueError('sources and targets must be [%d, 2]' % n)
+        xy = torch.empty((n, max_points, 2), dtype=torch.float64, device=self.device)
+        cnt = torch.empty((n,), dtype=torch.int32, device=self.device)
+        if n == 0:
+            return xy, cnt
+        s, cur = launch_stream(self.device, stream)
+        _lib.check(_lib.lib.simaps_shortest_path(
+            self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d), _lib.ptr(self.occupancy),
+            _lib.ptr(src), _lib.ptr(tgt), max_points, _lib.ptr(xy), _lib.ptr(cnt), _lib.stream_handle(s)))
+        hold(s, cur, src, tgt, xy, cnt, agents_d, self.envs_d, self.robots_d, self.occupancy)
+        return xy, cnt
 
     def ingest(self, depth, seg_raw, camera='forward', slots=None, seg_ids=None, stream=None):
         """Robot.update_map minus the simulator (envs.py:925, 2056-2066) for map slots `slots` (all

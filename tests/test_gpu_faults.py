@@ -110,6 +110,69 @@ def test_barrier_timeout_flag_reaches_the_caller(S):
     assert _lib.lib.simaps_fault_status(0) == 0       # the product library's word is separate
 
 
+def test_path_pop_cap_reaches_the_caller(S):
+    """the path kernels post SIMAPS_FAULT_ROUNDS when the SPFA's pop guard stops a live
+    queue (the diagnostic build caps it at 64 pops, which every detour query exceeds), so a capped
+    run cannot return wrong waypoints with rc 0; straight-line queries (no SPFA) post nothing."""
+    _lib, batch, synthetic = S
+    if not os.path.exists(DIAG_LIB):
+        pytest.fail('build the diagnostic library first: make -C spatial-intention-maps_amd/csrc diag')
+    L = _lib._load(DIAG_LIB)
+    L.simaps_fault_status(1)
+    scene = synthetic.make_scene('lifting_4-small_divider', 3)
+    b = batch.StateBatch([scene])
+    rl, rw = scene['room_length'], scene['room_width']
+
+    def run(src, tgt):
+        s = torch.tensor(src, dtype=torch.float64, device=b.device)
+        t = torch.tensor(tgt, dtype=torch.float64, device=b.device)
+        xy = torch.empty((b.N, 64, 2), dtype=torch.float64, device=b.device)
+        cnt = torch.empty((b.N,), dtype=torch.int32, device=b.device)
+        rc = L.simaps_shortest_path(b.cfg, b.N, _lib.ptr(b.agents_d), _lib.ptr(b.envs_d), _lib.ptr(b.robots_d),
+                                    _lib.ptr(b.occupancy), _lib.ptr(s), _lib.ptr(t), 64, _lib.ptr(xy), _lib.ptr(cnt),
+                                    _lib.stream_handle())
+        torch.cuda.synchronize()
+        return rc
+    # across the divider: every query needs a detour (SPFA)
+    src = [[-rl / 4, -rw / 4]] * b.N
+    tgt = [[rl / 4, rw / 4 - 0.01 * a] for a in range(b.N)]
+    assert run(src, tgt) == 0
+    assert L.simaps_fault_status(0) & _lib.FAULT_ROUNDS
+    with pytest.raises(_lib.DeviceFault):
+        _lib.check_faults(L)
+    # a straight line (same point) runs no SPFA: no fault
+    assert run(src, src) == 0
+    assert L.simaps_fault_status(0) == 0
+    assert _lib.lib.simaps_fault_status(0) == 0
+
+
+def test_path_bad_descriptor_is_reported(S):
+    """sp_distance / path kernels clamp a robot index past num_robots (and a robot class
+    outside 0..3) like get_state and post SIMAPS_FAULT_DESCRIPTOR."""
+    _lib, batch, synthetic = S
+    scene = synthetic.make_scene('lifting_4-small_divider', 5)
+    b = batch.StateBatch([scene])
+    robots, envs, ag, paths = batch.pack_descriptors([scene], b.agents)
+    robots = np.concatenate([robots, np.repeat(robots[:1], 8)])
+    ag['robot'][1] = 6
+    R, E, A = (_dev(batch, x, b.device) for x in (robots, envs, ag))
+    src = torch.zeros((b.N, 2), dtype=torch.float64, device=b.device)
+    tgt = torch.zeros((b.N, 3, 2), dtype=torch.float64, device=b.device)
+    out = torch.empty((b.N, 3), dtype=torch.float64, device=b.device)
+    _lib.lib.simaps_fault_status(1)
+    assert _lib.lib.simaps_sp_distance(b.cfg, b.N, _lib.ptr(A), _lib.ptr(E), _lib.ptr(R), _lib.ptr(b.occupancy),
+                                       _lib.ptr(src), _lib.ptr(tgt), 3, _lib.ptr(out), _lib.stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert _lib.lib.simaps_fault_status(1) == _lib.FAULT_DESCRIPTOR
+    xy = torch.empty((b.N, 64, 2), dtype=torch.float64, device=b.device)
+    cnt = torch.empty((b.N,), dtype=torch.int32, device=b.device)
+    assert _lib.lib.simaps_shortest_path(b.cfg, b.N, _lib.ptr(A), _lib.ptr(E), _lib.ptr(R), _lib.ptr(b.occupancy),
+                                         _lib.ptr(src), _lib.ptr(src), 64, _lib.ptr(xy), _lib.ptr(cnt),
+                                         _lib.stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert _lib.lib.simaps_fault_status(1) == _lib.FAULT_DESCRIPTOR
+
+
 def test_side_stream_render_matches_default_stream(S):
     """render on a non-current stream; outputs / inputs are held for that stream and the
     reader waits for it."""

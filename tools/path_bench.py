@@ -1,0 +1,68 @@
+"""Movement-path throughput (OccupancyMap.shortest_path, simaps_shortest_path) by launch size, GPU box.
+
+For each (config, envs): robot position -> a target across x = 0 (detours around the divider), all
+inputs resident; the device half alone, timed with HIP events on the launch stream over K launches.
+With --stamps (the stamp build libsimaps_prof.so) also the per-query SPFA time and pops, i.e. ns per
+pop.  One JSON line per launch size.
+
+    python tools/path_bench.py [--stamps]
+"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if '--stamps' in sys.argv:
+    os.environ['SIMAPS_LIB'] = os.environ.get('SIMAPS_PROF_LIB', os.path.join(ROOT, 'spatial-intention-maps_amd', 'simaps',
+                                                                                'libsimaps_prof.so'))
+sys.path.insert(0, os.path.join(ROOT, 'spatial-intention-maps_amd'))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from simaps import _lib, batch, synthetic  # noqa: E402
+
+
+def case(cfg, envs, steps):
+    scenes = [synthetic.make_scene(cfg, e % 64) for e in range(envs)]
+    b = batch.StateBatch(scenes)
+    rs = np.random.RandomState(0)
+    rl, rw = scenes[0]['room_length'], scenes[0]['room_width']
+    N = b.N
+    psrc = np.array([scenes[e]['robots'][a]['position'][:2] for e, a in b.agents])
+    ptgt = np.stack([rs.uniform(0.05, rl / 2, N) * -np.sign(psrc[:, 0]), rs.uniform(-rw / 2, rw / 2, N)], -1)
+    src = torch.as_tensor(psrc).cuda()
+    tgt = torch.as_tensor(ptgt).cuda()
+    for _ in range(2):
+        b.launch_shortest_paths(src, tgt)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(s)
+    for _ in range(steps):
+        xy, cnt = b.launch_shortest_paths(src, tgt)
+    e1.record(s)
+    torch.cuda.synchronize()
+    _lib.check_faults()
+    ms = e0.elapsed_time(e1) / steps
+    out = {'config': cfg, 'paths_per_launch': N, 'ms_per_launch': ms, 'paths_per_s': N / (ms * 1e-3),
+           'detours': int((cnt.cpu().numpy() > 2).sum())}
+    if '--stamps' in sys.argv:
+        L = _lib.lib
+        L.simaps_debug_read_stamps.argtypes = [ctypes.c_void_p]
+        st = np.zeros((8192, 80), dtype=np.uint64)
+        assert L.simaps_debug_read_stamps(st.ctypes.data) == 0
+        st = st[:min(N, 8192)].astype(np.int64)
+        full = st[:, 3] > 0  # ran the SPFA (not a straight line)
+        spfa_us = (st[full, 3] - st[full, 2]) / 100.0  # s_memrealtime: 100 MHz
+        pops = st[full, 7]
+        out.update({'spfa_queries': int(full.sum()), 'spfa_us_median': float(np.median(spfa_us)),
+                    'pops_median': float(np.median(pops)),
+                    'ns_per_pop_median': float(np.median(spfa_us * 1e3 / np.maximum(pops, 1))),
+                    'query_us_median': float(np.median((st[full, 6] - st[full, 0]) / 100.0))})
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == '__main__':
+    for cfg, envs in (('lifting_4-small_divider', 64), ('lifting_4-small_divider', 256), ('lifting_4-small_divider', 512),
+                      ('pushing_4-large_empty', 64), ('pushing_4-large_empty', 256), ('pushing_4-large_empty', 512)):
+        case(cfg, envs, 5 if '--stamps' in sys.argv else 10)
