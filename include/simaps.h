@@ -177,6 +177,19 @@ int simaps_fault_status(int clear);
 /* Number of channels C of the stack for an env with `num_robots` robots (envs.py:2071-2113). */
 int simaps_num_channels(const simaps_config *cfg, int num_robots);
 
+/* Host helper: the per-step robot descriptors from arrays (the drop-in's array fast path), HOST memory.
+ *   pose [R][3] (x, y, heading), target [R][2] (target_end_effector_position[:2]), flags [R] (bit 0
+ *   idle, bit 1 LiftingRobot lift_state == 'lifting'), type_group [R][2] (SIMAPS_* class, group_index),
+ *   waypoints [R][K][2] (robot.waypoint_positions[:, :2], padded), wp_count [R] (len(waypoint_positions),
+ *   -1 = None: a robot that has not acted yet, which must be idle), wp_index [R]
+ *   (controller.waypoint_index) -> robots [R] and paths [R][2 * SIMAPS_MAX_PATH][2]: robot r's
+ *   intention path (RobotController.get_intention_path, envs.py:1475-1476) at point 2 r P, its reversed
+ *   history path (get_history_path()[::-1], envs.py:1478-1479, 2318) at 2 r P + P (P = SIMAPS_MAX_PATH).
+ *   Byte-identical to packing the same robots one by one.  SIMAPS_EUNSUPPORTED if a path exceeds P points. */
+int simaps_pack_robots(int R, const double *pose, const double *target, const int32_t *flags, const int32_t *type_group,
+                       const double *waypoints, int K, const int32_t *wp_count, const int32_t *wp_index,
+                       simaps_robot *robots, double *paths);
+
 /* Host helper: Mapper._create_robot_mask(cls, show_lifted_cube) into out[96*96] (float32, host). */
 int simaps_robot_mask(int type, int with_cube, float *out);
 

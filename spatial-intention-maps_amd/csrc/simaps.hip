@@ -3378,6 +3378,67 @@ int simaps_num_channels(const simaps_config *c, int num_robots)
     return n;
 }
 
+int simaps_pack_robots(int R, const double *pose, const double *target, const int32_t *flags, const int32_t *type_group,
+                       const double *waypoints, int K, const int32_t *wp_count, const int32_t *wp_index,
+                       simaps_robot *robots, double *paths)
+{
+    if (R < 0 || K < 0) return fail(SIMAPS_EINVAL, "R < 0 or K < 0");
+    if (R == 0) return 0;
+    if (!pose || !target || !flags || !type_group || !wp_count || !wp_index || !robots || !paths || (K > 0 && !waypoints))
+        return fail(SIMAPS_EINVAL, "NULL buffer");
+    constexpr int P = SIMAPS_MAX_PATH;
+    for (int r = 0; r < R; r++) {
+        simaps_robot &o = robots[r];
+        const double x = pose[3 * r], y = pose[3 * r + 1];
+        const int t = type_group[2 * r], g = type_group[2 * r + 1];
+        if (t < 0 || t > 3 || g < 0 || g > 3) return fail(SIMAPS_EINVAL, "robot %d: class %d / group %d", r, t, g);
+        const bool idle = flags[r] & 1;
+        const int n = wp_count[r], idx = wp_index[r];
+        o.x = x;
+        o.y = y;
+        o.heading = pose[3 * r + 2];
+        o.type = t;
+        o.group_index = g;
+        o.lifting = (flags[r] >> 1) & 1;
+        o.idle = idle;
+        o.intention_off = 2 * P * r;
+        o.history_off = 2 * P * r + P;
+        double *ip = paths + (size_t)2 * (2 * P * r), *hp = ip + 2 * P;
+        if (n < 0) {  // never acted: waypoints / target / index None (envs.py:828-832, 958-963, 1373-1376)
+            if (!idle) return fail(SIMAPS_EINVAL, "robot %d is not idle but has no waypoints", r);
+            o.target_x = o.target_y = 0.0;
+            o.intention_len = o.history_len = 0;
+            continue;
+        }
+        if (n > K || idx < 0) return fail(SIMAPS_EINVAL, "robot %d: %d waypoints (K = %d), index %d", r, n, K, idx);
+        o.target_x = target[2 * r];
+        o.target_y = target[2 * r + 1];
+        const double *w = waypoints + (size_t)2 * K * r;
+        // get_intention_path (envs.py:1475-1476): [position] + waypoints[idx:-1] + [target]
+        const int mid = idx < n - 1 ? n - 1 - idx : 0;
+        // get_history_path()[::-1] (envs.py:1478-1479, 2318): [position] + waypoints[:idx] reversed
+        const int hist = idx < n ? idx : n;
+        if (mid + 2 > P || hist + 1 > P) return fail(SIMAPS_EUNSUPPORTED, "robot %d: path longer than %d points", r, P);
+        ip[0] = x;
+        ip[1] = y;
+        for (int k = 0; k < mid; k++) {
+            ip[2 + 2 * k] = w[2 * (idx + k)];
+            ip[3 + 2 * k] = w[2 * (idx + k) + 1];
+        }
+        ip[2 + 2 * mid] = target[2 * r];
+        ip[3 + 2 * mid] = target[2 * r + 1];
+        o.intention_len = mid + 2;
+        hp[0] = x;
+        hp[1] = y;
+        for (int k = 0; k < hist; k++) {
+            hp[2 + 2 * k] = w[2 * (hist - 1 - k)];
+            hp[3 + 2 * k] = w[2 * (hist - 1 - k) + 1];
+        }
+        o.history_len = hist + 1;
+    }
+    return 0;
+}
+
 int simaps_robot_mask(int type, int with_cube, float *out)
 {
     if (type < 0 || type > 3 || !out) return fail(SIMAPS_EINVAL, "bad robot type / output");

@@ -74,6 +74,8 @@ def _load(path=LIB_PATH):
     L.simaps_last_error.restype = ctypes.c_char_p
     L.simaps_num_channels.argtypes = [ctypes.POINTER(Config), i32]
     L.simaps_num_channels.restype = i32
+    L.simaps_pack_robots.argtypes = [i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp]
+    L.simaps_pack_robots.restype = i32
     L.simaps_robot_mask.argtypes = [i32, i32, vp]
     L.simaps_robot_mask.restype = i32
     L.simaps_get_state.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, vp, i32,
@@ -101,7 +103,7 @@ def _load(path=LIB_PATH):
 lib = _load()
 
 EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_fault_status', 'simaps_num_channels',
-            'simaps_robot_mask', 'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest', 'simaps_ingest_chunks',
+            'simaps_robot_mask', 'simaps_pack_robots', 'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest', 'simaps_ingest_chunks',
             'simaps_sssp_grid', 'simaps_grid_path')
 
 # error codes and device fault bits (include/simaps.h)

@@ -115,6 +115,29 @@ def pack_descriptors(scenes, agents):
     return robots, envs, ag, paths
 
 
+def descriptor_arrays(scenes):
+    """The per-step robot state of `scenes` as the arrays StateBatch.set_descriptor_arrays takes
+    (what a simulator keeps per robot anyway): pose [R, 3], target [R, 2], idle [R], lifting [R],
+    waypoints [R, K, 2] (padded), wp_count [R] (-1: None, never acted), wp_index [R]; R = all
+    robots of all scenes in order."""
+    rl = [r for s in scenes for r in s['robots']]
+    R = len(rl)
+    K = max([len(r['waypoint_positions']) for r in rl if r['waypoint_positions'] is not None] + [1])
+    out = {'pose': np.zeros((R, 3)), 'target': np.zeros((R, 2)), 'idle': np.zeros(R, bool), 'lifting': np.zeros(R, bool),
+           'waypoints': np.zeros((R, K, 2)), 'wp_count': np.full(R, -1, np.int32), 'wp_index': np.zeros(R, np.int32)}
+    for k, r in enumerate(rl):
+        out['pose'][k] = (r['position'][0], r['position'][1], r['heading'])
+        out['idle'][k] = bool(r['idle'])
+        out['lifting'][k] = r.get('lift_state') == 'lifting'
+        if r['waypoint_positions'] is not None and r['target_ee'] is not None and r['waypoint_index'] is not None:
+            out['target'][k] = r['target_ee'][:2]
+            w = np.asarray([p[:2] for p in r['waypoint_positions']], dtype=np.float64).reshape(-1, 2)
+            out['waypoints'][k, :len(w)] = w
+            out['wp_count'][k] = len(w)
+            out['wp_index'][k] = r['waypoint_index']
+    return out
+
+
 def resolve_device(device):
     """torch.device with an explicit index ('cuda' -> 'cuda:<current>'), so tensors' devices compare equal."""
     dev = torch.device(device)
@@ -180,12 +203,18 @@ class StateBatch:
         self.occupancy = torch.from_numpy(occ).to(self.device)
         self.overhead = torch.from_numpy(ovh).to(self.device)
         self.set_descriptors(scenes)
+        self.n_robots = sum(len(s['robots']) for s in scenes)
+        self._type_group = np.array([(_lib.TYPE_IDS[r['type']], r['group_index']) for s in scenes for r in s['robots']],
+                                    dtype=np.int32).reshape(-1, 2)
         self.layout = layout
 
     def set_descriptors(self, scenes):
         """Upload a new per-step scene descriptor (poses, controller state, paths)."""
         robots, envs, ag, paths = pack_descriptors(scenes, self.agents)
-        self.scenes = scenes  # (ingest takes the camera pose from here)
+        self.scenes = scenes
+        # (ingest takes the camera poses from here)
+        self.pose_host = np.stack([robots['x'], robots['y'], robots['heading']], 1) if len(robots) else np.zeros((0, 3))
+        self._robot_off = envs['robot_off'].astype(np.int64)
         # one host->device copy for the four arrays (256-B aligned sections of one byte buffer):
         # each small copy costs a driver round trip
         parts = [np.ascontiguousarray(a).view(np.uint8).reshape(-1) for a in (robots, envs, ag, paths)]
@@ -197,6 +226,48 @@ class StateBatch:
         self.robots_d, self.envs_d, self.agents_d, self.paths_d = (dev[o:o + p.nbytes] for o, p in zip(offs, parts))
         if not hasattr(self, '_subsets'):
             self._subsets = {}  # subset agent lists depend on self.agents only: kept across steps
+
+    # -- the array fast path ----------------------------------------------------
+    def set_descriptor_arrays(self, pose, target, idle, lifting, waypoints, wp_count, wp_index):
+        """Per-step robot state as arrays, all robots of all envs in order (R = robots in the batch;
+        shapes as descriptor_arrays() returns, [E, A, ...] accepted): packed into the C structs by
+        the native simaps_pack_robots (no per-robot Python), staged in pinned host memory and
+        uploaded with ONE asynchronous copy on the current stream.  Robot classes / groups, the envs
+        and the agent list are the batch's (fixed at construction); only poses, targets, flags and
+        paths change per step."""
+        R = self.n_robots
+        f64 = lambda a, *shape: np.ascontiguousarray(a, dtype=np.float64).reshape(*shape)  # noqa: E731
+        pose, target = f64(pose, R, 3), f64(target, R, 2)
+        wps = np.ascontiguousarray(waypoints, dtype=np.float64)
+        K = wps.shape[-2] if wps.ndim >= 2 else 0
+        wps = wps.reshape(R, K, 2)
+        flags = (np.asarray(idle, dtype=np.int32).reshape(R) | (np.asarray(lifting, dtype=np.int32).reshape(R) << 1))
+        cnt = np.ascontiguousarray(wp_count, dtype=np.int32).reshape(R)
+        idx = np.ascontiguousarray(wp_index, dtype=np.int32).reshape(R)
+        if getattr(self, '_stage', None) is None:
+            self._rob_bytes = -(-R * _lib.ROBOT_DTYPE.itemsize // 256) * 256
+            nb = self._rob_bytes + R * 2 * _lib.MAX_PATH * 16
+            # a ring of pinned staging buffers: one is rewritten only after its copy has completed
+            self._stage = [torch.empty(max(nb, 256), dtype=torch.uint8).pin_memory() for _ in range(3)]
+            self._stage_ev = [None] * 3
+            self._stage_k = 0
+        k = self._stage_k
+        self._stage_k = (k + 1) % len(self._stage)
+        if self._stage_ev[k] is not None:
+            self._stage_ev[k].synchronize()
+        host = self._stage[k]
+        hp = host.data_ptr()
+        _lib.check(_lib.lib.simaps_pack_robots(
+            R, pose.ctypes.data, target.ctypes.data, flags.ctypes.data, self._type_group.ctypes.data,
+            wps.ctypes.data if K else None, K, cnt.ctypes.data, idx.ctypes.data, hp, hp + self._rob_bytes))
+        dev = torch.empty(host.shape, dtype=torch.uint8, device=self.device)
+        dev.copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._stage_ev[k] = ev
+        self.robots_d = dev[:R * _lib.ROBOT_DTYPE.itemsize]
+        self.paths_d = dev[self._rob_bytes:]
+        self.pose_host = pose
 
     def set_maps(self, occupancy=None, overhead=None, slots=None):
         """Replace the per-agent global maps -- what Mapper.update / OccupancyMap.update produce each
@@ -367,9 +438,8 @@ class StateBatch:
         want = (n, spec.height_px, spec.width_px)
         if tuple(dep.shape) != want or tuple(seg.shape) != want:
             raise ValueError('depth and seg_raw must be %s' % (want,))
-        params = np.array([spec.params(self.scenes[e]['robots'][a]['position'][0], self.scenes[e]['robots'][a]['position'][1],
-                                       self.scenes[e]['robots'][a]['heading']) for e, a in (self.agents[k] for k in idx)],
-                          dtype=np.float64).reshape(n, 9)
+        poses = [self.pose_host[self._robot_off[e] + a] for e, a in (self.agents[k] for k in idx)]
+        params = np.array([spec.params(p[0], p[1], p[2]) for p in poses], dtype=np.float64).reshape(n, 9)
         ids = np.zeros(len(self.scenes), dtype=_lib.SEG_IDS_DTYPE)
         for e, sc in enumerate(self.scenes):
             d = (seg_ids[e] if seg_ids is not None else synthetic.SEG_IDS)

@@ -45,6 +45,8 @@ class VectorEnvObservations:
         self.groups = [robot_groups(s) for s in scenes]
         self.slot = {ea: n for n, ea in enumerate(self.batch.agents)}
         self.num_envs = len(scenes)
+        # [env][group] -> map slots of the group's robots (the all-robots get_state structure)
+        self._all_slots = [[[self.slot[(e, a)] for a in g] for g in self.groups[e]] for e in range(self.num_envs)]
 
     # -- per-step inputs -------------------------------------------------------------------------
     def update(self, scenes=None, occupancy=None, overhead=None, slots=None):
@@ -58,6 +60,22 @@ class VectorEnvObservations:
         if occupancy is not None or overhead is not None:
             self.batch.set_maps(occupancy, overhead, slots)
 
+    def update_arrays(self, pose, target, idle, lifting, waypoints, wp_count, wp_index):
+        """update() from per-robot arrays instead of scene dicts (the fast path: native packing,
+        one pinned asynchronous upload); see StateBatch.set_descriptor_arrays / batch.descriptor_arrays."""
+        self.batch.set_descriptor_arrays(pose, target, idle, lifting, waypoints, wp_count, wp_index)
+
+    def update_map(self, robots, depth, seg_raw, camera='forward', seg_ids=None, stream=None):
+        """Robot.update_map() (envs.py:925-926) for the robots `robots` ([(env, robot), ...], distinct)
+        from their camera frames (depth buffer [n, Hc, Wc] float32, segmentation body ids [n, Hc, Wc]):
+        one simaps_ingest launch updates their overhead / occupancy maps in place on the device, with
+        the camera poses of the current descriptor.  Called for every robot by VectorEnv.reset()
+        (envs.py:214-215), for the awaiting robots at the end of VectorEnv.step() (277-280), and for
+        a single moving robot every 200 simulation steps by RobotController.step (1401-1403) --
+        successive calls apply in order (stream order)."""
+        self.batch.ingest(depth, seg_raw, camera=camera, slots=[self.slot[(e, a)] for e, a in robots],
+                          seg_ids=seg_ids, stream=stream)
+
     # -- VectorEnv.get_state ---------------------------------------------------------------------
     def get_state(self, all_robots=False, awaiting=None, save_figures=False, numpy=False, stream=None):
         """[env][group][robot] -> (96, 96, C) float32 state, or None for robots not awaiting a new
@@ -66,10 +84,19 @@ class VectorEnvObservations:
         like the reference (one device->host copy for the whole batch); otherwise device tensors."""
         if save_figures:
             raise NotImplementedError('save_figures is a host-side matplotlib debug path (out of scope)')
+        if all_robots or awaiting is None:  # every robot: the batch's own agent list, structure precomputed
+            out = self.batch.as_hwc(self.batch.render(stream=stream))
+            if numpy:
+                if stream is not None:
+                    torch.cuda.current_stream(self.batch.device).wait_stream(stream)
+                out = out.cpu().numpy()
+                _lib.check_faults()
+            rows = out if numpy else out.unbind(0)
+            return [[[rows[k] for k in g] for g in env] for env in self._all_slots]
         want = []
         for e, s in enumerate(self.batch.scenes):
             for a in range(len(s['robots'])):
-                if all_robots or awaiting is None or awaiting[e][a]:
+                if awaiting[e][a]:
                     want.append(self.slot[(e, a)])
         out = self.batch.as_hwc(self.batch.render(slots=want, stream=stream))
         if numpy:

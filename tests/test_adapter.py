@@ -158,3 +158,58 @@ def test_adapter_on_reference_objects_matches_fixture(path):
             rob = batch.pack_descriptors([got], agents)[0]
             assert (rob['idle'] == 1).all() and (rob['intention_len'] == 0).all()
         e += 1
+
+
+@pytest.mark.parametrize('cfg', ['lifting_4-small_divider', 'lifting_2_throwing_2-large_empty', 'rescue_4-small_empty',
+                                 'lifting_4-large_rooms-history', 'lifting_4-large_doors'])
+def test_native_pack_robots_matches_scene_packing(cfg):
+    """simaps_pack_robots (the drop-in's array fast path, host C++) writes the same robot records and
+    the same intention / history path points as pack_descriptors -- only the path offsets differ
+    (fixed stride 2 * SIMAPS_MAX_PATH per robot) -- including robots that never acted."""
+    from simaps import _lib
+    scenes = [synthetic.make_scene(cfg, 40 + e) for e in range(4)]
+    scenes[1] = synthetic.never_acted(scenes[1])
+    scenes[2] = synthetic.never_acted(scenes[2], robots=[1, 2])
+    agents = [(e, a) for e, s in enumerate(scenes) for a in range(len(s['robots']))]
+    want_r, _, _, want_p = batch.pack_descriptors(scenes, agents)
+    d = batch.descriptor_arrays(scenes)
+    R = len(want_r)
+    P = _lib.MAX_PATH
+    tg = np.array([(_lib.TYPE_IDS[r['type']], r['group_index']) for s in scenes for r in s['robots']], np.int32)
+    flags = d['idle'].astype(np.int32) | (d['lifting'].astype(np.int32) << 1)
+    got_r = np.zeros(R, _lib.ROBOT_DTYPE)
+    got_p = np.zeros((R * 2 * P, 2))
+    K = d['waypoints'].shape[1]
+    assert _lib.lib.simaps_pack_robots(R, d['pose'].ctypes.data, d['target'].ctypes.data, flags.ctypes.data,
+                                       tg.ctypes.data, d['waypoints'].ctypes.data, K, d['wp_count'].ctypes.data,
+                                       d['wp_index'].ctypes.data, got_r.ctypes.data, got_p.ctypes.data) == 0
+    for f in _lib.ROBOT_DTYPE.names:
+        if f.endswith('_off'):
+            continue
+        assert np.array_equal(got_r[f], want_r[f]), f
+    for k in range(R):
+        for name in ('intention', 'history'):
+            n = want_r[name + '_len'][k]
+            a = want_p[want_r[name + '_off'][k]:][:n]
+            b = got_p[got_r[name + '_off'][k]:][:n]
+            assert a.tobytes() == b.tobytes(), (k, name)
+
+
+def test_native_pack_robots_rejects_bad_rows():
+    from simaps import _lib
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 1)]
+    d = batch.descriptor_arrays(scenes)
+    tg = np.zeros((4, 2), np.int32)
+    out_r = np.zeros(4, _lib.ROBOT_DTYPE)
+    out_p = np.zeros((4 * 2 * _lib.MAX_PATH, 2))
+
+    def pack(flags, cnt, idx, wps):
+        return _lib.lib.simaps_pack_robots(4, d['pose'].ctypes.data, d['target'].ctypes.data, flags.ctypes.data,
+                                           tg.ctypes.data, wps.ctypes.data, wps.shape[1], cnt.ctypes.data,
+                                           idx.ctypes.data, out_r.ctypes.data, out_p.ctypes.data)
+    moving = np.zeros(4, np.int32)
+    cnt = d['wp_count'].copy()
+    cnt[2] = -1  # None paths on a moving robot
+    assert pack(moving, cnt, d['wp_index'], d['waypoints']) == _lib.EINVAL
+    long_w = np.zeros((4, 20, 2))
+    assert pack(moving, np.full(4, 20, np.int32), np.ones(4, np.int32), long_w) == _lib.EUNSUPPORTED

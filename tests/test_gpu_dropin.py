@@ -507,3 +507,74 @@ def test_rotate_rounding_modes(V, cfg):
         differ += not _bitwise(sf[n], z['e%d_a%d_state' % (e, a)])
         assert _bitwise(sf[n], O.agent_state(fma[e], a)), (e, a)
     assert differ >= len(bf.agents) // 2, differ
+
+
+@pytest.mark.parametrize('cfg', ['lifting_4-small_divider', 'lifting_2_throwing_2-large_empty', 'rescue_4-small_empty',
+                                 'lifting_4-large_rooms-history', 'lifting_4-small_divider-spatial'])
+def test_update_arrays_matches_scene_update(V, cfg):
+    """The array fast path (update_arrays: native packing, pinned one-copy upload) renders exactly
+    what update(scenes) renders, over several steps (the staging ring wraps), with robots that never
+    acted among them; both equal the oracle."""
+    synthetic, vector_env = V
+    from simaps import batch
+    base = [synthetic.make_scene(cfg, 300 + e) for e in range(4)]
+    a = vector_env.VectorEnvObservations(base, layout='chw')
+    b = vector_env.VectorEnvObservations(base, layout='chw')
+    for step in range(5):
+        scenes = [synthetic.make_scene(cfg, 300 + e, seed_base=77 * step) for e in range(4)]
+        for e, sc in enumerate(scenes):  # the maps stay the batch's (base scenes')
+            sc['occupancy'], sc['overhead'] = base[e]['occupancy'], base[e]['overhead']
+        if step % 2:
+            scenes[1] = synthetic.never_acted(scenes[1])
+            scenes[3] = synthetic.never_acted(scenes[3], robots=[0, 2])
+        a.update(scenes=scenes)
+        b.update_arrays(**batch.descriptor_arrays(scenes))
+        sa = a.get_state(all_robots=True, numpy=True)
+        sb = b.get_state(all_robots=True, numpy=True)
+        for e in range(4):
+            for ga, gb, idx in zip(sa[e], sb[e], vector_env.robot_groups(scenes[e])):
+                for xa, xb, r in zip(ga, gb, idx):
+                    assert _bitwise(xa, xb), (step, e, r)
+                    if step in (0, 3):
+                        assert _bitwise(xb, O.agent_state(scenes[e], r)), (step, e, r)
+
+
+def test_periodic_remap_successive_frames(V):
+    """RobotController.step's periodic update_map (envs.py:1401-1403): one moving robot's K frames,
+    taken at K successive poses, ingested in K single-robot launches (each after the pose update)
+    equal the oracle applying the same frames in order; the robot's next state is the oracle's."""
+    synthetic, vector_env = V
+    from simaps import batch, camera
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 330 + e) for e in range(4)]
+    obs = vector_env.VectorEnvObservations(scenes, layout='hwc')
+    spec = camera.CAMERAS['forward']
+    e, a = 2, 1
+    sc = scenes[e]
+    ref_ov, ref_oc = sc['overhead'][a].copy(), sc['occupancy'][a].copy()
+    x0, y0, h0 = sc['robots'][a]['position'][0], sc['robots'][a]['position'][1], sc['robots'][a]['heading']
+    arrays = batch.descriptor_arrays(scenes)
+    r = obs.batch._robot_off[e] + a
+    for k in range(4):  # the robot drives 2 cm and turns 10 degrees per re-map
+        pose = (x0 + 0.02 * k * np.cos(h0), y0 + 0.02 * k * np.sin(h0), h0 + np.radians(10) * k)
+        arrays['pose'][r] = pose
+        obs.update_arrays(**arrays)
+        moved = dict(sc, robots=[dict(rb) for rb in sc['robots']])
+        moved['robots'][a]['position'] = (pose[0], pose[1], 0)
+        moved['robots'][a]['heading'] = pose[2]
+        db, raw = synthetic.camera_images(moved, a, 'forward', seed=900 + k)
+        obs.update_map([(e, a)], db[None], raw[None])
+        O.ingest(ref_ov, ref_oc, db, raw, spec.params(*pose), spec, synthetic.SEG_IDS, True)
+    slot = obs.slot[(e, a)]
+    assert _bitwise(obs.batch.overhead[slot].cpu().numpy(), ref_ov)
+    assert np.array_equal(obs.batch.occupancy[slot].cpu().numpy(), ref_oc)
+    # the other robots' maps are untouched
+    for (e2, a2), s2 in obs.slot.items():
+        if (e2, a2) != (e, a):
+            assert np.array_equal(obs.batch.occupancy[s2].cpu().numpy(), scenes[e2]['occupancy'][a2])
+    moved['overhead'] = sc['overhead'].copy()
+    moved['occupancy'] = sc['occupancy'].copy()
+    moved['overhead'][a], moved['occupancy'][a] = ref_ov, ref_oc
+    st = obs.get_state(awaiting=[[False] * 4, [False] * 4, [k == a for k in range(4)], [False] * 4], numpy=True)
+    g = [gi for gi, grp in enumerate(vector_env.robot_groups(sc)) if a in grp][0]
+    x = st[e][g][vector_env.robot_groups(sc)[g].index(a)]
+    assert _bitwise(x, O.agent_state(moved, a))

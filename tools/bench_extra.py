@@ -98,27 +98,76 @@ def bench_dropin_step(args):
     loop pays per step beside its simulator (the bench line times the kernel alone)."""
     from simaps import vector_env
     scenes = [synthetic.make_scene(args.config, e) for e in range(args.envs)]
+    arrays = batch.descriptor_arrays(scenes)
+    n = sum(len(s['robots']) for s in scenes)
+    for mode in ('scenes', 'arrays'):
+        obs = vector_env.VectorEnvObservations(scenes, layout='chw')
+        if mode == 'scenes':
+            upd = lambda: obs.update(scenes=scenes)  # noqa: E731
+        else:
+            upd = lambda: obs.update_arrays(**arrays)  # noqa: E731
+
+        def step():
+            upd()
+            obs.get_state()
+            torch.cuda.synchronize()
+        for _ in range(5):
+            step()
+        ts, tu, tg = [], [], []
+        for _ in range(max(args.steps, 300)):  # per-step times: the median resists the shared host's noise
+            t0 = time.perf_counter()
+            upd()
+            t1 = time.perf_counter()
+            obs.get_state()
+            t2 = time.perf_counter()
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            ts.append(t3 - t0)
+            tu.append(t1 - t0)
+            tg.append(t2 - t1)
+        dt = float(np.median(ts))
+        print(json.dumps({'row': 'dropin_step', 'update': mode, 'config': args.config, 'stacks_per_step': n,
+                          'ms_per_step': dt * 1e3, 'ms_per_step_mean': float(np.mean(ts)) * 1e3,
+                          'host_update_ms': float(np.median(tu)) * 1e3, 'host_get_state_ms': float(np.median(tg)) * 1e3,
+                          'stacks_per_s_end_to_end': n / dt,
+                          'note': 'update(%s) + get_state() + synchronize, host packing and uploads included; '
+                                  'median of %d steps' % (mode, len(ts))}),
+              flush=True)
+
+
+def bench_remap(args):
+    """The periodic re-map of one moving robot (RobotController.step -> update_map every 200
+    simulation steps, envs.py:1401-1403): a single-frame simaps_ingest, end to end (host prep +
+    upload + launch + synchronize, frame already on the device) and the two kernels alone."""
+    from simaps import vector_env
+    scenes = [synthetic.make_scene(args.config, e) for e in range(args.envs)]
     obs = vector_env.VectorEnvObservations(scenes, layout='chw')
+    db, raw = synthetic.camera_images(scenes[3], 2, 'forward', seed=1)
+    dep, seg = torch.as_tensor(db[None]).cuda(), torch.as_tensor(raw[None]).cuda()
 
     def step():
-        obs.update(scenes=scenes)
-        obs.get_state()
+        obs.update_map([(3, 2)], dep, seg)
         torch.cuda.synchronize()
     for _ in range(5):
         step()
     ts = []
-    for _ in range(max(args.steps, 200)):  # per-step times: the median resists the shared host's noise
+    for _ in range(300):
         t0 = time.perf_counter()
         step()
         ts.append(time.perf_counter() - t0)
-    dt = float(np.median(ts))
-    n = sum(len(s['robots']) for s in scenes)
-    print(json.dumps({'row': 'dropin_step', 'config': args.config, 'stacks_per_step': n,
-                      'ms_per_step': dt * 1e3, 'ms_per_step_mean': float(np.mean(ts)) * 1e3,
-                      'stacks_per_s_end_to_end': n / dt,
-                      'note': 'update(scenes) + get_state() + synchronize, host packing and uploads included; '
-                              'median of %d steps' % len(ts)}),
-          flush=True)
+    prep = obs.batch.prepare_ingest(dep, seg, camera='forward', slots=[obs.slot[(3, 2)]])
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(s)
+    for _ in range(100):
+        obs.batch.launch_ingest(prep)
+    e1.record(s)
+    torch.cuda.synchronize()
+    print(json.dumps({'row': 'remap_one_robot', 'config': args.config, 'frames_per_launch': 1,
+                      'ms_end_to_end': float(np.median(ts)) * 1e3, 'kernel_ms': e0.elapsed_time(e1) / 100,
+                      'note': 'update_map([(env, robot)], frame) + synchronize, median of 300; kernels: HIP events '
+                              'over 100 back-to-back launches'}), flush=True)
 
 
 def bench_ingest(args):
@@ -179,6 +228,7 @@ def bench_ingest(args):
 if __name__ == '__main__':
     if '--dropin-only' in sys.argv:
         bench_dropin_step(argparse.Namespace(config='lifting_4-small_divider', envs=64, steps=50))
+        bench_remap(argparse.Namespace(config='lifting_4-small_divider', envs=64))
         sys.exit(0)
     if '--ingest-only' in sys.argv:
         sys.argv.remove('--ingest-only')
