@@ -40,8 +40,15 @@ class VectorEnvObservations:
     (C, 96, 96) planes (what a conv policy consumes, policies.py:44-45) -- states returned by
     get_state() are always the reference's (96, 96, C) index order (views for 'chw')."""
 
-    def __init__(self, scenes, device='cuda', layout='hwc'):
+    def __init__(self, scenes, device='cuda', layout='hwc', reuse_outputs=0):
+        """reuse_outputs=R > 0: all-robots get_state() renders into a ring of R preallocated output
+        batches and returns a structure of views built once per ring slot (no per-call allocation
+        or per-robot view creation: ~0.2 ms of host time per 256 stacks).  The states of a call are
+        then overwritten R calls later -- copy what must live longer (the reference returns fresh
+        arrays; the default R = 0 keeps that)."""
         self.batch = _batch.StateBatch(scenes, device=device, layout=layout)
+        self._ring = [None] * int(reuse_outputs)
+        self._ring_k = 0
         self.groups = [robot_groups(s) for s in scenes]
         self.slot = {ea: n for n, ea in enumerate(self.batch.agents)}
         self.num_envs = len(scenes)
@@ -84,6 +91,16 @@ class VectorEnvObservations:
         like the reference (one device->host copy for the whole batch); otherwise device tensors."""
         if save_figures:
             raise NotImplementedError('save_figures is a host-side matplotlib debug path (out of scope)')
+        if (all_robots or awaiting is None) and self._ring and not numpy:
+            k = self._ring_k
+            self._ring_k = (k + 1) % len(self._ring)
+            if self._ring[k] is None:
+                buf = self.batch.alloc_state()
+                rows = self.batch.as_hwc(buf).unbind(0)
+                self._ring[k] = (buf, [[[rows[q] for q in g] for g in env] for env in self._all_slots])
+            buf, views = self._ring[k]
+            self.batch.render(out=buf, stream=stream)
+            return views
         if all_robots or awaiting is None:  # every robot: the batch's own agent list, structure precomputed
             out = self.batch.as_hwc(self.batch.render(stream=stream))
             if numpy:

@@ -100,8 +100,8 @@ def bench_dropin_step(args):
     scenes = [synthetic.make_scene(args.config, e) for e in range(args.envs)]
     arrays = batch.descriptor_arrays(scenes)
     n = sum(len(s['robots']) for s in scenes)
-    for mode in ('scenes', 'arrays'):
-        obs = vector_env.VectorEnvObservations(scenes, layout='chw')
+    for mode in ('scenes', 'arrays', 'arrays+ring'):
+        obs = vector_env.VectorEnvObservations(scenes, layout='chw', reuse_outputs=2 if mode == 'arrays+ring' else 0)
         if mode == 'scenes':
             upd = lambda: obs.update(scenes=scenes)  # noqa: E731
         else:
