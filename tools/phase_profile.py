@@ -42,7 +42,11 @@ def main():
     st = st[:b.N].astype(np.int64)
     if args.dump:
         np.save(args.dump, st)
-    us = lambda k1, k0: float(np.median((st[:, k1] - st[:, k0]) / 100.0))  # noqa: E731
+    def us(k1, k0):
+        """median over workgroups of stamp k1 - stamp k0 (us); workgroups that recorded neither are
+        left out, and a pair no workgroup recorded (a phase this build / config skips) is None."""
+        m = (st[:, k1] > 0) & (st[:, k0] > 0)
+        return float(np.median((st[m, k1] - st[m, k0]) / 100.0)) if m.any() else None
     res = {'config': args.config, 'layout': args.layout, 'N': b.N,
            'total_us_median': us(6, 0), 'span_us': float((st[:, 6].max() - st[:, 0].min()) / 100.0),
            'sweep_track_us': {'agent_load': us(43, 0), 'first_ballot': us(46, 43), 'all_ballots': us(47, 46), 'v2_ballots_sync': us(15, 47), 'cspace_loads_ballots': us(15, 0), 'cspace_dilate': us(2, 15), 'cspace': us(2, 0), 'snap': us(48, 2), 'init': us(3, 48), 'rounds': us(49, 3), 'finish': us(50, 49), 'scale': us(7, 50), 'rounds_finish_scale': us(7, 3), 'end': us(7, 0)},
@@ -54,8 +58,10 @@ def main():
            'distance_us': {'values': us(16, 5), 'block_min': us(17, 16), 'stores': us(6, 17), 'all': us(6, 5)},
            'sweep_rounds_us': {'round_%d' % r: us(19 + r, 18 + r) for r in range(3)},
            'wave_sweep_r0_us': {'start': [us(32 + w, 18) for w in range(8)], 'end': [us(24 + w, 18) for w in range(8)]},
-           'clock_mhz_sweep_w0': float(np.median((st[:, 45] - st[:, 44]) / ((st[:, 24] - st[:, 18]) / 100.0))),
-           'dilate_clk_from52': {str(k): float(np.median(st[:, k].astype(np.int64) - st[:, 52].astype(np.int64))) for k in (53, 54, 55, 56, 57, 58, 59)},
+           'clock_mhz_sweep_w0': float(np.median((st[:, 45] - st[:, 44]) / ((st[:, 24] - st[:, 18]) / 100.0)))
+           if (st[:, 45] > 0).any() else None,
+           'dilate_clk_from52': {str(k): float(np.median(st[:, k].astype(np.int64) - st[:, 52].astype(np.int64)))
+                                 for k in (53, 54, 55, 56, 57, 58, 59) if (st[:, k] > 0).any()},
            'spread_us': {name: [float(np.percentile((st[:, k1].astype(np.int64) - st[:, 0].astype(np.int64)) / 100.0, q)) for q in (10, 50, 90, 100)]
                          for name, k1 in (('sweep_end', 7), ('render_end', 8), ('join', 4), ('total', 6))},
            'start_skew_us': float((np.percentile(st[:, 0], 100) - np.percentile(st[:, 0], 0)) / 100.0),
@@ -70,6 +76,8 @@ def main():
     per_wave = np.median(st[:, 64:72].astype(np.float64), axis=0)
     res['sssp_relaxations_per_stack'] = float(sum(n * (w if ((k + 2 * (k >> 2)) & 3) < 2 else h) * 3
                                                   for k, n in enumerate(per_wave)))
+    # drop the phases this build / config never stamped
+    res = {k: ({q: v for q, v in d.items() if v is not None} if isinstance(d, dict) else d) for k, d in res.items()}
     print(json.dumps(res, indent=1))
 
 
