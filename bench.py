@@ -141,6 +141,9 @@ def main():
     ap.add_argument('--cpu-budget', type=float, default=6.0, help='seconds per CPU-baseline leg and worker')
     ap.add_argument('--cpu-procs', type=int, default=0, help='CPU-baseline processes (default: usable cores, capped)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--shared-gpu', action='store_true',
+                    help='rehearsal on a 1-GPU box: every rank renders on cuda:0 and the barriers / reductions go '
+                         'over gloo (RCCL refuses two ranks on one device); NOT a scaling measurement')
     args = ap.parse_args()
 
     import numpy as np
@@ -149,10 +152,14 @@ def main():
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    local = 0 if args.shared_gpu else int(os.environ.get('LOCAL_RANK', '0'))
     torch.cuda.set_device(local)
+    red = 'cpu' if args.shared_gpu else 'cuda'  # device of the timing / counter reductions
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if args.shared_gpu:
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
 
     from simaps import batch, synthetic
     strong = args.total_envs is not None
@@ -175,10 +182,10 @@ def main():
         if k == args.steps - 1:
             ev1.record(stream)
 
-    elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, 'cuda')
-    kern_ms = max_over_ranks([ev0.elapsed_time(ev1) / args.steps], world, 'cuda')[0]
+    elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, red)
+    kern_ms = max_over_ranks([ev0.elapsed_time(ev1) / args.steps], world, red)[0]
 
-    stacks_per_step = int(sum_over_ranks([b.N], world, 'cuda')[0])
+    stacks_per_step = int(sum_over_ranks([b.N], world, red)[0])
     value = stacks_per_step * args.steps / elapsed
     B = algorithmic_bytes_per_stack(b.H, b.W, b.C)
     achieved = B * b.N / (kern_ms * 1e-3) / 1e9
@@ -194,7 +201,9 @@ def main():
                 traffic_src = 'from_profile: profiles/pmc_traffic.json (%s, rocprofv3 PMC passes)' % t.get('tag')
         except (OSError, ValueError):
             traffic = None
-    gather = gather_states(out, args.gather, world, rank) if args.gather and world > 1 else None
+    gather = None
+    if args.gather and world > 1:
+        gather = gather_states(out.cpu() if args.shared_gpu else out, args.gather, world, rank)
 
     if rank == 0:
         res = {
@@ -205,7 +214,8 @@ def main():
             'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic (seeded scenes, SURVEY 8(d))',
             'config': {'workload': args.config, 'agents_per_env': len(scenes[0]['robots']),
                        'stacks_per_step': stacks_per_step, 'grid': '%dx%d' % (b.H, b.W), 'channels': b.C,
-                       'layout': args.layout, 'parallelism': 'env-sharded x%d' % world},
+                       'layout': args.layout,
+                       'parallelism': 'env-sharded x%d' % world + (' (shared-gpu rehearsal, gloo)' if args.shared_gpu else '')},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'traffic_source': traffic_src,
                          'kernel': 'get_state_kernel', 'kernel_ms': kern_ms,
