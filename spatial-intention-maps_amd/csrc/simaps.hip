@@ -2593,100 +2593,123 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         const uint8_t pbits = (uint8_t)((lane + 1) | 0x10);  // a relaxed head: parent edge `lane`, queued
         if (lane == 0) { dist[su] = 0.0f; queue[0] = (uint16_t)su; pin[su] = 0x10; }
         __builtin_amdgcn_wave_barrier();
-        int qh = 0, qt = 1, count = 1, front = su;  // live entries queue[qh .. qt) (mod cells); front == queue[qh]
+        // live entries queue[qh .. qt) (mod cells); front == queue[qh]; second == queue[qh + 1] when
+        // count >= 2 (prefetched one pop ahead, so the SLF front's distance is read in the same round
+        // as the popped vertex's edges instead of after them)
+        int qh = 0, qt = 1, count = 1, front = su, second = su;
         // (the wave's stores below are made by every lane with the same address and value: no exec
         // masking around them)
         lds_float *Ld = (lds_float *)dist;
         lds_u16 *Lq = (lds_u16 *)queue;
         lds_u8 *Li = (lds_u8 *)pin;
         int pops = 0;
-        for (; count > 0 && pops < SIMAPS_POP_CAP; pops++) {  // the cap is never reached by a correct SPFA
-            const int u = front;
+        for (;;) {
+            // (front / second are wave-uniform: keep them in SGPRs across the loop)
+            const int u = __builtin_amdgcn_readfirstlane(front);
             qh = qh + 1 == cells ? 0 : qh + 1;
-            count--;
+            count--;                           // entries queue[qh .. qt) after the pop
+            const int F0 = __builtin_amdgcn_readfirstlane(second);  // the next front (valid if count >= 1)
+            const int q2 = qh + 1 == cells ? 0 : qh + 1;
             const int v = u + doff;
             // one round of reads (in-order LDS sees this wave's earlier writes); the ballots below
-            // consume them together
-            const int nfr = Lq[qh];  // the next front (valid if count > 0)
+            // consume them together.  Lane 8's v is u: its pin read is u's (parent bits to keep).
             const float du = Ld[u], dv = Ld[v];
             const int pv = Li[v];
+            // the front's distance before this pop's relaxations (F0 is a queue entry, < cells, when
+            // count >= 1; otherwise unused, and clamped so the read stays inside the array)
+            const float dF0 = Ld[(unsigned)F0 < (unsigned)cells ? F0 : 0];
+            const int third = Lq[q2];          // queue[qh + 1]: the next pop's second (if count >= 2)
             const float nd = du + wl;
             const bool better = lane < 8 && nd < dv;
             const uint64_t imp = __ballot(better);
             const uint64_t notq = __ballot(!(pv & 0x10));
-            int nf = __builtin_amdgcn_readfirstlane(nfr);
             Li[u] = (uint8_t)(__builtin_amdgcn_readlane(pv, 8) & 0xf);  // u leaves the queue (pyx:92)
+            int nf = F0, nsecond = __builtin_amdgcn_readfirstlane(third);
             if (imp) {
                 if (better) { Ld[v] = nd; Li[v] = pbits; }
                 const uint64_t push = imp & notq;
                 if (push) {
-                    // The pushes of this pop, in edge order, resolved lane-parallel (lanes 0-7 own the
-                    // edges).  pyx:104-111 pushes each at the tail and swaps it with the front if its
-                    // distance is below the front's at that moment, so: the front's distance seen by
-                    // edge k is F0's (lowered by this pop only if F0 is the head of an earlier edge jf <
-                    // k: F0 is queued, so never pushed, but it may be relaxed) until the first push that
-                    // beats it (js); after that it is the running minimum of the pushed distances from
-                    // js on.  A swapping push's slot receives the previous front (F0 or the previous
-                    // swapping push's vertex); the last swapper ends at the front.
+                    // The pushes of this pop, in edge order (pyx:104-111): each goes to the tail and
+                    // swaps with the front if its distance is below the front's at that moment.  The
+                    // front's distance seen by edge k is F0's, lowered by this pop only if F0 is the
+                    // head of an earlier edge jf < k (F0 is queued, so never pushed, but it may be
+                    // relaxed) -- until the first push that beats it (js); from then on it is the
+                    // running minimum of the pushed distances from js on.  A swapping push's slot
+                    // receives the previous front (F0 or the previous swapping push's vertex); the last
+                    // swapper ends at the front.
                     const int np = __popcll(push);
-                    const bool isP = (push >> lane) & 1;
-                    const int rank = __popcll(push & ((1ull << lane) - 1));
-                    uint64_t cand = push;
-                    int F0 = nf, jf = 64;
-                    float dbefore = 0.0f, dafter = 0.0f;
-                    if (count == 0) {  // the queue was empty: the first push becomes the front
+                    const uint64_t fm = count > 0 ? __ballot(lane < 8 && v == F0) : 0ull;
+                    const int jf = fm ? __builtin_ctzll(fm) : 64;
+                    const float dafter = (fm && ((imp >> jf) & 1))
+                                             ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), jf)) : dF0;
+                    if (np == 1 && count > 0) {
+                        // one push (the common case): a scalar decision, no scans
                         const int p1 = __builtin_ctzll(push);
-                        F0 = __builtin_amdgcn_readlane(v, p1);
-                        dbefore = dafter = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), p1));
-                        cand &= cand - 1;
+                        const int vp = __builtin_amdgcn_readlane(v, p1);
+                        const float ndp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), p1));
+                        const bool sw = ndp < (p1 > jf ? dafter : dF0);
+                        const int content = sw ? F0 : vp;
+                        Lq[qt] = (uint16_t)content;
+                        if (sw) { Lq[qh] = (uint16_t)vp; nf = vp; }
+                        if (count == 1) nsecond = content;  // the tail slot was queue[qh + 1]
+                        qt = qt + 1 == cells ? 0 : qt + 1;
+                        count++;
                     } else {
-                        const uint64_t fm = __ballot(lane < 8 && v == nf);
-                        if (fm) {
-                            jf = __builtin_ctzll(fm);
-                            dbefore = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), jf));
-                            dafter = ((imp >> jf) & 1) ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), jf)) : dbefore;
-                        } else {
-                            dbefore = dafter = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(Ld[nf])));
+                        const bool isP = (push >> lane) & 1;
+                        const int rank = __popcll(push & ((1ull << lane) - 1));
+                        uint64_t cand = push;
+                        int Fq = F0;
+                        float dbefore = dF0, dseen = dafter;
+                        if (count == 0) {  // the queue was empty: the first push becomes the front
+                            const int p1 = __builtin_ctzll(push);
+                            Fq = __builtin_amdgcn_readlane(v, p1);
+                            dbefore = dseen = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), p1));
+                            cand &= cand - 1;
                         }
-                    }
-                    const bool isC = (cand >> lane) & 1;
-                    const uint64_t sF0 = __ballot(isC && nd < (lane > jf ? dafter : dbefore));
-                    int content = v, newfront = F0;
-                    if (sF0) {
-                        const int js = __builtin_ctzll(sF0);
-                        // exclusive prefix minimum of nd over the candidate lanes in [js, lane) (DPP
-                        // row shifts: lanes 0-7 lie in one row)
-                        float y = (isC && lane >= js) ? nd : INFINITY;
+                        const bool isC = (cand >> lane) & 1;
+                        const uint64_t sF0 = __ballot(isC && nd < (lane > jf ? dseen : dbefore));
+                        int content = v, newfront = Fq;
+                        if (sF0) {
+                            const int js = __builtin_ctzll(sF0);
+                            // exclusive prefix minimum of nd over the candidate lanes in [js, lane) (DPP
+                            // row shifts: lanes 0-7 lie in one row)
+                            float y = (isC && lane >= js) ? nd : INFINITY;
 #define SPFA_SHR(x, n, old) __builtin_amdgcn_update_dpp((old), (x), 0x110 + (n), 0xf, 0xf, false)
 #define SPFA_SHRF(x, n) __int_as_float(SPFA_SHR(__float_as_int(x), n, (int)INF_BITS))
-                        y = fminf(y, SPFA_SHRF(y, 1));
-                        y = fminf(y, SPFA_SHRF(y, 2));
-                        y = fminf(y, SPFA_SHRF(y, 4));
-                        const float pm = SPFA_SHRF(y, 1);
-                        const bool sw = isC && (lane == js || (lane > js && nd < pm));
-                        const uint64_t swm = __ballot(sw);
-                        // the previous swapper's vertex: exclusive "last valid" scan of v over swappers
-                        int z = sw ? v : -1, zs;
-                        zs = SPFA_SHR(z, 1, -1); z = z >= 0 ? z : zs;
-                        zs = SPFA_SHR(z, 2, -1); z = z >= 0 ? z : zs;
-                        zs = SPFA_SHR(z, 4, -1); z = z >= 0 ? z : zs;
-                        const int prev = SPFA_SHR(z, 1, -1);
+                            y = fminf(y, SPFA_SHRF(y, 1));
+                            y = fminf(y, SPFA_SHRF(y, 2));
+                            y = fminf(y, SPFA_SHRF(y, 4));
+                            const float pm = SPFA_SHRF(y, 1);
+                            const bool sw = isC && (lane == js || (lane > js && nd < pm));
+                            const uint64_t swm = __ballot(sw);
+                            // the previous swapper's vertex: exclusive "last valid" scan of v over swappers
+                            int z = sw ? v : -1, zs;
+                            zs = SPFA_SHR(z, 1, -1); z = z >= 0 ? z : zs;
+                            zs = SPFA_SHR(z, 2, -1); z = z >= 0 ? z : zs;
+                            zs = SPFA_SHR(z, 4, -1); z = z >= 0 ? z : zs;
+                            const int prev = SPFA_SHR(z, 1, -1);
 #undef SPFA_SHRF
 #undef SPFA_SHR
-                        if (sw) content = prev >= 0 ? prev : F0;
-                        newfront = __builtin_amdgcn_readlane(v, 63 - __builtin_clzll(swm));
-                    }
-                    if (isP) {
+                            if (sw) content = prev >= 0 ? prev : Fq;
+                            newfront = __builtin_amdgcn_readlane(v, 63 - __builtin_clzll(swm));
+                        }
                         const int slot = qt + rank < cells ? qt + rank : qt + rank - cells;
-                        Lq[slot] = (uint16_t)content;
+                        if (isP) Lq[slot] = (uint16_t)content;
+                        if (sF0) Lq[qh] = (uint16_t)newfront;  // after the lanes' stores (in the empty case qh is p1's slot)
+                        if (count <= 1) {  // the pushes wrote queue[qh + 1]: the next pop's second
+                            const uint64_t at = __ballot(isP && slot == q2);
+                            if (at) nsecond = __builtin_amdgcn_readlane(content, __builtin_ctzll(at));
+                        }
+                        qt = qt + np < cells ? qt + np : qt + np - cells;
+                        count += np;
+                        nf = newfront;
                     }
-                    if (sF0) Lq[qh] = (uint16_t)newfront;  // after the lanes' stores (in the empty case qh is p1's slot)
-                    qt = qt + np < cells ? qt + np : qt + np - cells;
-                    count += np;
-                    nf = newfront;
                 }
             }
             front = nf;
+            second = nsecond;
+            ++pops;
+            if (count <= 0 || pops >= SIMAPS_POP_CAP) break;  // the cap is never reached by a correct SPFA
         }
         if (lane == 0) {
             STAMP_VAL(7, pops);  // (stamp build: tools/path_profile.py reports ns per pop)

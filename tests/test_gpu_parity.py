@@ -88,10 +88,12 @@ def test_layout_chw_matches_hwc(S):
                                  'lifting_4-large_empty-nonspatial', 'lifting_2_pushing_2-large_empty-all',
                                  'lifting_4-large_doors', 'lifting_4-large_tunnels', 'lifting_4-large_rooms',
                                  'lifting_2_throwing_2-large_doors', 'lifting_4-large_rooms-history'])
-def test_oracle_parity_fresh_seeds(S, cfg):
-    """Seeds never used for the goldens: every agent of 6 envs vs the (golden-pinned) oracle."""
+@pytest.mark.parametrize('rounding', ['fma', 'plain'])
+def test_oracle_parity_fresh_seeds(S, cfg, rounding):
+    """Seeds never used for the goldens: every agent of 6 envs vs the (golden-pinned) oracle, in
+    both host roundings of scipy.ndimage.rotate's out_center (rotate.npz / rotate_plain.npz)."""
     batch, K, synthetic = S
-    scenes = [synthetic.make_scene(cfg, 100 + e) for e in range(6)]
+    scenes = [dict(synthetic.make_scene(cfg, 100 + e), rotate_rounding=rounding) for e in range(6)]
     b = batch.StateBatch(scenes)
     st = b.as_hwc(b.render()).cpu().numpy()
     for n, (e, a) in enumerate(b.agents):

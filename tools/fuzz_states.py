@@ -3,7 +3,11 @@ through the C ABI in one launch per configuration and compared bitwise with the 
 workers in a process pool; the nonspatial intention channels within 1e-7, like the GPU tests).
 Seeds 5000+ are used by no test.  Prints one JSON line per configuration and a total.
 
-    python tools/fuzz_states.py [envs_per_config] [procs] [--perturb]
+    python tools/fuzz_states.py [envs_per_config] [procs] [--perturb] [--plain]
+
+--plain renders and checks with the plain-dgemv rounding of scipy.ndimage.rotate's out_center
+(rotate_plain.npz's host) instead of the FMA one; --perturb also leaves ~10 % of the robots in the
+never-acted state (None waypoints / target / index, idle).
 """
 import json
 import os
@@ -24,7 +28,13 @@ CONFIGS = ['lifting_1-small_empty', 'lifting_4-small_divider', 'pushing_4-large_
 SEED0 = 5000
 
 
-def perturbed_scene(cfg, e, perturb):
+def perturbed_scene(cfg, e, perturb, rounding='fma'):
+    s = _perturbed_scene(cfg, e, perturb)
+    s['rotate_rounding'] = rounding
+    return s
+
+
+def _perturbed_scene(cfg, e, perturb):
     """make_scene(cfg, SEED0 + e); with perturb, robots anywhere in the room but 2 cm from its edge
     (next to walls, on dividers: the snap slow path), headings half the time on exact multiples of
     45 deg (+-pi, -0.0 included), positions half the time on pixel corners, random idle flags, and
@@ -44,6 +54,8 @@ def perturbed_scene(cfg, e, perturb):
         r['heading'] = float(rs.choice([-np.pi, np.pi, -0.0, 0.0, np.pi / 4, -3 * np.pi / 4, np.pi / 2])
                              if rs.rand() < 0.5 else rs.uniform(-np.pi, np.pi))
         r['idle'] = bool(rs.rand() < 0.25)
+        if rs.rand() < 0.1:  # never acted (Robot.__init__ / reset state)
+            r.update(idle=True, waypoint_positions=None, waypoint_index=None, target_ee=None)
     scale = [-0.5, 0.0, 0.25, 3.0][sum(map(ord, cfg)) % 4]
     s['flags'] = dict(s['flags'], shortest_path_map_scale=scale)
     return s
@@ -51,13 +63,14 @@ def perturbed_scene(cfg, e, perturb):
 
 def _oracle(job):
     import oracle as O
-    cfg, e, a, perturb = job
-    return O.agent_state(perturbed_scene(cfg, e, perturb), a)
+    cfg, e, a, perturb, rounding = job
+    return O.agent_state(perturbed_scene(cfg, e, perturb, rounding), a)
 
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith('--')]
     perturb = '--perturb' in sys.argv
+    rounding = 'plain' if '--plain' in sys.argv else 'fma'
     envs = int(args[0]) if len(args) > 0 else 16
     procs = int(args[1]) if len(args) > 1 else 16
     import torch
@@ -67,11 +80,11 @@ def main():
     with get_context('spawn').Pool(procs) as pool:
         for cfg in CONFIGS:
             t0 = time.time()
-            scenes = [perturbed_scene(cfg, e, perturb) for e in range(envs)]
+            scenes = [perturbed_scene(cfg, e, perturb, rounding) for e in range(envs)]
             b = batch.StateBatch(scenes)
             st = b.as_hwc(b.render()).cpu().numpy()
             torch.cuda.synchronize()
-            refs = pool.map(_oracle, [(cfg, e, a, perturb) for e, a in b.agents], chunksize=4)
+            refs = pool.map(_oracle, [(cfg, e, a, perturb, rounding) for e, a in b.agents], chunksize=4)
             nb = 0
             for n, (e, a) in enumerate(b.agents):
                 ns = _nonspatial_slice(scenes[e]['flags'], len(scenes[e]['robots']))
@@ -91,8 +104,9 @@ def main():
             total += len(b.agents)
             bad += nb
             print(json.dumps({'config': cfg, 'stacks': len(b.agents), 'mismatches': nb, 's': round(time.time() - t0, 1),
-                              'perturbed': perturb}), flush=True)
-    print(json.dumps({'total_stacks': total, 'mismatches': bad, 'seeds': [SEED0, SEED0 + envs - 1], 'perturbed': perturb}),
+                              'perturbed': perturb, 'rotate_rounding': rounding}), flush=True)
+    print(json.dumps({'total_stacks': total, 'mismatches': bad, 'seeds': [SEED0, SEED0 + envs - 1], 'perturbed': perturb,
+                      'rotate_rounding': rounding}),
           flush=True)
 
 
