@@ -238,15 +238,6 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
  *   max-reduction that also records each chunk's box of touched map pixels, then one sweep of each
  *   frame's box). */
 
-/* Which ingest kernels simaps_ingest launches (host-side, process-wide; returns the previous mode):
- *   0 automatic: per-frame workgroups (one 1024-thread workgroup reduces a whole frame in an LDS hash
- *     table and writes the winners itself) for N >= SIMAPS_INGEST_FRAME_MIN frames -- throughput --
- *     and the two-kernel point-chunk path below that -- latency (a frame spread over ~22 CUs);
- *   1 point chunks always; 2 per-frame always (camera heights <= 1024; otherwise point chunks).
- * Both give the same maps bit for bit. */
-#define SIMAPS_INGEST_FRAME_MIN 128
-int simaps_ingest_mode(int mode);
-
 /* Point-pass chunks (2048 camera pixels each) per frame of an Hc x Wc camera: the boxes scratch of
  *   simaps_ingest holds 4 uint32 per chunk and frame.  SIMAPS_EINVAL for a non-positive size. */
 int simaps_ingest_chunks(int height_px, int width_px);

@@ -3243,148 +3243,6 @@ __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
     }
 }
 
-
-// ------------------------------------------------------------------------------------------------
-// Per-frame ingest (round 3): ONE 1024-thread workgroup per frame reduces all of the frame's points
-// in an LDS hash table of (map pixel -> key) -- a forward frame touches ~4-5 k distinct map pixels
-// (an overhead frame ~11 k) -- and writes the winners' overhead values itself: no global key map
-// traffic, no box / resolve pass.  A pixel whose probe sequence finds no free slot (table full:
-// overhead frames) goes to the global key map instead, entirely (slots only ever go from free to
-// owned, so every point of that pixel sees the same full sequence), and is resolved at the end from
-// a list of such pixels.  Rounds of INGF_WG * 8 points, the next round's loads in flight while the
-// current one is reduced.  Same keys, same winners as the chunked kernels (max key per pixel).
-// ------------------------------------------------------------------------------------------------
-constexpr int INGF_WG = 1024, INGF_ROUND = INGF_WG * INGEST_PPT;
-constexpr int INGF_HS = 8192;      // hash slots: u64 key + i32 pixel tag (96 KB)
-constexpr int INGF_PROBES = 16;    // linear-probe limit before the global key map
-constexpr int INGF_LIST = 4096;    // pixels resolved from the global key map (overflow: full sweep)
-constexpr int INGF_MAX_HC = 1024;  // camera rows (pixel_y table)
-
-__device__ __forceinline__ unsigned ingf_hash(int pix) { return ((unsigned)pix * 0x9E3779B1u) >> (32 - 13); }
-static_assert(INGF_HS == 1 << 13, "hash width");
-
-// grid (frames)
-__global__ void __launch_bounds__(INGF_WG) ingest_frame_kernel(
-    simaps_config cfg, simaps_camera cam, const simaps_agent *__restrict__ agents,
-    const simaps_seg_ids *__restrict__ seg_ids, const double *__restrict__ cam_params,
-    const float *__restrict__ depth, const int32_t *__restrict__ seg_raw, float *__restrict__ overhead,
-    uint8_t *__restrict__ occupancy, unsigned long long *__restrict__ keys)
-{
-    __shared__ unsigned long long hk[INGF_HS];
-    __shared__ int ht[INGF_HS];
-    __shared__ float F[12], pxT[INGEST_MAX_WC], pyT[INGF_MAX_HC];
-    __shared__ int glist[INGF_LIST];
-    __shared__ int gcount;
-    const int n = blockIdx.x, tid = threadIdx.x;
-    const int H = cfg.H, W = cfg.W, Hc = cam.height_px, Wc = cam.width_px, NP = Hc * Wc;
-    const float *db = depth + (size_t)n * NP;
-    const int32_t *raw = seg_raw + (size_t)n * NP;
-    float dv[INGEST_PPT], dn[INGEST_PPT] = {};
-    int rv[INGEST_PPT], rn[INGEST_PPT] = {};
-    ingest_load(db, raw, tid * INGEST_PPT, NP, dv, rv);  // round 0 first: the tables hide its latency
-    const simaps_agent ag = agents[n];
-    const simaps_seg_ids ids = seg_ids[ag.env];
-    const float c1 = (float)(cam.far_m * cam.near_m), cfar = (float)cam.far_m, cfn = (float)(cam.far_m - cam.near_m);
-    const float cx2 = (float)cam.cx2, cy2 = (float)cam.cy2;
-    if (tid == 0) {
-        camera_frame(cam_params + 9 * (size_t)n, F);
-        gcount = 0;
-    }
-    for (int j = tid; j < Wc; j += INGF_WG) pxT[j] = cx2 * ((float)j / (float)Wc - 0.5f);
-    for (int i = tid; i < Hc; i += INGF_WG) pyT[i] = cy2 * (0.5f - ((float)i + 1.0f) / (float)Hc);
-    for (int e = tid; e < INGF_HS; e += INGF_WG) ht[e] = -1, hk[e] = 0ull;
-    const float h2 = (float)((double)H / 2), w2 = (float)((double)W / 2);
-    const size_t base = (size_t)ag.map_slot * H * W;
-    __syncthreads();
-    for (int r0 = 0; r0 < NP; r0 += INGF_ROUND) {
-        const int k0 = r0 + tid * INGEST_PPT;
-        if (r0 + INGF_ROUND < NP) ingest_load(db, raw, k0 + INGF_ROUND, NP, dn, rn);
-        int pix[INGEST_PPT];
-        unsigned long long key[INGEST_PPT];
-        int i = k0 / Wc, j = k0 - i * Wc;
-#pragma unroll
-        for (int q = 0; q < INGEST_PPT; q++, j = (j + 1 == Wc) ? (i++, 0) : j + 1) {
-            const int k = k0 + q;
-            pix[q] = -1;
-            key[q] = 0ull;
-            if (k >= NP) continue;
-            const float dep = c1 / (cfar - cfn * dv[q]);
-            const float px = pxT[j], py = pyT[i];
-            float p[3];
-            for (int cc = 0; cc < 3; cc++) {
-                float t = F[3 + cc] + px * F[9 + cc];
-                t = t + py * F[6 + cc];
-                p[cc] = F[cc] + dep * t;
-            }
-            const int r = rv[q];
-            float seg = 0.125f * (r == 0 ? 1.0f : 0.0f);
-            seg += 0.25f * ((r >= ids.min_obstacle && r <= ids.max_obstacle) ? 1.0f : 0.0f);
-            if (ids.has_receptacle) seg += 0.375f * (r == ids.receptacle ? 1.0f : 0.0f);
-            seg += 0.5f * ((r >= ids.min_cube && r <= ids.max_cube) ? 1.0f : 0.0f);
-            int pi = np_f32_to_i32(floorf(h2 - p[1] * 96.0f)), pj = np_f32_to_i32(floorf(w2 + p[0] * 96.0f));
-            pi = pi < 0 ? 0 : (pi > H - 1 ? H - 1 : pi);
-            pj = pj < 0 ? 0 : (pj > W - 1 ? W - 1 : pj);
-            pix[q] = pi * W + pj;
-            if (seg == 0.25f) occupancy[base + pix[q]] = 1;  // np.isclose(seg, obstacle) (seg values are exact)
-            const unsigned zb = __float_as_uint(p[2]);
-            const unsigned zk = p[2] != p[2] ? 0xffffffffu : ((zb & 0x80000000u) ? ~zb : (zb | 0x80000000u));
-            key[q] = ((unsigned long long)zk << 32) | (((unsigned)(k + 1) << 4) | (unsigned)(seg * 8.0f));
-        }
-        // runs of one map pixel inside the lane: the run's last entry carries the run's max key
-#pragma unroll
-        for (int q = 1; q < INGEST_PPT; q++)
-            if (pix[q] == pix[q - 1] && pix[q] >= 0) {
-                key[q] = key[q] > key[q - 1] ? key[q] : key[q - 1];
-                pix[q - 1] = -1;
-            }
-#pragma unroll
-        for (int q = 0; q < INGEST_PPT; q++) {
-            const int px_ = pix[q];
-            if (px_ < 0) continue;
-            unsigned h = ingf_hash(px_);
-            bool done = false;
-            for (int pr = 0; pr < INGF_PROBES && !done; pr++, h = (h + 1) & (INGF_HS - 1)) {
-                int t = ht[h];
-                if (t == -1) t = atomicCAS(&ht[h], -1, px_), t = t == -1 ? px_ : t;
-                if (t == px_) {
-                    atomicMax(&hk[h], key[q]);
-                    done = true;
-                }
-            }
-            if (!done) {  // no slot: this pixel lives in the global key map (zero on entry)
-                if (atomicMax(&keys[base + px_], key[q]) == 0ull) {
-                    const int s = atomicAdd(&gcount, 1);
-                    if (s < INGF_LIST) glist[s] = px_;
-                }
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < INGEST_PPT; q++) dv[q] = dn[q], rv[q] = rn[q];
-    }
-    __syncthreads();  // (also waits for this workgroup's global atomics: vmcnt(0) before the barrier)
-    // the winners: overhead = seg code / 8 (Mapper.update's last write after the argsort by z)
-    for (int e = tid; e < INGF_HS; e += INGF_WG) {
-        const int p = ht[e];
-        if (p >= 0) overhead[base + p] = (float)(hk[e] & 15ull) * 0.125f;
-    }
-    const int ng = gcount;
-    if (ng <= INGF_LIST) {
-        for (int e = tid; e < ng; e += INGF_WG) {
-            const int p = glist[e];
-            const unsigned long long kv = atomicExch(&keys[base + p], 0ull);  // read and re-zero
-            overhead[base + p] = (float)(kv & 15ull) * 0.125f;
-        }
-    } else {  // list overflow: sweep the frame's whole key map
-        for (int p = tid; p < H * W; p += INGF_WG) {
-            const unsigned long long kv = __hip_atomic_load(&keys[base + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (kv) {
-                atomicExch(&keys[base + p], 0ull);
-                overhead[base + p] = (float)(kv & 15ull) * 0.125f;
-            }
-        }
-    }
-}
-
 }  // namespace
 
 // =================================================================================================
@@ -3394,12 +3252,10 @@ __global__ void __launch_bounds__(INGF_WG) ingest_frame_kernel(
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
-#include <atomic>
 #include <mutex>
 
 namespace {
 thread_local char g_err[512] = "";
-std::atomic<int> g_ingest_mode{0};  // simaps_ingest_mode
 
 int fail(int code, const char *fmt, ...)
 {
@@ -3685,12 +3541,6 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
     return 0;
 }
 
-int simaps_ingest_mode(int mode)
-{
-    if (mode < 0 || mode > 2) return fail(SIMAPS_EINVAL, "ingest mode %d not in 0..2", mode);
-    return g_ingest_mode.exchange(mode);
-}
-
 int simaps_ingest_chunks(int height_px, int width_px)
 {
     if (height_px <= 0 || width_px <= 0) return fail(SIMAPS_EINVAL, "bad camera size");
@@ -3716,14 +3566,6 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
     if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d frames per launch (grid y <= 65535)", N);
     const int nch = ingest_chunks(cam->height_px, cam->width_px);  // point-pass chunks per frame
     if ((rc = pending_faults())) return rc;  // (after the argument checks: they need no device)
-    const int mode = g_ingest_mode.load();
-    if ((mode == 2 || (mode == 0 && N >= SIMAPS_INGEST_FRAME_MIN)) && cam->height_px <= INGF_MAX_HC) {
-        hipLaunchKernelGGL(ingest_frame_kernel, dim3(N), dim3(INGF_WG), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids,
-                           cam_params, depth, seg_raw, overhead, occupancy, reinterpret_cast<unsigned long long *>(keys));
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return fail(SIMAPS_EHIP, "ingest launch: %s", hipGetErrorString(e));
-        return 0;
-    }
     hipLaunchKernelGGL(ingest_points_kernel, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids,
                        cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes);
     hipLaunchKernelGGL(ingest_resolve_kernel, dim3(INGEST_RES_G, N), dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg, agents, overhead,

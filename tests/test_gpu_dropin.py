@@ -221,7 +221,7 @@ def test_maze_paths_reference_goldens(V):
     assert longest == int(z['longest_path']) >= 5
 
 
-def test_ingest_reference_goldens(V, ingest_mode):
+def test_ingest_reference_goldens(V):
     """Observation ingest through simaps_ingest vs the reference's own
     Mapper.update on the committed frames (forward-facing and overhead cameras)."""
     synthetic, vector_env = V
@@ -240,17 +240,8 @@ def test_ingest_reference_goldens(V, ingest_mode):
         assert int(b._keys.abs().sum()) == 0          # scratch left zeroed
 
 
-@pytest.fixture(params=[1, 2], ids=['chunks', 'per_frame'])
-def ingest_mode(request):
-    """Both ingest kernel paths (include/simaps.h simaps_ingest_mode): 1 point chunks, 2 per-frame."""
-    from simaps import _lib
-    prev = _lib.lib.simaps_ingest_mode(request.param)
-    yield request.param
-    _lib.lib.simaps_ingest_mode(prev)
-
-
 @pytest.mark.parametrize('kind', ['forward', 'overhead'])
-def test_ingest_then_get_state_vs_oracle(V, kind, ingest_mode):
+def test_ingest_then_get_state_vs_oracle(V, kind):
     """update_map + get_state end to end on the device vs the oracle (fresh frames; z ties resolved
     as 'later camera pixel wins' on both sides)."""
     synthetic, vector_env = V
@@ -273,7 +264,7 @@ def test_ingest_then_get_state_vs_oracle(V, kind, ingest_mode):
         assert _bitwise(st[n], O.agent_state(s, a)), (e, a)
 
 
-def test_ingest_full_size_two_frames_vs_oracle(V, ingest_mode):
+def test_ingest_full_size_two_frames_vs_oracle(V):
     """The BASELINE launch size (64 envs x 4 agents = 256 frames, 22 point chunks each) ingested
     twice in a row (the second frame lands on the first's maps): every agent's overhead / occupancy
     bitwise vs the oracle, and the key scratch back to zero after each launch."""
@@ -587,36 +578,3 @@ def test_periodic_remap_successive_frames(V):
     g = [gi for gi, grp in enumerate(vector_env.robot_groups(sc)) if a in grp][0]
     x = st[e][g][vector_env.robot_groups(sc)[g].index(a)]
     assert _bitwise(x, O.agent_state(moved, a))
-
-
-def test_ingest_per_frame_table_overflow_vs_oracle(V):
-    """Frames whose points spread over most of the map (random depths: ~25 k distinct map pixels
-    per 43 k-point frame, past the per-frame kernel's 8,192 LDS slots AND its 4,096-entry list of
-    global-map pixels): the per-frame path's probe-limit fallback and the list-overflow sweep give
-    the same maps as the point-chunk path and the oracle, and leave the key scratch zeroed."""
-    synthetic, vector_env = V
-    from simaps import _lib, batch, camera
-    scenes = [synthetic.make_scene('pushing_4-large_empty', 230 + e) for e in range(3)]
-    spec = camera.CAMERAS['forward']
-    rs = np.random.RandomState(11)
-    n = 4
-    depth = rs.uniform(0.0, 1.0, (n, spec.height_px, spec.width_px)).astype(np.float32)
-    seg = rs.choice(np.array([-1, 0, 1, 2, 3, 4, 99], np.int32), size=depth.shape)
-    maps = {}
-    for mode in (1, 2):
-        prev = _lib.lib.simaps_ingest_mode(mode)
-        try:
-            b = batch.StateBatch(scenes)
-            b.ingest(depth, seg, camera='forward', slots=[0, 3, 5, 10])
-            maps[mode] = (b.overhead.cpu().numpy(), b.occupancy.cpu().numpy())
-            assert int(b._keys.abs().sum()) == 0
-        finally:
-            _lib.lib.simaps_ingest_mode(prev)
-    assert _bitwise(maps[1][0], maps[2][0]) and np.array_equal(maps[1][1], maps[2][1])
-    for q, k in enumerate([0, 3, 5, 10]):
-        e, a = b.agents[k]
-        s, r = scenes[e], scenes[e]['robots'][a]
-        ov, oc = s['overhead'][a].copy(), s['occupancy'][a].copy()
-        O.ingest(ov, oc, depth[q], seg[q], spec.params(r['position'][0], r['position'][1], r['heading']), spec,
-                 synthetic.SEG_IDS, s['receptacle_position'] is not None)
-        assert _bitwise(maps[2][0][k], ov) and np.array_equal(maps[2][1][k], oc), k

@@ -3,10 +3,7 @@
 overhead / occupancy maps are compared bitwise with the CPU oracle's Mapper.update + obstacle
 scatter (process pool; z ties resolved 'later camera pixel wins' on both sides, as in the tests).
 
-    python tools/fuzz_ingest.py [envs_per_config] [procs] [--mode 0|1|2]
-
---mode: simaps_ingest_mode (0 automatic: per-frame workgroups from 128 frames; 1 point chunks;
-2 per-frame).
+    python tools/fuzz_ingest.py [envs_per_config] [procs]
 """
 import json
 import os
@@ -38,16 +35,9 @@ def _oracle(job):
 
 
 def main():
-    argv = list(sys.argv[1:])
-    mode = 0
-    if '--mode' in argv:
-        k = argv.index('--mode')
-        mode = int(argv[k + 1])
-        del argv[k:k + 2]
-    envs = int(argv[0]) if len(argv) > 0 else 16
-    procs = int(argv[1]) if len(argv) > 1 else 16
-    from simaps import _lib, batch, synthetic
-    _lib.lib.simaps_ingest_mode(mode)
+    envs = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    procs = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+    from simaps import batch, synthetic
     tot = {'frames': 0, 'mismatches': 0}
     with get_context('spawn').Pool(procs) as pool:
         for cfg, kind in CASES:
@@ -68,7 +58,6 @@ def main():
                               'maps_changed': changed, 'keys_zero_after': keys_zero, 's': round(time.time() - t0, 1)}),
                   flush=True)
     tot['seeds'] = [SEED0, SEED0 + envs - 1]
-    tot['ingest_mode'] = mode
     print(json.dumps(tot), flush=True)
 
 
