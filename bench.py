@@ -61,39 +61,40 @@ def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu'):
     the job time).  step(k) runs step k (k < 0 for warmup); sync() waits for the device."""
     import torch
     import torch.distributed as dist
+    coll = world > 1 or (dist.is_available() and dist.is_initialized())  # (--init-dist: one rank, real collectives)
     for k in range(warmup):
         step(-1 - k)
     sync()
-    if world > 1:
+    if coll:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     for k in range(steps):
         step(k)
     sync()
-    if world > 1:
+    if coll:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     return max_over_ranks([elapsed], world, reduce_device)[0]
 
 
 def max_over_ranks(values, world, device='cpu'):
-    """Element-wise max of per-rank floats (identity for world == 1)."""
-    if world == 1:
+    """Element-wise max of per-rank floats (identity for world == 1 without a process group)."""
+    import torch.distributed as dist
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return list(values)
     import torch
-    import torch.distributed as dist
     t = torch.tensor(values, dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t.cpu()]
 
 
 def sum_over_ranks(values, world, device='cpu'):
-    """Element-wise sum of per-rank numbers (identity for world == 1)."""
-    if world == 1:
+    """Element-wise sum of per-rank numbers (identity for world == 1 without a process group)."""
+    import torch.distributed as dist
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return list(values)
     import torch
-    import torch.distributed as dist
     t = torch.tensor(values, dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(x) for x in t.cpu()]
@@ -141,6 +142,9 @@ def main():
     ap.add_argument('--cpu-budget', type=float, default=6.0, help='seconds per CPU-baseline leg and worker')
     ap.add_argument('--cpu-procs', type=int, default=0, help='CPU-baseline processes (default: usable cores, capped)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--init-dist', action='store_true',
+                    help='initialise the process group even for one rank (exercises the RCCL init / barrier / '
+                         'all_reduce path on a 1-GPU box)')
     ap.add_argument('--shared-gpu', action='store_true',
                     help='rehearsal on a 1-GPU box: every rank renders on cuda:0 and the barriers / reductions go '
                          'over gloo (RCCL refuses two ranks on one device); NOT a scaling measurement')
@@ -155,7 +159,8 @@ def main():
     local = 0 if args.shared_gpu else int(os.environ.get('LOCAL_RANK', '0'))
     torch.cuda.set_device(local)
     red = 'cpu' if args.shared_gpu else 'cuda'  # device of the timing / counter reductions
-    if world > 1:
+    dist_on = world > 1 or args.init_dist
+    if dist_on:
         if args.shared_gpu:
             dist.init_process_group('gloo')
         else:
@@ -227,7 +232,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_budget, args.cpu_procs)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 
