@@ -2620,9 +2620,10 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
             const float dF0 = Ld[(unsigned)F0 < (unsigned)cells ? F0 : 0];
             const int third = Lq[q2];          // queue[qh + 1]: the next pop's second (if count >= 2)
             const float nd = du + wl;
-            const bool better = lane < 8 && nd < dv;
-            const uint64_t imp = __ballot(better);
-            const uint64_t notq = __ballot(!(pv & 0x10));
+            // (lanes >= 8: v = u, so nd = du + 1 > dv: never `better`; no lane test needed)
+            const bool better = nd < dv;
+            const uint64_t imp = __builtin_amdgcn_ballot_w64(better);
+            const uint64_t notq = __builtin_amdgcn_ballot_w64(!(pv & 0x10));
             Li[u] = (uint8_t)(__builtin_amdgcn_readlane(pv, 8) & 0xf);  // u leaves the queue (pyx:92)
             int nf = F0, nsecond = __builtin_amdgcn_readfirstlane(third);
             if (imp) {
@@ -2638,10 +2639,12 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     // receives the previous front (F0 or the previous swapping push's vertex); the last
                     // swapper ends at the front.
                     const int np = __popcll(push);
-                    const uint64_t fm = count > 0 ? __ballot(lane < 8 && v == F0) : 0ull;
-                    const int jf = fm ? __builtin_ctzll(fm) : 64;
-                    const float dafter = (fm && ((imp >> jf) & 1))
-                                             ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), jf)) : dF0;
+                    // F0 as the head of an edge this pop IMPROVED (lane jf): only then does its
+                    // distance change for the later edges.  (Lanes >= 8 have v = u != F0 and never
+                    // improve; with an empty queue F0 is stale, but that case ignores jf.)
+                    const uint64_t fmi = __builtin_amdgcn_ballot_w64(v == F0) & imp;
+                    const int jf = fmi ? __builtin_ctzll(fmi) : 64;
+                    const float dafter = fmi ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), jf)) : dF0;
                     if (np == 1 && count > 0) {
                         // one push (the common case): a scalar decision, no scans
                         const int p1 = __builtin_ctzll(push);
