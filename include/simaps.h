@@ -225,6 +225,14 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
                          const simaps_robot *robots, const uint8_t *occupancy, const double *sources,
                          const double *targets, int max_points, double *out_xy, int32_t *out_count, void *stream);
 
+/* Which path kernels simaps_shortest_path / simaps_grid_path launch (host-side, process-wide; returns
+ * the previous mode): 0 automatic, 1 compact (the SPFA runs to an empty queue; more queries per CU),
+ * 2 early exit (the SSSP fixpoint by directional sweeps first, then the SPFA only until every vertex of
+ * the target's parent chain has its final distance -- whose parent then can no longer change).  Both
+ * return the reference's waypoints exactly.  Automatic takes the early exit while all queries of the
+ * launch fit on the device at once. */
+int simaps_path_mode(int mode);
+
 /* Batched observation ingest into the per-agent maps (occupancy / overhead [M, H, W], slot
  *   agents[n].map_slot), from depth [N][Hc][Wc] float32 (pybullet depth buffer) and seg_raw
  *   [N][Hc][Wc] int32 (body ids), cam_params [N][9] fp64 = _get_camera_params(robot pose)

@@ -2520,18 +2520,24 @@ struct PathHdr {
     int src_q[2][2], src_s[2][2], src_ok[2];
     int flag[2];
     int nseg;
-    unsigned fault;  // SIMAPS_FAULT_* bits of this query
+    unsigned fault;        // SIMAPS_FAULT_* bits of this query
+    int changed[3];        // (EARLY) per-round "a sweep improved a cell" flags
+    uint64_t dirty[4][2];  // (EARLY) per sweep direction: lines to relax again
 };
 constexpr int OFF_PS = align16((int)sizeof(PathHdr));
 constexpr int OFF_PA = OFF_PS + align16((int)(offsetof(SsspScratch, dtab) + sizeof(B128) * MAX_WIN_ROWS));
-template <int CELLS>
+// EARLY: + the SSSP fixpoint `fin` f32 [CELLS] (the get_state sweeps from the snapped source), for the
+// SPFA's early exit (path_core)
+template <int CELLS, bool EARLY>
 constexpr int path_lds_bytes()
 {
-    return align16(OFF_PA + 7 * CELLS > OFF_PS + (int)sizeof(SsspScratch) ? OFF_PA + 7 * CELLS
-                                                                           : OFF_PS + (int)sizeof(SsspScratch));
+    return align16(OFF_PA + (EARLY ? 11 : 7) * CELLS > OFF_PS + (int)sizeof(SsspScratch)
+                       ? OFF_PA + (EARLY ? 11 : 7) * CELLS : OFF_PS + (int)sizeof(SsspScratch));
 }
-static_assert(path_lds_bytes<PATH_SMALL_CELLS>() * 4 <= 160 * 1024, "4 small-room queries per CU");
-static_assert(path_lds_bytes<SIMAPS_MAX_ROOM_CELLS>() * 2 <= 160 * 1024, "2 queries per CU at the room limit");
+static_assert(path_lds_bytes<PATH_SMALL_CELLS, false>() * 4 <= 160 * 1024, "4 small-room queries per CU");
+static_assert(path_lds_bytes<SIMAPS_MAX_ROOM_CELLS, false>() * 2 <= 160 * 1024, "2 queries per CU at the room limit");
+static_assert(path_lds_bytes<PATH_SMALL_CELLS, true>() * 2 <= 160 * 1024, "2 small-room early-exit queries per CU");
+static_assert(path_lds_bytes<SIMAPS_MAX_ROOM_CELLS, true>() <= 160 * 1024, "early-exit query at the room limit");
 static_assert(MAX_ROWS <= 256 && SIMAPS_MAX_ROOM_W <= 256, "rect cells pack as (row << 8) | col");
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
@@ -2551,11 +2557,12 @@ __device__ __forceinline__ int dir_off(int k, int pw)
 // approximate_polygon and the line-of-sight pruning on `line_mask`.  Leaves the kept waypoints in
 // outp[0, cnt) (u16 rect cells (row << 8) | col, target first, i.e. before pyx:152's reversal) and
 // returns cnt in wave 0.  All PNT threads call it.
-template <int CELLS>
+template <int CELLS, bool EARLY>
 __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr, int H, int W, bool run_spfa,
                                          int line_mask, const uint16_t *&outp_ret)
 {
     float *dist = reinterpret_cast<float *>(arr);
+    float *fin = reinterpret_cast<float *>(arr + 7 * CELLS);  // (EARLY only)
     uint16_t *queue = reinterpret_cast<uint16_t *>(arr + 4 * CELLS);
     uint8_t *pin = reinterpret_cast<uint8_t *>(arr + 6 * CELLS);
     // after the parent walk: dense path (u16 rect cells) in the queue region, chain flags in pin,
@@ -2583,10 +2590,35 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         const bool fr = rr >= 1 && rr <= h && cc >= 1 && cc <= w && b_test(S.freeb[rr - 1], cc - 1);
         dist[k] = fr ? INFR : -INFINITY;
         pin[k] = 0;
+        if (EARLY) fin[k] = fr ? INFINITY : -INFINITY;
     }
-    lds_barrier();
     const int su = (sh.src_s[0][0] - sh.i0 + 1) * pw + (sh.src_s[0][1] - sh.j0 + 1);
     const int tv = (sh.src_s[1][0] - sh.i0 + 1) * pw + (sh.src_s[1][1] - sh.j0 + 1);
+    if (EARLY && tid < 8) {  // only the source's row / column is dirty (all else is +-inf)
+        const int d2 = tid >> 1, word = tid & 1;
+        const int bit = d2 < 2 ? sh.src_s[0][0] - sh.i0 : sh.src_s[0][1] - sh.j0;
+        sh.dirty[d2][word] = (bit >> 6) == word ? 1ull << (bit & 63) : 0ull;
+        if (tid < 3) sh.changed[tid] = 0;
+    }
+    lds_barrier();
+    if (EARLY && run_spfa) {
+        // The f32 fixpoint of the graph from the source -- the SPFA's final distances, bitwise (SURVEY
+        // a10) -- by the get_state sweeps, one direction per wave, rounds until nothing improves.
+        // A vertex whose SPFA distance already equals it can never improve again, so its parent is
+        // final: the SPFA below may stop as soon as the target's whole parent chain is final.
+        if (tid == 0) fin[su] = 0.0f;
+        lds_barrier();
+        const int wave = tid >> 6;
+        int steps = 0, round = 0;
+        for (;; round++) {
+            if (tid == 0) sh.changed[(round + 1) % 3] = 0;
+            if (sweep(fin, h, w, pw, wave, sh.dirty, steps) && lane == 0) sh.changed[round % 3] = 1;
+            lds_barrier();
+            if (!sh.changed[round % 3] || round >= h * w + 16) break;
+        }
+        if (tid == 0 && round >= h * w + 16) sh.fault |= SIMAPS_FAULT_ROUNDS;
+        if (tid == 0) STAMP_VAL(8, round + 1);
+    }
     if (tid < 64 && run_spfa) {
         const int doff = lane < 8 ? dir_off(lane, pw) : 0;
         const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
@@ -2602,7 +2634,10 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         lds_float *Ld = (lds_float *)dist;
         lds_u16 *Lq = (lds_u16 *)queue;
         lds_u8 *Li = (lds_u8 *)pin;
-        int pops = 0;
+        int pops = 0, next_check = 0;
+        bool early = false;
+        lds_float *Lfin = (lds_float *)fin;
+        const float finT = EARLY ? fin[tv] : 0.0f;  // the target's fixpoint distance
         for (;;) {
             // (front / second are wave-uniform: keep them in SGPRs across the loop)
             const int u = __builtin_amdgcn_readfirstlane(front);
@@ -2619,6 +2654,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
             // count >= 1; otherwise unused, and clamped so the read stays inside the array)
             const float dF0 = Ld[(unsigned)F0 < (unsigned)cells ? F0 : 0];
             const int third = Lq[q2];          // queue[qh + 1]: the next pop's second (if count >= 2)
+            const float dT = EARLY ? Ld[tv] : 0.0f;  // (EARLY) the target's distance before this pop
             const float nd = du + wl;
             // (lanes >= 8: v = u, so nd = du + 1 > dv: never `better`; no lane test needed)
             const bool better = nd < dv;
@@ -2713,10 +2749,26 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
             second = nsecond;
             ++pops;
             if (count <= 0 || pops >= SIMAPS_POP_CAP) break;  // the cap is never reached by a correct SPFA
+            if (EARLY && dT == finT && pops >= next_check) {
+                // early exit: is every vertex of the target's parent chain at its final distance?
+                // (one LDS round per chain step: the parent's distance, fixpoint and parent bits)
+                int v = tv, pv = Li[tv];
+                bool ok = true;
+                for (int st = 0; v != su; st++) {
+                    const int pd = pv & 0xf;
+                    if (!pd || st >= cells) { ok = false; break; }
+                    v -= __builtin_amdgcn_readlane(doff, pd - 1);
+                    const float a = Ld[v], b = Lfin[v];
+                    pv = Li[v];
+                    if (a != b) { ok = false; break; }
+                }
+                if (ok) { early = true; break; }
+                next_check = pops + 64;  // not yet: look again a little later
+            }
         }
         if (lane == 0) {
-            STAMP_VAL(7, pops);  // (stamp build: tools/path_profile.py reports ns per pop)
-            if (count > 0) sh.fault |= SIMAPS_FAULT_ROUNDS;  // the pop cap stopped a live queue
+            STAMP_VAL(7, pops);  // (stamp build: tools/path_bench.py reports ns per pop)
+            if (count > 0 && !early) sh.fault |= SIMAPS_FAULT_ROUNDS;  // the pop cap stopped a live queue
         }
     }
     lds_barrier();
@@ -2820,7 +2872,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
     return 0;
 }
 
-template <int CELLS>
+template <int CELLS, bool EARLY>
 __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents,
                                                    const simaps_env *__restrict__ envs,
                                                    const simaps_robot *__restrict__ robots,
@@ -2829,7 +2881,7 @@ __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry g
                                                    int max_pts, double *__restrict__ out_xy, int *__restrict__ out_n,
                                                    unsigned *fault)
 {
-    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS>()];
+    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS, EARLY>()];
     PathHdr &sh = *reinterpret_cast<PathHdr *>(smem);
     SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_PS);
     const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -2872,7 +2924,7 @@ __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry g
     if (tid == 0) STAMP_NB(1);
     snap_sources(sh, S, 2, g);
     const uint16_t *outp;
-    const int cnt = path_core<CELLS>(sh, S, smem + OFF_PA, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE, outp);
+    const int cnt = path_core<CELLS, EARLY>(sh, S, smem + OFF_PA, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE, outp);
     if (tid < 64) {
         // (7) positions (envs.py:2494-2503); path[0] / path[-1] replaced by the given positions
         if (cnt < 2) {
@@ -2898,14 +2950,14 @@ __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry g
 // workgroup per (grid, source, target): the same exact SPFA / parent walk / approximate_polygon as
 // path_kernel, without the cspace, snap and straight-line steps of OccupancyMap.shortest_path, the
 // line-of-sight pruning on the grid itself, and the waypoints returned as cells (target last).
-template <int CELLS>
+template <int CELLS, bool EARLY>
 __global__ void __launch_bounds__(PNT) grid_path_kernel(int H, int W, const uint8_t *__restrict__ grids,
                                                         const int32_t *__restrict__ sources,
                                                         const int32_t *__restrict__ targets, int wi0, int wj0, int wh,
                                                         int ww, int max_pts, int32_t *__restrict__ out_ij,
                                                         int32_t *__restrict__ out_n, unsigned *fault)
 {
-    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS>()];
+    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS, EARLY>()];
     PathHdr &sh = *reinterpret_cast<PathHdr *>(smem);
     SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_PS);
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2939,7 +2991,7 @@ __global__ void __launch_bounds__(PNT) grid_path_kernel(int H, int W, const uint
         return;
     }
     const uint16_t *outp;
-    const int cnt = path_core<CELLS>(sh, S, smem + OFF_PA, H, W, true, LINE_GRID_ONE, outp);
+    const int cnt = path_core<CELLS, EARLY>(sh, S, smem + OFF_PA, H, W, true, LINE_GRID_ONE, outp);
     if (tid < 64) {
         if (cnt > max_pts) {
             if (lane == 0) out_n[b] = -cnt;  // caller's buffer too small
@@ -3255,6 +3307,7 @@ __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 
 namespace {
@@ -3354,6 +3407,25 @@ Geometry make_geometry()
         }
     }
     return g;
+}
+
+// Path kernel choice: the early-exit variant (SSSP fixpoint first, then the SPFA only until the target's
+// parent chain is final) holds fewer queries per CU (LDS: 2 instead of 4 in small rooms, 1 instead of
+// 2 in large ones), so it is taken while every query of the launch is resident at once, where each
+// query's latency is the launch's; simaps_path_mode forces either.
+std::atomic<int> g_path_mode{0};
+bool path_early(int n, bool small)
+{
+    const int mode = g_path_mode.load();
+    if (mode) return mode == 2;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            cus = c;
+        if (cus <= 0) cus = 256;
+    }
+    return n <= (small ? 2 : 1) * cus;
 }
 
 int check_cfg(const simaps_config *c)
@@ -3533,15 +3605,28 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
         return fail(SIMAPS_EINVAL, "NULL buffer");
     if ((rc = pending_faults())) return rc;
     const Geometry geo = make_geometry();
-    if ((cfg->room_h + 2) * ((cfg->room_w + 2) | 1) <= PATH_SMALL_CELLS)
-        hipLaunchKernelGGL(path_kernel<PATH_SMALL_CELLS>, dim3(N), dim3(PNT), 0, (hipStream_t)stream, *cfg, geo, agents, envs,
-                           robots, occupancy, sources, targets, max_points, out_xy, out_count, g_fault_dev);
-    else
-        hipLaunchKernelGGL(path_kernel<SIMAPS_MAX_ROOM_CELLS>, dim3(N), dim3(PNT), 0, (hipStream_t)stream, *cfg, geo, agents,
-                           envs, robots, occupancy, sources, targets, max_points, out_xy, out_count, g_fault_dev);
+    const bool small = (cfg->room_h + 2) * ((cfg->room_w + 2) | 1) <= PATH_SMALL_CELLS;
+    const hipStream_t st = (hipStream_t)stream;
+#define SIMAPS_PATH_LAUNCH(C, E)                                                                       \
+    hipLaunchKernelGGL((path_kernel<C, E>), dim3(N), dim3(PNT), 0, st, *cfg, geo, agents, envs, robots, occupancy, sources, \
+                       targets, max_points, out_xy, out_count, g_fault_dev)
+    if (path_early(N, small)) {
+        if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, true);
+        else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true);
+    } else {
+        if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, false);
+        else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, false);
+    }
+#undef SIMAPS_PATH_LAUNCH
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "shortest_path launch: %s", hipGetErrorString(e));
     return 0;
+}
+
+int simaps_path_mode(int mode)
+{
+    if (mode < 0 || mode > 2) return fail(SIMAPS_EINVAL, "path mode %d not in 0..2", mode);
+    return g_path_mode.exchange(mode);
 }
 
 int simaps_ingest_chunks(int height_px, int width_px)
@@ -3590,12 +3675,19 @@ int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *s
     if (ww > SIMAPS_MAX_ROOM_W || wh > MAX_ROWS || (wh + 2) * ((ww + 2) | 1) > SIMAPS_MAX_ROOM_CELLS)
         return fail(SIMAPS_EUNSUPPORTED, "window %dx%d exceeds the LDS-resident limit", wh, ww);
     if (const int rc = pending_faults()) return rc;
-    if ((wh + 2) * ((ww + 2) | 1) <= PATH_SMALL_CELLS)
-        hipLaunchKernelGGL(grid_path_kernel<PATH_SMALL_CELLS>, dim3(B), dim3(PNT), 0, (hipStream_t)stream, H, W, grids, sources,
-                           targets, wi0, wj0, wh, ww, max_points, out_ij, out_count, g_fault_dev);
-    else
-        hipLaunchKernelGGL(grid_path_kernel<SIMAPS_MAX_ROOM_CELLS>, dim3(B), dim3(PNT), 0, (hipStream_t)stream, H, W, grids,
-                           sources, targets, wi0, wj0, wh, ww, max_points, out_ij, out_count, g_fault_dev);
+    const bool small = (wh + 2) * ((ww + 2) | 1) <= PATH_SMALL_CELLS;
+    const hipStream_t st = (hipStream_t)stream;
+#define SIMAPS_GRID_PATH_LAUNCH(C, E)                                                                  \
+    hipLaunchKernelGGL((grid_path_kernel<C, E>), dim3(B), dim3(PNT), 0, st, H, W, grids, sources, targets, wi0, wj0, wh, \
+                       ww, max_points, out_ij, out_count, g_fault_dev)
+    if (path_early(B, small)) {
+        if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, true);
+        else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true);
+    } else {
+        if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, false);
+        else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, false);
+    }
+#undef SIMAPS_GRID_PATH_LAUNCH
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "grid_path launch: %s", hipGetErrorString(e));
     return 0;

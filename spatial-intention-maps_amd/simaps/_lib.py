@@ -87,6 +87,8 @@ def _load(path=LIB_PATH):
     L.simaps_shortest_path.restype = i32
     L.simaps_ingest.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(Camera), i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.simaps_ingest.restype = i32
+    L.simaps_path_mode.argtypes = [i32]
+    L.simaps_path_mode.restype = i32
     L.simaps_ingest_chunks.argtypes = [i32, i32]
     L.simaps_ingest_chunks.restype = i32
     L.simaps_sssp_grid.argtypes = [i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp]
@@ -103,7 +105,7 @@ def _load(path=LIB_PATH):
 lib = _load()
 
 EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_fault_status', 'simaps_num_channels',
-            'simaps_robot_mask', 'simaps_pack_robots', 'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest', 'simaps_ingest_chunks',
+            'simaps_robot_mask', 'simaps_pack_robots', 'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest', 'simaps_ingest_chunks', 'simaps_path_mode',
             'simaps_sssp_grid', 'simaps_grid_path')
 
 # error codes and device fault bits (include/simaps.h)

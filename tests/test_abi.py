@@ -20,7 +20,7 @@ def declared_symbols():
 def test_header_declares_the_abi():
     assert declared_symbols() == sorted(['simaps_abi_version', 'simaps_last_error', 'simaps_fault_status',
                                          'simaps_num_channels', 'simaps_sp_distance', 'simaps_shortest_path',
-                                         'simaps_ingest', 'simaps_ingest_chunks', 'simaps_robot_mask', 'simaps_pack_robots',
+                                         'simaps_ingest', 'simaps_ingest_chunks', 'simaps_path_mode', 'simaps_robot_mask', 'simaps_pack_robots',
                                          'simaps_get_state', 'simaps_sssp_grid',
                                          'simaps_grid_path'])
 

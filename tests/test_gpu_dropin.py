@@ -162,7 +162,17 @@ def test_distance_to_receptacle_dropin(V):
             assert got[e][a] == [ao.shortest_path_distance(s['receptacle_position'], p) for p in pos[e][a]]
 
 
-def test_shortest_path_reference_goldens(V):
+@pytest.fixture(params=[1, 2], ids=['compact', 'early_exit'])
+def path_mode(request):
+    """Both path kernel variants (include/simaps.h simaps_path_mode): 1 the SPFA to an empty queue,
+    2 the SSSP fixpoint first and the SPFA only until the target's parent chain is final."""
+    from simaps import _lib
+    prev = _lib.lib.simaps_path_mode(request.param)
+    yield request.param
+    _lib.lib.simaps_path_mode(prev)
+
+
+def test_shortest_path_reference_goldens(V, path_mode):
     """Movement paths through simaps_shortest_path vs the reference's own
     OccupancyMap.shortest_path outputs (straight-line test, EDT snap, exact SPFA parents,
     approximate_polygon, line-of-sight pruning)."""
@@ -192,7 +202,7 @@ def test_shortest_path_reference_goldens(V):
     assert nontrivial >= 40
 
 
-def test_maze_paths_reference_goldens(V):
+def test_maze_paths_reference_goldens(V, path_mode):
     """Movement paths on the maze environments (large_doors / tunnels / rooms) vs the reference's
     own OccupancyMap.shortest_path: long detours through doors and tunnels, exactly."""
     synthetic, vector_env = V
@@ -287,7 +297,7 @@ def test_ingest_full_size_two_frames_vs_oracle(V):
         assert _bitwise(ov[n], scenes[e]['overhead'][a]) and np.array_equal(oc[n], scenes[e]['occupancy'][a]), (e, a)
 
 
-def test_gridgraph_shortest_path_reference_goldens(V):
+def test_gridgraph_shortest_path_reference_goldens(V, path_mode):
     """GridGraph.shortest_path (pyx:121-154) on raw cells against the reference itself: the demo
     sample (free / blocked / equal ends) and random grids with free values 1, 2, 255 (line of sight
     counts any cell != 1 as blocked), blocked sources, unreachable targets."""
@@ -376,7 +386,7 @@ def _dp_tie(grid, src, tgt):
     return False
 
 
-def test_gridgraph_paths_fuzz_vs_oracle(V):
+def test_gridgraph_paths_fuzz_vs_oracle(V, path_mode):
     """GridGraph.shortest_path / shortest_path_image on ~1,000 (grid, source, target) cases built to
     create equal-length-path ties, bitwise against the oracle's C restatement of pyx:69-154 (itself
     pinned to the reference by tests/test_oracle_golden.py): the lane-parallel SLF resolution of the

@@ -4,7 +4,7 @@
 oracle in a process pool.  A path mismatch is classified with the tests' approximate_polygon tie
 check (tests/test_gpu_dropin.py::_dp_tie): at such a tie the reference's own pick is host-dependent.
 
-    python tools/fuzz_rows.py [envs_per_config] [queries_per_agent] [procs]
+    python tools/fuzz_rows.py [envs_per_config] [queries_per_agent] [procs] [--path-mode 0|1|2]
 """
 import json
 import os
@@ -50,10 +50,17 @@ def _oracle(job):
 
 
 def main():
-    envs = int(sys.argv[1]) if len(sys.argv) > 1 else 16
-    Q = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-    procs = int(sys.argv[3]) if len(sys.argv) > 3 else 16
-    from simaps import batch, synthetic
+    argv = list(sys.argv[1:])
+    mode = 0
+    if '--path-mode' in argv:  # simaps_path_mode: 0 automatic, 1 compact, 2 early exit
+        k = argv.index('--path-mode')
+        mode = int(argv[k + 1])
+        del argv[k:k + 2]
+    envs = int(argv[0]) if len(argv) > 0 else 16
+    Q = int(argv[1]) if len(argv) > 1 else 4
+    procs = int(argv[2]) if len(argv) > 2 else 16
+    from simaps import _lib, batch, synthetic
+    _lib.lib.simaps_path_mode(mode)
     tot = {'paths': 0, 'paths_with_detours': 0, 'path_mismatches': 0, 'at_ties': 0, 'lookups': 0, 'lookup_mismatches': 0}
     with get_context('spawn').Pool(procs) as pool:
         for cfg in CONFIGS:
@@ -77,6 +84,7 @@ def main():
             r['s'] = round(time.time() - t0, 1)
             print(json.dumps(r), flush=True)
     tot['seeds'] = [SEED0, SEED0 + envs - 1]
+    tot['path_mode'] = mode
     print(json.dumps(tot), flush=True)
 
 

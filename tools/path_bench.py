@@ -22,14 +22,23 @@ import torch  # noqa: E402
 from simaps import _lib, batch, synthetic  # noqa: E402
 
 
-def case(cfg, envs, steps):
+def case(cfg, envs, steps, mode=0, targets='across'):
+    """targets: 'across' -- a random point on the other side of x = 0 (around the divider, if any);
+    'local' -- a random point of the robot's own 96 x 96 local map (the action space of
+    Robot.store_new_action, envs.py:857-876), clipped to the room."""
     scenes = [synthetic.make_scene(cfg, e % 64) for e in range(envs)]
     b = batch.StateBatch(scenes)
     rs = np.random.RandomState(0)
     rl, rw = scenes[0]['room_length'], scenes[0]['room_width']
     N = b.N
     psrc = np.array([scenes[e]['robots'][a]['position'][:2] for e, a in b.agents])
-    ptgt = np.stack([rs.uniform(0.05, rl / 2, N) * -np.sign(psrc[:, 0]), rs.uniform(-rw / 2, rw / 2, N)], -1)
+    if targets == 'across':
+        ptgt = np.stack([rs.uniform(0.05, rl / 2, N) * -np.sign(psrc[:, 0]), rs.uniform(-rw / 2, rw / 2, N)], -1)
+    else:
+        ptgt = psrc + rs.uniform(-0.5, 0.5, (N, 2))
+        ptgt[:, 0] = np.clip(ptgt[:, 0], -rl / 2 + 0.02, rl / 2 - 0.02)
+        ptgt[:, 1] = np.clip(ptgt[:, 1], -rw / 2 + 0.02, rw / 2 - 0.02)
+    prev = _lib.lib.simaps_path_mode(mode)
     src = torch.as_tensor(psrc).cuda()
     tgt = torch.as_tensor(ptgt).cuda()
     for _ in range(2):
@@ -43,8 +52,10 @@ def case(cfg, envs, steps):
     e1.record(s)
     torch.cuda.synchronize()
     _lib.check_faults()
+    _lib.lib.simaps_path_mode(prev)
     ms = e0.elapsed_time(e1) / steps
-    out = {'config': cfg, 'paths_per_launch': N, 'ms_per_launch': ms, 'paths_per_s': N / (ms * 1e-3),
+    out = {'config': cfg, 'targets': targets, 'path_mode': {0: 'auto', 1: 'compact', 2: 'early_exit'}[mode],
+           'paths_per_launch': N, 'ms_per_launch': ms, 'paths_per_s': N / (ms * 1e-3),
            'detours': int((cnt.cpu().numpy() > 2).sum())}
     if '--stamps' in sys.argv:
         L = _lib.lib
@@ -57,6 +68,7 @@ def case(cfg, envs, steps):
         pops = st[full, 7]
         out.update({'spfa_queries': int(full.sum()), 'spfa_us_median': float(np.median(spfa_us)),
                     'pops_median': float(np.median(pops)),
+                    'sweep_rounds_median': float(np.median(st[full, 8])) if mode == 2 else None,
                     'ns_per_pop_median': float(np.median(spfa_us * 1e3 / np.maximum(pops, 1))),
                     'query_us_median': float(np.median((st[full, 6] - st[full, 0]) / 100.0))})
     print(json.dumps(out), flush=True)
@@ -66,7 +78,11 @@ if __name__ == '__main__':
     # (pushing_4-large_empty has no obstacles: nearly all its paths are straight lines, and a launch
     # lasts as long as its slowest query -- a snapped end's full-room SPFA; lifting_4-large_doors:
     # large rooms with detours)
-    for cfg, envs in (('lifting_4-small_divider', 64), ('lifting_4-small_divider', 256), ('lifting_4-small_divider', 512),
-                      ('pushing_4-large_empty', 64), ('pushing_4-large_empty', 512),
-                      ('lifting_4-large_doors', 64), ('lifting_4-large_doors', 256), ('lifting_4-large_doors', 512)):
-        case(cfg, envs, 5 if '--stamps' in sys.argv else 10)
+    steps = 5 if '--stamps' in sys.argv else 10
+    for targets in ('across', 'local'):
+        for cfg, envs in (('lifting_4-small_divider', 16), ('lifting_4-small_divider', 64), ('lifting_4-small_divider', 128),
+                          ('lifting_4-small_divider', 256), ('lifting_4-small_divider', 512),
+                          ('lifting_4-large_doors', 16), ('lifting_4-large_doors', 64), ('lifting_4-large_doors', 256),
+                          ('lifting_4-large_doors', 512)):
+            for mode in (1, 2):
+                case(cfg, envs, steps, mode, targets)
