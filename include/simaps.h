@@ -226,11 +226,12 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
                          const double *targets, int max_points, double *out_xy, int32_t *out_count, void *stream);
 
 /* Which path kernels simaps_shortest_path / simaps_grid_path launch (host-side, process-wide; returns
- * the previous mode): 0 automatic, 1 compact (the SPFA runs to an empty queue; more queries per CU),
- * 2 early exit (the SSSP fixpoint by directional sweeps first, then the SPFA only until every vertex of
- * the target's parent chain has its final distance -- whose parent then can no longer change).  Both
- * return the reference's waypoints exactly.  Automatic takes the early exit while all queries of the
- * launch fit on the device at once. */
+ * the previous mode): 0 automatic (= 2), 1 compact (the SPFA runs to an empty queue), 2 early exit
+ * (the SSSP fixpoint by directional sweeps first, then the SPFA only until every vertex of the
+ * target's parent chain has its final distance -- whose parent then can no longer change; the
+ * fixpoint is parked in a library-owned device buffer per stream, grown outside graph capture -- a
+ * launch that would need to grow it during capture takes the compact kernels).  Both return the
+ * reference's waypoints exactly. */
 int simaps_path_mode(int mode);
 
 /* Batched observation ingest into the per-agent maps (occupancy / overhead [M, H, W], slot

@@ -2523,21 +2523,20 @@ struct PathHdr {
     unsigned fault;        // SIMAPS_FAULT_* bits of this query
     int changed[3];        // (EARLY) per-round "a sweep improved a cell" flags
     uint64_t dirty[4][2];  // (EARLY) per sweep direction: lines to relax again
+    float finT;            // (EARLY) the target's fixpoint distance
 };
 constexpr int OFF_PS = align16((int)sizeof(PathHdr));
 constexpr int OFF_PA = OFF_PS + align16((int)(offsetof(SsspScratch, dtab) + sizeof(B128) * MAX_WIN_ROWS));
-// EARLY: + the SSSP fixpoint `fin` f32 [CELLS] (the get_state sweeps from the snapped source), for the
-// SPFA's early exit (path_core)
-template <int CELLS, bool EARLY>
+// (The early-exit variant's SSSP fixpoint runs in the dist array and is then parked in global memory --
+// the per-stream scratch of path_scratch(), CELLS f32 per query -- so both variants have this layout.)
+template <int CELLS>
 constexpr int path_lds_bytes()
 {
-    return align16(OFF_PA + (EARLY ? 11 : 7) * CELLS > OFF_PS + (int)sizeof(SsspScratch)
-                       ? OFF_PA + (EARLY ? 11 : 7) * CELLS : OFF_PS + (int)sizeof(SsspScratch));
+    return align16(OFF_PA + 7 * CELLS > OFF_PS + (int)sizeof(SsspScratch) ? OFF_PA + 7 * CELLS
+                                                                           : OFF_PS + (int)sizeof(SsspScratch));
 }
-static_assert(path_lds_bytes<PATH_SMALL_CELLS, false>() * 4 <= 160 * 1024, "4 small-room queries per CU");
-static_assert(path_lds_bytes<SIMAPS_MAX_ROOM_CELLS, false>() * 2 <= 160 * 1024, "2 queries per CU at the room limit");
-static_assert(path_lds_bytes<PATH_SMALL_CELLS, true>() * 2 <= 160 * 1024, "2 small-room early-exit queries per CU");
-static_assert(path_lds_bytes<SIMAPS_MAX_ROOM_CELLS, true>() <= 160 * 1024, "early-exit query at the room limit");
+static_assert(path_lds_bytes<PATH_SMALL_CELLS>() * 4 <= 160 * 1024, "4 small-room queries per CU");
+static_assert(path_lds_bytes<SIMAPS_MAX_ROOM_CELLS>() * 2 <= 160 * 1024, "2 queries per CU at the room limit");
 static_assert(MAX_ROWS <= 256 && SIMAPS_MAX_ROOM_W <= 256, "rect cells pack as (row << 8) | col");
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
@@ -2559,10 +2558,9 @@ __device__ __forceinline__ int dir_off(int k, int pw)
 // returns cnt in wave 0.  All PNT threads call it.
 template <int CELLS, bool EARLY>
 __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr, int H, int W, bool run_spfa,
-                                         int line_mask, const uint16_t *&outp_ret)
+                                         int line_mask, float *gfin, const uint16_t *&outp_ret)
 {
     float *dist = reinterpret_cast<float *>(arr);
-    float *fin = reinterpret_cast<float *>(arr + 7 * CELLS);  // (EARLY only)
     uint16_t *queue = reinterpret_cast<uint16_t *>(arr + 4 * CELLS);
     uint8_t *pin = reinterpret_cast<uint8_t *>(arr + 6 * CELLS);
     // after the parent walk: dense path (u16 rect cells) in the queue region, chain flags in pin,
@@ -2588,9 +2586,8 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
     for (int k = tid; k < cells; k += PNT) {
         const int rr = k / pw, cc = k - rr * pw;  // (once per cell)
         const bool fr = rr >= 1 && rr <= h && cc >= 1 && cc <= w && b_test(S.freeb[rr - 1], cc - 1);
-        dist[k] = fr ? INFR : -INFINITY;
+        dist[k] = fr ? (EARLY ? INFINITY : INFR) : -INFINITY;  // (EARLY: the sweeps' initial state)
         pin[k] = 0;
-        if (EARLY) fin[k] = fr ? INFINITY : -INFINITY;
     }
     const int su = (sh.src_s[0][0] - sh.i0 + 1) * pw + (sh.src_s[0][1] - sh.j0 + 1);
     const int tv = (sh.src_s[1][0] - sh.i0 + 1) * pw + (sh.src_s[1][1] - sh.j0 + 1);
@@ -2605,19 +2602,29 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         // The f32 fixpoint of the graph from the source -- the SPFA's final distances, bitwise (SURVEY
         // a10) -- by the get_state sweeps, one direction per wave, rounds until nothing improves.
         // A vertex whose SPFA distance already equals it can never improve again, so its parent is
-        // final: the SPFA below may stop as soon as the target's whole parent chain is final.
-        if (tid == 0) fin[su] = 0.0f;
+        // final: the SPFA below may stop as soon as the target's whole parent chain is final.  The
+        // sweeps run in the dist array; the fixpoint then moves to this query's global scratch (read
+        // back only along the parent chain) and dist takes the SPFA's initial state.
+        if (tid == 0) dist[su] = 0.0f;
         lds_barrier();
         const int wave = tid >> 6;
         int steps = 0, round = 0;
         for (;; round++) {
             if (tid == 0) sh.changed[(round + 1) % 3] = 0;
-            if (sweep(fin, h, w, pw, wave, sh.dirty, steps) && lane == 0) sh.changed[round % 3] = 1;
+            if (sweep(dist, h, w, pw, wave, sh.dirty, steps) && lane == 0) sh.changed[round % 3] = 1;
             lds_barrier();
             if (!sh.changed[round % 3] || round >= h * w + 16) break;
         }
         if (tid == 0 && round >= h * w + 16) sh.fault |= SIMAPS_FAULT_ROUNDS;
+        if (tid == 0) sh.finT = dist[tv];
+        for (int k = tid; k < cells; k += PNT) {
+            const float f = dist[k];
+            gfin[k] = f;
+            dist[k] = f == -INFINITY ? -INFINITY : INFR;
+        }
+        __syncthreads();  // (global stores of the other waves -> wave 0's chain checks; LDS likewise)
         if (tid == 0) STAMP_VAL(8, round + 1);
+        if (tid == 0) STAMP_NB(10);  // (stamp build: the sweeps' end)
     }
     if (tid < 64 && run_spfa) {
         const int doff = lane < 8 ? dir_off(lane, pw) : 0;
@@ -2634,138 +2641,160 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         lds_float *Ld = (lds_float *)dist;
         lds_u16 *Lq = (lds_u16 *)queue;
         lds_u8 *Li = (lds_u8 *)pin;
-        int pops = 0, next_check = 0;
+        // pops: done so far; lim: the next pop count at which the loop looks beyond its queue -- the
+        // pop cap (never reached by a correct SPFA) or, in EARLY, the next early-exit check -- so the
+        // common pop pays one scalar compare for both
+        int pops = 0, gap = 64, lim = EARLY ? 32 : SIMAPS_POP_CAP;
         bool early = false;
-        lds_float *Lfin = (lds_float *)fin;
-        const float finT = EARLY ? fin[tv] : 0.0f;  // the target's fixpoint distance
-        for (;;) {
-            // (front / second are wave-uniform: keep them in SGPRs across the loop)
-            const int u = __builtin_amdgcn_readfirstlane(front);
-            qh = qh + 1 == cells ? 0 : qh + 1;
-            count--;                           // entries queue[qh .. qt) after the pop
-            const int F0 = __builtin_amdgcn_readfirstlane(second);  // the next front (valid if count >= 1)
-            const int q2 = qh + 1 == cells ? 0 : qh + 1;
-            const int v = u + doff;
-            // one round of reads (in-order LDS sees this wave's earlier writes); the ballots below
-            // consume them together.  Lane 8's v is u: its pin read is u's (parent bits to keep).
-            const float du = Ld[u], dv = Ld[v];
-            const int pv = Li[v];
-            // the front's distance before this pop's relaxations (F0 is a queue entry, < cells, when
-            // count >= 1; otherwise unused, and clamped so the read stays inside the array)
-            const float dF0 = Ld[(unsigned)F0 < (unsigned)cells ? F0 : 0];
-            const int third = Lq[q2];          // queue[qh + 1]: the next pop's second (if count >= 2)
-            const float dT = EARLY ? Ld[tv] : 0.0f;  // (EARLY) the target's distance before this pop
-            const float nd = du + wl;
-            // (lanes >= 8: v = u, so nd = du + 1 > dv: never `better`; no lane test needed)
-            const bool better = nd < dv;
-            const uint64_t imp = __builtin_amdgcn_ballot_w64(better);
-            const uint64_t notq = __builtin_amdgcn_ballot_w64(!(pv & 0x10));
-            Li[u] = (uint8_t)(__builtin_amdgcn_readlane(pv, 8) & 0xf);  // u leaves the queue (pyx:92)
-            int nf = F0, nsecond = __builtin_amdgcn_readfirstlane(third);
-            if (imp) {
-                if (better) { Ld[v] = nd; Li[v] = pbits; }
-                const uint64_t push = imp & notq;
-                if (push) {
-                    // The pushes of this pop, in edge order (pyx:104-111): each goes to the tail and
-                    // swaps with the front if its distance is below the front's at that moment.  The
-                    // front's distance seen by edge k is F0's, lowered by this pop only if F0 is the
-                    // head of an earlier edge jf < k (F0 is queued, so never pushed, but it may be
-                    // relaxed) -- until the first push that beats it (js); from then on it is the
-                    // running minimum of the pushed distances from js on.  A swapping push's slot
-                    // receives the previous front (F0 or the previous swapping push's vertex); the last
-                    // swapper ends at the front.
-                    const int np = __popcll(push);
-                    // F0 as the head of an edge this pop IMPROVED (lane jf): only then does its
-                    // distance change for the later edges.  (Lanes >= 8 have v = u != F0 and never
-                    // improve; with an empty queue F0 is stale, but that case ignores jf.)
-                    const uint64_t fmi = __builtin_amdgcn_ballot_w64(v == F0) & imp;
-                    const int jf = fmi ? __builtin_ctzll(fmi) : 64;
-                    const float dafter = fmi ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), jf)) : dF0;
-                    if (np == 1 && count > 0) {
-                        // one push (the common case): a scalar decision, no scans
-                        const int p1 = __builtin_ctzll(push);
-                        const int vp = __builtin_amdgcn_readlane(v, p1);
-                        const float ndp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), p1));
-                        const bool sw = ndp < (p1 > jf ? dafter : dF0);
-                        const int content = sw ? F0 : vp;
-                        Lq[qt] = (uint16_t)content;
-                        if (sw) { Lq[qh] = (uint16_t)vp; nf = vp; }
-                        if (count == 1) nsecond = content;  // the tail slot was queue[qh + 1]
-                        qt = qt + 1 == cells ? 0 : qt + 1;
-                        count++;
-                    } else {
-                        const bool isP = (push >> lane) & 1;
-                        const int rank = __popcll(push & ((1ull << lane) - 1));
-                        uint64_t cand = push;
-                        int Fq = F0;
-                        float dbefore = dF0, dseen = dafter;
-                        if (count == 0) {  // the queue was empty: the first push becomes the front
-                            const int p1 = __builtin_ctzll(push);
-                            Fq = __builtin_amdgcn_readlane(v, p1);
-                            dbefore = dseen = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), p1));
-                            cand &= cand - 1;
+        // the target's fixpoint distance (uniform: kept in an SGPR)
+        const float finT = EARLY ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh.finT))) : 0.0f;
+        // an unreachable target (fixpoint +inf) never gets a parent: the SPFA cannot change the path
+        if (EARLY && finT == INFINITY) count = 0, early = true;
+        // pop rounds (inner loop: one exit, so the common pop ends in one compare) up to `lim`, then
+        // (EARLY) an early-exit check
+        if (count > 0)
+            for (;;) {
+                for (;;) {
+                    // (front / second are wave-uniform: keep them in SGPRs across the loop)
+                    const int u = __builtin_amdgcn_readfirstlane(front);
+                    qh = qh + 1 == cells ? 0 : qh + 1;
+                    count--;                           // entries queue[qh .. qt) after the pop
+                    const int F0 = __builtin_amdgcn_readfirstlane(second);  // the next front (valid if count >= 1)
+                    const int q2 = qh + 1 == cells ? 0 : qh + 1;
+                    const int v = u + doff;
+                    // one round of reads (in-order LDS sees this wave's earlier writes); the ballots below
+                    // consume them together.  Lane 8's v is u: its pin read is u's (parent bits to keep).
+                    const float du = Ld[u], dv = Ld[v];
+                    const int pv = Li[v];
+                    // the front's distance before this pop's relaxations (F0 is a queue entry, < cells, when
+                    // count >= 1; otherwise unused, and clamped so the read stays inside the array)
+                    const float dF0 = Ld[(unsigned)F0 < (unsigned)cells ? F0 : 0];
+                    const int third = Lq[q2];          // queue[qh + 1]: the next pop's second (if count >= 2)
+                    const float nd = du + wl;
+                    // (lanes >= 8: v = u, so nd = du + 1 > dv: never `better`; no lane test needed)
+                    const bool better = nd < dv;
+                    const uint64_t imp = __builtin_amdgcn_ballot_w64(better);
+                    const uint64_t notq = __builtin_amdgcn_ballot_w64(!(pv & 0x10));
+                    Li[u] = (uint8_t)(__builtin_amdgcn_readlane(pv, 8) & 0xf);  // u leaves the queue (pyx:92)
+                    int nf = F0, nsecond = __builtin_amdgcn_readfirstlane(third);
+                    if (imp) {
+                        if (better) { Ld[v] = nd; Li[v] = pbits; }
+                        const uint64_t push = imp & notq;
+                        if (push) {
+                            // The pushes of this pop, in edge order (pyx:104-111): each goes to the tail and
+                            // swaps with the front if its distance is below the front's at that moment.  The
+                            // front's distance seen by edge k is F0's, lowered by this pop only if F0 is the
+                            // head of an earlier edge jf < k (F0 is queued, so never pushed, but it may be
+                            // relaxed) -- until the first push that beats it (js); from then on it is the
+                            // running minimum of the pushed distances from js on.  A swapping push's slot
+                            // receives the previous front (F0 or the previous swapping push's vertex); the last
+                            // swapper ends at the front.
+                            const int np = __popcll(push);
+                            // F0 as the head of an edge this pop IMPROVED (lane jf): only then does its
+                            // distance change for the later edges.  (Lanes >= 8 have v = u != F0 and never
+                            // improve; with an empty queue F0 is stale, but that case ignores jf.)
+                            const uint64_t fmi = __builtin_amdgcn_ballot_w64(v == F0) & imp;
+                            const int jf = fmi ? __builtin_ctzll(fmi) : 64;
+                            const float dafter = fmi ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), jf)) : dF0;
+                            if (np == 1 && count > 0) {
+                                // one push (the common case): a scalar decision, no scans
+                                const int p1 = __builtin_ctzll(push);
+                                const int vp = __builtin_amdgcn_readlane(v, p1);
+                                const float ndp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), p1));
+                                const bool sw = ndp < (p1 > jf ? dafter : dF0);
+                                const int content = sw ? F0 : vp;
+                                Lq[qt] = (uint16_t)content;
+                                if (sw) { Lq[qh] = (uint16_t)vp; nf = vp; }
+                                if (count == 1) nsecond = content;  // the tail slot was queue[qh + 1]
+                                qt = qt + 1 == cells ? 0 : qt + 1;
+                                count++;
+                            } else {
+                                const bool isP = (push >> lane) & 1;
+                                const int rank = __popcll(push & ((1ull << lane) - 1));
+                                uint64_t cand = push;
+                                int Fq = F0;
+                                float dbefore = dF0, dseen = dafter;
+                                if (count == 0) {  // the queue was empty: the first push becomes the front
+                                    const int p1 = __builtin_ctzll(push);
+                                    Fq = __builtin_amdgcn_readlane(v, p1);
+                                    dbefore = dseen = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nd), p1));
+                                    cand &= cand - 1;
+                                }
+                                const bool isC = (cand >> lane) & 1;
+                                const uint64_t sF0 = __ballot(isC && nd < (lane > jf ? dseen : dbefore));
+                                int content = v, newfront = Fq;
+                                if (sF0) {
+                                    const int js = __builtin_ctzll(sF0);
+                                    // exclusive prefix minimum of nd over the candidate lanes in [js, lane) (DPP
+                                    // row shifts: lanes 0-7 lie in one row)
+                                    float y = (isC && lane >= js) ? nd : INFINITY;
+        #define SPFA_SHR(x, n, old) __builtin_amdgcn_update_dpp((old), (x), 0x110 + (n), 0xf, 0xf, false)
+        #define SPFA_SHRF(x, n) __int_as_float(SPFA_SHR(__float_as_int(x), n, (int)INF_BITS))
+                                    y = fminf(y, SPFA_SHRF(y, 1));
+                                    y = fminf(y, SPFA_SHRF(y, 2));
+                                    y = fminf(y, SPFA_SHRF(y, 4));
+                                    const float pm = SPFA_SHRF(y, 1);
+                                    const bool sw = isC && (lane == js || (lane > js && nd < pm));
+                                    const uint64_t swm = __ballot(sw);
+                                    // the previous swapper's vertex: exclusive "last valid" scan of v over swappers
+                                    int z = sw ? v : -1, zs;
+                                    zs = SPFA_SHR(z, 1, -1); z = z >= 0 ? z : zs;
+                                    zs = SPFA_SHR(z, 2, -1); z = z >= 0 ? z : zs;
+                                    zs = SPFA_SHR(z, 4, -1); z = z >= 0 ? z : zs;
+                                    const int prev = SPFA_SHR(z, 1, -1);
+        #undef SPFA_SHRF
+        #undef SPFA_SHR
+                                    if (sw) content = prev >= 0 ? prev : Fq;
+                                    newfront = __builtin_amdgcn_readlane(v, 63 - __builtin_clzll(swm));
+                                }
+                                const int slot = qt + rank < cells ? qt + rank : qt + rank - cells;
+                                if (isP) Lq[slot] = (uint16_t)content;
+                                if (sF0) Lq[qh] = (uint16_t)newfront;  // after the lanes' stores (in the empty case qh is p1's slot)
+                                if (count <= 1) {  // the pushes wrote queue[qh + 1]: the next pop's second
+                                    const uint64_t at = __ballot(isP && slot == q2);
+                                    if (at) nsecond = __builtin_amdgcn_readlane(content, __builtin_ctzll(at));
+                                }
+                                qt = qt + np < cells ? qt + np : qt + np - cells;
+                                count += np;
+                                nf = newfront;
+                            }
                         }
-                        const bool isC = (cand >> lane) & 1;
-                        const uint64_t sF0 = __ballot(isC && nd < (lane > jf ? dseen : dbefore));
-                        int content = v, newfront = Fq;
-                        if (sF0) {
-                            const int js = __builtin_ctzll(sF0);
-                            // exclusive prefix minimum of nd over the candidate lanes in [js, lane) (DPP
-                            // row shifts: lanes 0-7 lie in one row)
-                            float y = (isC && lane >= js) ? nd : INFINITY;
-#define SPFA_SHR(x, n, old) __builtin_amdgcn_update_dpp((old), (x), 0x110 + (n), 0xf, 0xf, false)
-#define SPFA_SHRF(x, n) __int_as_float(SPFA_SHR(__float_as_int(x), n, (int)INF_BITS))
-                            y = fminf(y, SPFA_SHRF(y, 1));
-                            y = fminf(y, SPFA_SHRF(y, 2));
-                            y = fminf(y, SPFA_SHRF(y, 4));
-                            const float pm = SPFA_SHRF(y, 1);
-                            const bool sw = isC && (lane == js || (lane > js && nd < pm));
-                            const uint64_t swm = __ballot(sw);
-                            // the previous swapper's vertex: exclusive "last valid" scan of v over swappers
-                            int z = sw ? v : -1, zs;
-                            zs = SPFA_SHR(z, 1, -1); z = z >= 0 ? z : zs;
-                            zs = SPFA_SHR(z, 2, -1); z = z >= 0 ? z : zs;
-                            zs = SPFA_SHR(z, 4, -1); z = z >= 0 ? z : zs;
-                            const int prev = SPFA_SHR(z, 1, -1);
-#undef SPFA_SHRF
-#undef SPFA_SHR
-                            if (sw) content = prev >= 0 ? prev : Fq;
-                            newfront = __builtin_amdgcn_readlane(v, 63 - __builtin_clzll(swm));
-                        }
-                        const int slot = qt + rank < cells ? qt + rank : qt + rank - cells;
-                        if (isP) Lq[slot] = (uint16_t)content;
-                        if (sF0) Lq[qh] = (uint16_t)newfront;  // after the lanes' stores (in the empty case qh is p1's slot)
-                        if (count <= 1) {  // the pushes wrote queue[qh + 1]: the next pop's second
-                            const uint64_t at = __ballot(isP && slot == q2);
-                            if (at) nsecond = __builtin_amdgcn_readlane(content, __builtin_ctzll(at));
-                        }
-                        qt = qt + np < cells ? qt + np : qt + np - cells;
-                        count += np;
-                        nf = newfront;
                     }
+                    front = nf;
+                    second = nsecond;
+                    ++pops;
+                    if (count <= 0 || pops >= lim) break;
                 }
-            }
-            front = nf;
-            second = nsecond;
-            ++pops;
-            if (count <= 0 || pops >= SIMAPS_POP_CAP) break;  // the cap is never reached by a correct SPFA
-            if (EARLY && dT == finT && pops >= next_check) {
-                // early exit: is every vertex of the target's parent chain at its final distance?
-                // (one LDS round per chain step: the parent's distance, fixpoint and parent bits)
-                int v = tv, pv = Li[tv];
-                bool ok = true;
-                for (int st = 0; v != su; st++) {
-                    const int pd = pv & 0xf;
-                    if (!pd || st >= cells) { ok = false; break; }
-                    v -= __builtin_amdgcn_readlane(doff, pd - 1);
-                    const float a = Ld[v], b = Lfin[v];
-                    pv = Li[v];
-                    if (a != b) { ok = false; break; }
+                if (count <= 0 || pops >= SIMAPS_POP_CAP) break;
+                // (EARLY only: lim < SIMAPS_POP_CAP) early exit: every 32 pops, is the target at its final
+                // distance and then every vertex of its parent chain?  The chain is walked in LDS (one
+                // round per step), 64 vertices to a batch, each batch's distances compared with the
+                // fixpoint in one lane-parallel global read.
+                lim = pops + 32;
+                if (EARLY && __builtin_amdgcn_readfirstlane(__float_as_int(Ld[tv])) == __float_as_int(finT)) {
+                    int v = tv, pv = Li[tv], st = 0;
+                    bool ok = true;
+                    while (ok && v != su) {
+                        int mine = -1;
+                        for (int k = 0; k < 64 && v != su; k++, st++) {
+                            const int pd = pv & 0xf;
+                            if (!pd || st >= cells) { ok = false; break; }
+                            v -= __builtin_amdgcn_readlane(doff, pd - 1);
+                            if (lane == k) mine = v;
+                            pv = Li[v];
+                        }
+                        if (ok && __ballot(mine >= 0 && Ld[mine] != gfin[mine])) ok = false;
+                    }
+                    // drain the walk's LDS reads here: left pending on any exit of this block, they make
+                    // the compiler wait for every LDS access at the loop's back edge on the common
+                    // (no-check) path too
+                    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+                    if (ok) { early = true; break; }
+                    lim = pops + gap;  // not yet: look again later, at doubling intervals (a failed walk
+                    gap *= 2;          // costs ~a chain's length of LDS rounds)
                 }
-                if (ok) { early = true; break; }
-                next_check = pops + 64;  // not yet: look again a little later
+                lim = lim < SIMAPS_POP_CAP ? lim : SIMAPS_POP_CAP;
             }
-        }
         if (lane == 0) {
             STAMP_VAL(7, pops);  // (stamp build: tools/path_bench.py reports ns per pop)
             if (count > 0 && !early) sh.fault |= SIMAPS_FAULT_ROUNDS;  // the pop cap stopped a live queue
@@ -2879,9 +2908,9 @@ __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry g
                                                    const uint8_t *__restrict__ occupancy,
                                                    const double *__restrict__ sources, const double *__restrict__ targets,
                                                    int max_pts, double *__restrict__ out_xy, int *__restrict__ out_n,
-                                                   unsigned *fault)
+                                                   float *scratch, unsigned *fault)
 {
-    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS, EARLY>()];
+    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS>()];
     PathHdr &sh = *reinterpret_cast<PathHdr *>(smem);
     SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_PS);
     const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -2924,7 +2953,8 @@ __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry g
     if (tid == 0) STAMP_NB(1);
     snap_sources(sh, S, 2, g);
     const uint16_t *outp;
-    const int cnt = path_core<CELLS, EARLY>(sh, S, smem + OFF_PA, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE, outp);
+    const int cnt = path_core<CELLS, EARLY>(sh, S, smem + OFF_PA, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE,
+                                            EARLY ? scratch + (size_t)n * CELLS : nullptr, outp);
     if (tid < 64) {
         // (7) positions (envs.py:2494-2503); path[0] / path[-1] replaced by the given positions
         if (cnt < 2) {
@@ -2955,9 +2985,9 @@ __global__ void __launch_bounds__(PNT) grid_path_kernel(int H, int W, const uint
                                                         const int32_t *__restrict__ sources,
                                                         const int32_t *__restrict__ targets, int wi0, int wj0, int wh,
                                                         int ww, int max_pts, int32_t *__restrict__ out_ij,
-                                                        int32_t *__restrict__ out_n, unsigned *fault)
+                                                        int32_t *__restrict__ out_n, float *scratch, unsigned *fault)
 {
-    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS, EARLY>()];
+    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS>()];
     PathHdr &sh = *reinterpret_cast<PathHdr *>(smem);
     SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_PS);
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2991,7 +3021,8 @@ __global__ void __launch_bounds__(PNT) grid_path_kernel(int H, int W, const uint
         return;
     }
     const uint16_t *outp;
-    const int cnt = path_core<CELLS, EARLY>(sh, S, smem + OFF_PA, H, W, true, LINE_GRID_ONE, outp);
+    const int cnt = path_core<CELLS, EARLY>(sh, S, smem + OFF_PA, H, W, true, LINE_GRID_ONE,
+                                            EARLY ? scratch + (size_t)b * CELLS : nullptr, outp);
     if (tid < 64) {
         if (cnt > max_pts) {
             if (lane == 0) out_n[b] = -cnt;  // caller's buffer too small
@@ -3309,6 +3340,7 @@ __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
 #include <cstring>
 #include <atomic>
 #include <mutex>
+#include <vector>
 
 namespace {
 thread_local char g_err[512] = "";
@@ -3410,22 +3442,57 @@ Geometry make_geometry()
 }
 
 // Path kernel choice: the early-exit variant (SSSP fixpoint first, then the SPFA only until the target's
-// parent chain is final) holds fewer queries per CU (LDS: 2 instead of 4 in small rooms, 1 instead of
-// 2 in large ones), so it is taken while every query of the launch is resident at once, where each
-// query's latency is the launch's; simaps_path_mode forces either.
+// parent chain is final) unless simaps_path_mode(1) forces the compact one.  Same LDS footprint and
+// the same pop loop, so it pays only its sweeps (~15 us small rooms, ~26 us large) and chain checks:
+// measured 0.7-1.05x the compact launch time for targets across the room and 0.5-0.95x for targets
+// in the robot's local map (the reference's action space), DESIGN.md section 5.
 std::atomic<int> g_path_mode{0};
-bool path_early(int n, bool small)
+bool path_early(int /*n*/, bool /*small*/)
 {
-    const int mode = g_path_mode.load();
-    if (mode) return mode == 2;
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0, c = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-            cus = c;
-        if (cus <= 0) cus = 256;
+    return g_path_mode.load() != 1;
+}
+
+// Device scratch of the early-exit path kernels (the SSSP fixpoint, CELLS f32 per query), one buffer
+// per (device, stream): launches on one stream are ordered, so its buffer is never shared by two live
+// kernels.  Grown (never shrunk) after the stream drains; while the stream is being captured into a
+// graph it cannot grow, and the caller then launches the compact variant (same results) instead.
+struct PathScratch {
+    int dev;
+    hipStream_t st;
+    void *p;
+    size_t bytes;
+};
+std::mutex g_scratch_mu;
+std::vector<PathScratch> g_scratch;
+float *path_scratch(hipStream_t st, size_t bytes)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(g_scratch_mu);
+    PathScratch *e = nullptr;
+    for (auto &x : g_scratch)
+        if (x.dev == dev && x.st == st) e = &x;
+    if (e && e->bytes >= bytes) return (float *)e->p;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
+    if (!e) {
+        g_scratch.push_back(PathScratch{dev, st, nullptr, 0});
+        e = &g_scratch.back();
     }
-    return n <= (small ? 2 : 1) * cus;
+    if (e->p) {
+        if (hipStreamSynchronize(st) != hipSuccess) return nullptr;  // its last kernel may still read it
+        (void)hipFree(e->p);
+        e->p = nullptr;
+        e->bytes = 0;
+    }
+    size_t n = (size_t)1 << 20;
+    while (n < bytes) n *= 2;
+    if (hipMalloc(&e->p, n) != hipSuccess) {
+        e->p = nullptr;
+        return nullptr;
+    }
+    e->bytes = n;
+    return (float *)e->p;
 }
 
 int check_cfg(const simaps_config *c)
@@ -3607,10 +3674,11 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
     const Geometry geo = make_geometry();
     const bool small = (cfg->room_h + 2) * ((cfg->room_w + 2) | 1) <= PATH_SMALL_CELLS;
     const hipStream_t st = (hipStream_t)stream;
+    float *scratch = path_early(N, small) ? path_scratch(st, (size_t)N * SIMAPS_MAX_ROOM_CELLS * sizeof(float)) : nullptr;
 #define SIMAPS_PATH_LAUNCH(C, E)                                                                       \
     hipLaunchKernelGGL((path_kernel<C, E>), dim3(N), dim3(PNT), 0, st, *cfg, geo, agents, envs, robots, occupancy, sources, \
-                       targets, max_points, out_xy, out_count, g_fault_dev)
-    if (path_early(N, small)) {
+                       targets, max_points, out_xy, out_count, scratch, g_fault_dev)
+    if (scratch) {
         if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, true);
         else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true);
     } else {
@@ -3677,10 +3745,11 @@ int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *s
     if (const int rc = pending_faults()) return rc;
     const bool small = (wh + 2) * ((ww + 2) | 1) <= PATH_SMALL_CELLS;
     const hipStream_t st = (hipStream_t)stream;
+    float *scratch = path_early(B, small) ? path_scratch(st, (size_t)B * SIMAPS_MAX_ROOM_CELLS * sizeof(float)) : nullptr;
 #define SIMAPS_GRID_PATH_LAUNCH(C, E)                                                                  \
     hipLaunchKernelGGL((grid_path_kernel<C, E>), dim3(B), dim3(PNT), 0, st, H, W, grids, sources, targets, wi0, wj0, wh, \
-                       ww, max_points, out_ij, out_count, g_fault_dev)
-    if (path_early(B, small)) {
+                       ww, max_points, out_ij, out_count, scratch, g_fault_dev)
+    if (scratch) {
         if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, true);
         else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true);
     } else {

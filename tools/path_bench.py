@@ -69,6 +69,7 @@ def case(cfg, envs, steps, mode=0, targets='across'):
         out.update({'spfa_queries': int(full.sum()), 'spfa_us_median': float(np.median(spfa_us)),
                     'pops_median': float(np.median(pops)),
                     'sweep_rounds_median': float(np.median(st[full, 8])) if mode == 2 else None,
+                    'sweeps_us_median': float(np.median((st[full, 10] - st[full, 2]) / 100.0)) if mode == 2 else None,
                     'ns_per_pop_median': float(np.median(spfa_us * 1e3 / np.maximum(pops, 1))),
                     'query_us_median': float(np.median((st[full, 6] - st[full, 0]) / 100.0))})
     print(json.dumps(out), flush=True)
