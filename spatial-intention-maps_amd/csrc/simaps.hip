@@ -991,9 +991,9 @@ struct SweepOut {
     int steps;  // lines processed (diagnostics)
 };
 
-// Sweep steps t0 .. (early exit past tmax) of a line space of len lines.
+// Sweep steps t0 .. t1 - 1 (early exit past tmax) of a line space of len lines.
 template <int DIR, int CPL, int PWC>
-__device__ SweepOut sweep_asm(lds_float *__restrict__ D, int len, int span, int t0, int tmax)
+__device__ SweepOut sweep_asm(lds_float *__restrict__ D, int len, int span, int t0, int tmax, int t1)
 {
     static_assert(PWC > 0, "compile-time pitch");
     constexpr bool VERT = DIR < 2, FWD = (DIR & 1) == 0;
@@ -1009,7 +1009,7 @@ __device__ SweepOut sweep_asm(lds_float *__restrict__ D, int len, int span, int 
     float one = act ? 1.0f : INFINITY, s2 = act ? SQRT2F : INFINITY, X = act ? INFINITY : -INFINITY;
     float p0 = INFINITY, p1 = INFINITY, acc = 0.0f, accg = 0.0f;
     float r00, r01, r10, r11, r20, r21, r30, r31, a, b, c, d, e, f;
-    const int lenr = len - t0;                 // steps from t0 to the end
+    const int lenr = t1 - t0;                  // steps from t0 to the end
     int ng = lenr > P ? (lenr - P) / P : 0;    // steady-state groups after the first
     const int rem = lenr > P ? (lenr - P) % P : 0;
     const int txm3 = tmax - t0 - 3;
@@ -1050,7 +1050,7 @@ __device__ SweepOut sweep_asm(lds_float *__restrict__ D, int len, int span, int 
               [gstep] "i"((FWD ? P : -P) * SL * 4)
             : "memory", "scc");
     }
-    return SweepOut{__ballot(acc < 0.0f), t0 + imin, min(t0 + imax, len - 1), min(tg + 4, lenr)};
+    return SweepOut{__ballot(acc < 0.0f), t0 + imin, min(t0 + imax, t1 - 1), min(tg + 4, lenr)};
 }
 #undef SWA_S2
 #undef SWA_BODY
@@ -1100,8 +1100,12 @@ __device__ __forceinline__ void mark_range(uint64_t *m, int a, int b)  // bits a
     mark_lines(m, a <= 63 ? bits64(a, min(b, 63)) : 0ull, b >= 64 ? bits64(max(a, 64) - 64, b - 64) : 0ull);
 }
 
-// One sweep of direction dir_in over source dm's array; true if it improved a cell.
-__device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_in, uint64_t (*dm)[2], int &steps)
+// One sweep of direction dir_in over source dm's array; true if it improved a cell.  With nparts > 1
+// (compile-time pitch only) the sweep covers part `part` of the direction's steps: it relaxes out of
+// the lines of steps [s0, s1) (their dirty bits are its own) and into the line of step s1, which the
+// next part relaxes out of -- marked dirty for it when this part improved that line.
+__device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_in, uint64_t (*dm)[2], int &steps,
+                                      int part = 0, int nparts = 1)
 {
     lds_float *D = (lds_float *)Dg;  // the distance arrays live in LDS: keep ds_* addressing
     // wave-uniform loop bounds: scalar loop control, no exec-mask merges at the back edge
@@ -1109,13 +1113,25 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
     h = __builtin_amdgcn_readfirstlane(h);
     w = __builtin_amdgcn_readfirstlane(w);
     pw = __builtin_amdgcn_readfirstlane(pw);
+    part = __builtin_amdgcn_readfirstlane(part);
+    nparts = __builtin_amdgcn_readfirstlane(nparts);
     const bool vert = dir < 2, fwd = (dir & 1) == 0;
     const int len = vert ? h : w, span = vert ? w : h;
     const int lane = threadIdx.x & 63;
+    // own steps [s0, s1) -> own dirty bits [b0, b1] (step t is line fwd ? t + 1 : len - t, bit line - 1)
+    const int s0 = part * len / nparts, s1 = (part + 1) * len / nparts;
+    const int b0 = fwd ? s0 : len - s1, b1 = fwd ? s1 - 1 : len - 1 - s0;
     uint64_t mlo = 0, mhi = 0;
     if (lane == 0) {  // snapshot-and-clear this direction's dirty lines (before any read of the array)
-        mlo = __hip_atomic_exchange(&dm[dir][0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        mhi = __hip_atomic_exchange(&dm[dir][1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (nparts == 1) {
+            mlo = __hip_atomic_exchange(&dm[dir][0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            mhi = __hip_atomic_exchange(&dm[dir][1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            const uint64_t klo = b0 <= 63 ? bits64(b0, min(b1, 63)) : 0ull;
+            const uint64_t khi = b1 >= 64 ? bits64(max(b0, 64) - 64, b1 - 64) : 0ull;
+            if (klo) mlo = __hip_atomic_fetch_and(&dm[dir][0], ~klo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & klo;
+            if (khi) mhi = __hip_atomic_fetch_and(&dm[dir][1], ~khi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & khi;
+        }
     }
     mlo = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(mlo >> 32)) << 32) |
           (uint32_t)__builtin_amdgcn_readfirstlane((int)mlo);
@@ -1125,20 +1141,25 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
     const int blo = mlo ? __builtin_ctzll(mlo) : 64 + __builtin_ctzll(mhi);
     const int bhi = mhi ? 127 - __builtin_clzll(mhi) : 63 - __builtin_clzll(mlo);
     const int t0 = fwd ? blo : len - 1 - bhi, tmax = fwd ? bhi : len - 1 - blo;  // step t: line fwd ? t + 1 : len - t
+    const int t1 = min(s1 + 1, len);
     if (pw == 95
     ) {  // every BASELINE room is 92 columns wide (pitch 95): the asm loop with immediate offsets
         SweepOut o;
         switch (dir) {
-        case 0: o = sweep_asm<0, 2, 95>(D, h, w, t0, tmax); break;
-        case 1: o = sweep_asm<1, 2, 95>(D, h, w, t0, tmax); break;
-        case 2: o = h <= 63 ? sweep_asm<2, 1, 95>(D, w, h, t0, tmax) : sweep_asm<2, 2, 95>(D, w, h, t0, tmax); break;
-        default: o = h <= 63 ? sweep_asm<3, 1, 95>(D, w, h, t0, tmax) : sweep_asm<3, 2, 95>(D, w, h, t0, tmax); break;
+        case 0: o = sweep_asm<0, 2, 95>(D, h, w, t0, tmax, t1); break;
+        case 1: o = sweep_asm<1, 2, 95>(D, h, w, t0, tmax, t1); break;
+        case 2: o = h <= 63 ? sweep_asm<2, 1, 95>(D, w, h, t0, tmax, t1) : sweep_asm<2, 2, 95>(D, w, h, t0, tmax, t1); break;
+        default: o = h <= 63 ? sweep_asm<3, 1, 95>(D, w, h, t0, tmax, t1) : sweep_asm<3, 2, 95>(D, w, h, t0, tmax, t1); break;
         }
         steps += o.steps;
         if (!o.lanes) return false;
         if (lane == 0) {
             const int a = fwd ? o.imin : len - 1 - o.imax, b = fwd ? o.imax : len - 1 - o.imin;
             mark_range(dm[dir ^ 1], max(a, 0), min(b, 127));
+            if (s1 < len && o.imax >= s1) {  // improved the next part's first line: its to relax out of
+                const int bit = fwd ? s1 : len - 1 - s1;
+                mark_range(dm[dir], bit, bit);
+            }
             const int cpl = span <= 63 ? 1 : 2;
             const uint64_t lo = cpl == 1 ? o.lanes : spread2((uint32_t)o.lanes);
             const uint64_t hi = cpl == 1 ? 0ull : spread2((uint32_t)(o.lanes >> 32));
@@ -1321,13 +1342,58 @@ __device__ __forceinline__ void sssp_max(Shared &sh, const float *dist, int nsrc
     sssp_max_final(sh, nsrc, g.nw, scale, g.t);
 }
 
+// Split sweeps (one source, compile-time pitch; the single-kernel users, whose other waves idle): the
+// two directions along the longer room side get KL waves each, the other two KS each, every wave one
+// part of its direction's steps (sweep(..., part, nparts)).  Shorter sweeps per round, more rounds.
+// Measured (tools/sssp_split_ab.sh, profiles/r3g_sssp_split_ab.jsonl): KL = KS = 2 takes 2-7 % off
+// simaps_sssp_grid and simaps_sp_distance; KL = 2 alone, 3 alone, or 4 / 2 are slower than no split
+// (their extra rounds outweigh the shorter ones).
+#ifndef SIMAPS_SSSP_SPLIT_L
+#define SIMAPS_SSSP_SPLIT_L 2
+#endif
+#ifndef SIMAPS_SSSP_SPLIT_S
+#define SIMAPS_SSSP_SPLIT_S 2
+#endif
+constexpr int SPLIT_WAVES = 2 * (SIMAPS_SSSP_SPLIT_L + SIMAPS_SSSP_SPLIT_S);
+static_assert(SPLIT_WAVES <= NT / 64, "split sweeps: one wave per part");
+__device__ __forceinline__ void sssp_rounds_split(Shared &sh, float *dist)
+{
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const int h = sh.h, w = sh.w, pw = sssp_pitch(w);
+    const int max_rounds = h * w + 16;
+    const Group gs{tid, 64 * SPLIT_WAVES, sh.bar[2], SPLIT_WAVES};
+    const int longd = w >= h ? 2 : 0;  // columns (right / left) sweep the w lines of a wide room
+    const bool lw = wave < 2 * SIMAPS_SSSP_SPLIT_L;
+    const int q = lw ? wave : wave - 2 * SIMAPS_SSSP_SPLIT_L;
+    const int dir = (lw ? longd : 2 - longd) + (q & 1), part = q >> 1;
+    const int nparts = lw ? SIMAPS_SSSP_SPLIT_L : SIMAPS_SSSP_SPLIT_S;
+    if (lw) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(2);
+    int *changed = sh.changed[0];
+    int steps = 0;
+    for (int round = 0;; round++) {
+        if (tid == 0) changed[(round + 1) % 3] = 0;
+        if (sh.src_ok[0] && sweep(dist, h, w, pw, dir, sh.dirty[0], steps, part, nparts) && (tid & 63) == 0)
+            changed[round % 3] = 1;
+        gs.sync();
+        if (!changed[round % 3] || round >= max_rounds) {
+            if (tid == 0)
+                __hip_atomic_fetch_max(&sh.rounds, round >= max_rounds ? 1 << 20 : round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            break;
+        }
+    }
+    __builtin_amdgcn_s_setprio(0);
+}
+
 // all threads (single-kernel users: sssp_grid_kernel, sp_distance_kernel)
 __device__ __forceinline__ void sssp(Shared &sh, SsspScratch &S, float *dist, int nsrc)
 {
     if (threadIdx.x < 16) (&sh.bar[0][0])[threadIdx.x] = 0u;
     sssp_init(sh, S, dist, nsrc, Group{(int)threadIdx.x, NT, nullptr, NT / 64});
     const int wave = threadIdx.x >> 6;
-    if (wave < 4 * nsrc) sssp_rounds(sh, dist, nsrc, Group{(int)threadIdx.x, 256 * nsrc, sh.bar[0], 4 * nsrc});
+    if (SPLIT_WAVES > 4 && nsrc == 1 && sssp_pitch(sh.w) == 95) {
+        if (wave < SPLIT_WAVES) sssp_rounds_split(sh, dist);
+    } else if (wave < 4 * nsrc) sssp_rounds(sh, dist, nsrc, Group{(int)threadIdx.x, 256 * nsrc, sh.bar[0], 4 * nsrc});
     lds_barrier();
     sssp_finish(sh, dist, nsrc, Group{(int)threadIdx.x, NT, nullptr, NT / 64});
     lds_barrier();
@@ -3454,8 +3520,9 @@ bool path_early(int /*n*/, bool /*small*/)
 
 // Device scratch of the early-exit path kernels (the SSSP fixpoint, CELLS f32 per query), one buffer
 // per (device, stream): launches on one stream are ordered, so its buffer is never shared by two live
-// kernels.  Grown (never shrunk) after the stream drains; while the stream is being captured into a
-// graph it cannot grow, and the caller then launches the compact variant (same results) instead.
+// kernels.  Grown (never shrunk) after the stream drains.  A launch being captured into a graph gets
+// none -- the graph would keep the pointer past a later growth -- and takes the compact kernels (same
+// results) instead.
 struct PathScratch {
     int dev;
     hipStream_t st;
@@ -3467,14 +3534,15 @@ std::vector<PathScratch> g_scratch;
 float *path_scratch(hipStream_t st, size_t bytes)
 {
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipGetDevice(&dev) != hipSuccess || hipStreamIsCapturing(st, &cap) != hipSuccess ||
+        cap != hipStreamCaptureStatusNone)
+        return nullptr;
     std::lock_guard<std::mutex> lock(g_scratch_mu);
     PathScratch *e = nullptr;
     for (auto &x : g_scratch)
         if (x.dev == dev && x.st == st) e = &x;
     if (e && e->bytes >= bytes) return (float *)e->p;
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
     if (!e) {
         g_scratch.push_back(PathScratch{dev, st, nullptr, 0});
         e = &g_scratch.back();

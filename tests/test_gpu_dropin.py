@@ -588,3 +588,43 @@ def test_periodic_remap_successive_frames(V):
     g = [gi for gi, grp in enumerate(vector_env.robot_groups(sc)) if a in grp][0]
     x = st[e][g][vector_env.robot_groups(sc)[g].index(a)]
     assert _bitwise(x, O.agent_state(moved, a))
+
+
+def test_path_launch_in_graph_capture(V):
+    """A path launch captured into a graph gets no early-exit scratch (the graph would keep its pointer
+    past a later growth) and runs the compact kernel: the replay equals the eager launches of both
+    kernels, in a maze room with long detours and local-map targets."""
+    synthetic, _ = V
+    from simaps import _lib, batch
+    scenes = [synthetic.make_scene('lifting_4-large_doors', 70 + e) for e in range(4)]
+    b = batch.StateBatch(scenes)
+    rs = np.random.RandomState(3)
+    rl, rw = scenes[0]['room_length'], scenes[0]['room_width']
+    psrc = np.array([scenes[e]['robots'][a]['position'][:2] for e, a in b.agents])
+    ptgt = psrc + rs.uniform(-0.5, 0.5, psrc.shape)
+    ptgt[:, 0] = np.clip(ptgt[:, 0], -rl / 2 + 0.02, rl / 2 - 0.02)
+    ptgt[:, 1] = np.clip(ptgt[:, 1], -rw / 2 + 0.02, rw / 2 - 0.02)
+    src, tgt = torch.as_tensor(psrc).cuda(), torch.as_tensor(ptgt).cuda()
+    prev = _lib.lib.simaps_path_mode(0)
+    try:
+        eager = {}
+        for mode in (1, 0):
+            _lib.lib.simaps_path_mode(mode)
+            xy, cnt = b.launch_shortest_paths(src, tgt)
+            eager[mode] = (xy.cpu().numpy(), cnt.cpu().numpy())
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            gxy, gcnt = b.launch_shortest_paths(src, tgt)
+        gxy.fill_(np.nan)
+        g.replay()
+        torch.cuda.synchronize()
+        _lib.check_faults()
+        got = (gxy.cpu().numpy(), gcnt.cpu().numpy())
+    finally:
+        _lib.lib.simaps_path_mode(prev)
+    for xy, cnt in eager.values():
+        assert np.array_equal(cnt, got[1])
+        for n, c in enumerate(cnt):
+            assert c >= 2 and np.array_equal(xy[n, :c], got[0][n, :c]), n
+    assert (got[1] > 2).sum() >= 3  # some detours

@@ -290,6 +290,39 @@ def test_sssp_grid_random(S):
         assert _bitwise(out[0], g['rand_img_%d' % q]), q
 
 
+def _room_grids(n, h, w, seed):
+    """n uint8 grids [h + 4, w + 4] whose free cells lie in the window (2, 2, h, w): a divider wall
+    with one gap (long detours) and random blocks; one random free source cell each."""
+    rs = np.random.RandomState(seed)
+    grids, srcs = [], []
+    for _ in range(n):
+        g = np.zeros((h + 4, w + 4), np.uint8)
+        g[2:2 + h, 2:2 + w] = 1
+        c = 2 + w // 2 + rs.randint(-8, 9)
+        g[2:2 + h, c] = 0
+        gap = 2 + rs.randint(0, h - 6)
+        g[gap:gap + 5, c] = 1
+        for _ in range(12):
+            i, j = 2 + rs.randint(0, h - 4), 2 + rs.randint(0, w - 4)
+            g[i:i + rs.randint(1, 5), j:j + rs.randint(1, 5)] = 0
+        fr = np.argwhere(g > 0)
+        grids.append(g)
+        srcs.append(tuple(int(x) for x in fr[rs.randint(len(fr))]))
+    return np.stack(grids), srcs
+
+
+@pytest.mark.parametrize('h', [44, 92])
+def test_sssp_grid_room_width_92(S, h):
+    """Rooms 92 cells wide (the BASELINE rooms' pitch 95: the sweeps' compile-time asm loops, and the
+    split-sweep variant when built with SIMAPS_SSSP_SPLIT_L / _S), with a divider: bitwise the SPFA."""
+    batch, K, synthetic = S
+    grids, srcs = _room_grids(6, h, 92, 40 + h)
+    out = batch.sssp_grid(torch.from_numpy(grids).cuda(), torch.tensor(srcs, dtype=torch.int32),
+                          window=(2, 2, h, 92)).cpu().numpy()
+    for q in range(len(srcs)):
+        assert _bitwise(out[q], O.spfa_image(grids[q], srcs[q])), q
+
+
 @pytest.mark.parametrize('mode', ['random', 'eighths_and_negzero'])
 def test_overhead_values_outside_seg_codes(S, mode):
     """Overhead maps holding values other than the SEG_VALUES codes k/8 (random floats, -0.0, a code
