@@ -593,17 +593,15 @@ def test_periodic_remap_successive_frames(V):
 def test_path_launch_in_graph_capture(V):
     """A path launch captured into a graph gets no early-exit scratch (the graph would keep its pointer
     past a later growth) and runs the compact kernel: the replay equals the eager launches of both
-    kernels, in a maze room with long detours and local-map targets."""
+    kernels, for targets across the divider (detours: the SPFA runs)."""
     synthetic, _ = V
     from simaps import _lib, batch
-    scenes = [synthetic.make_scene('lifting_4-large_doors', 70 + e) for e in range(4)]
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 70 + e) for e in range(8)]
     b = batch.StateBatch(scenes)
     rs = np.random.RandomState(3)
     rl, rw = scenes[0]['room_length'], scenes[0]['room_width']
     psrc = np.array([scenes[e]['robots'][a]['position'][:2] for e, a in b.agents])
-    ptgt = psrc + rs.uniform(-0.5, 0.5, psrc.shape)
-    ptgt[:, 0] = np.clip(ptgt[:, 0], -rl / 2 + 0.02, rl / 2 - 0.02)
-    ptgt[:, 1] = np.clip(ptgt[:, 1], -rw / 2 + 0.02, rw / 2 - 0.02)
+    ptgt = np.stack([rs.uniform(0.05, rl / 2, b.N) * -np.sign(psrc[:, 0]), rs.uniform(-rw / 2, rw / 2, b.N)], -1)
     src, tgt = torch.as_tensor(psrc).cuda(), torch.as_tensor(ptgt).cuda()
     prev = _lib.lib.simaps_path_mode(0)
     try:
@@ -627,4 +625,4 @@ def test_path_launch_in_graph_capture(V):
         assert np.array_equal(cnt, got[1])
         for n, c in enumerate(cnt):
             assert c >= 2 and np.array_equal(xy[n, :c], got[0][n, :c]), n
-    assert (got[1] > 2).sum() >= 3  # some detours
+    assert (got[1] > 2).sum() >= 8  # detours
