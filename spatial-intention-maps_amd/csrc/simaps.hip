@@ -3116,12 +3116,6 @@ __device__ __forceinline__ float dot3f(const float *a, const float *b)
     return (float)((((double)(a[0] * b[0])) + (double)(a[1] * b[1])) + (double)(a[2] * b[2]));
 }
 
-// numpy float32 -> int32 cast (x86 cvttss2si): NaN / out of range -> INT_MIN
-__device__ __forceinline__ int np_f32_to_i32(float v)
-{
-    return (v >= -2147483648.0f && v < 2147483648.0f) ? (int)v : INT32_MIN;
-}
-
 // Two passes, no recomputation and no reset pass:
 //   ingest_points_kernel  grid (chunks of INGEST_PTS camera pixels, frames): each point once -- its
 //                         map pixel, its obstacle bit (occupancy byte store) and its key (monotone z
@@ -3220,6 +3214,17 @@ __device__ __forceinline__ void ingest_load(const float *db, const int32_t *raw,
     }
 }
 
+// np.floor(v).astype(np.int32) then np.clip(., 0, n - 1) (envs.py:2440-2442) of an already floored
+// float32 f: the hardware convert saturates and takes NaN to 0, med3 clamps, and a value >= 2^31
+// (INT32_MIN in numpy, x86 cvttss2si) clips to 0
+__device__ __forceinline__ int ingest_clip(float f, int n)
+{
+    int c;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(c) : "v"(f));
+    c = min(max(c, 0), n - 1);  // (v_med3_i32)
+    return f >= 2147483648.0f ? 0 : c;
+}
+
 // grid (chunks, frames)
 __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     simaps_config cfg, simaps_camera cam, const simaps_agent *__restrict__ agents,
@@ -3228,7 +3233,10 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     unsigned long long *__restrict__ keys, unsigned *__restrict__ boxes)
 {
     __shared__ unsigned long long win[INGEST_WIN];
-    __shared__ float F[12], pxT[INGEST_MAX_WC], pyT[INGEST_MAX_ROWS];
+    // per chunk: A[c][j] = right[c] * pixel_x(j) + principal[c] (column j), Bt[c][i] = up[c] * pixel_y(i)
+    // (row row0 + i): a point's ray t[c] = A[c][j] + Bt[c][i], the same float32 operations in the same
+    // order as per point (capture_image, envs.py:1946-1950)
+    __shared__ float A[3][INGEST_MAX_WC], Bt[3][INGEST_MAX_ROWS];
     __shared__ int box[4];  // min i, -max i, min j, -max j of the chunk's map pixels
     const int n = blockIdx.y, tid = threadIdx.x;
     const int H = cfg.H, W = cfg.W, Hc = cam.height_px, Wc = cam.width_px, NP = Hc * Wc;
@@ -3243,58 +3251,72 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     const simaps_seg_ids ids = seg_ids[ag.env];
     const float c1 = (float)(cam.far_m * cam.near_m), cfar = (float)cam.far_m, cfn = (float)(cam.far_m - cam.near_m);
     const float cx2 = (float)cam.cx2, cy2 = (float)cam.cy2;
-    // per chunk once: the camera frame (one lane) and the pixel_x / pixel_y tables of its columns and
-    // rows (envs.py:1946-1947; the same float32 divisions every point would repeat)
+    // the camera frame, in every wave (uniform: no LDS round trip and no barrier before the tables)
+    float F[12];
+    camera_frame(cam_params + 9 * (size_t)n, F);
+#pragma unroll
+    for (int c = 0; c < 12; c++) F[c] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F[c])));
+    // per chunk once: the column and row tables (envs.py:1946-1947; the float32 divisions and products
+    // every point of a column / row would repeat)
     const int row0 = (blockIdx.x * INGEST_PTS) / Wc;
-    if (tid == 0) camera_frame(cam_params + 9 * (size_t)n, F);
     if (tid < 4) box[tid] = INT32_MAX;
-    for (int j = tid; j < Wc; j += INGEST_WG) pxT[j] = cx2 * ((float)j / (float)Wc - 0.5f);
-    if (tid < INGEST_MAX_ROWS) pyT[tid] = cy2 * (0.5f - ((float)(row0 + tid) + 1.0f) / (float)Hc);
+    for (int j = tid; j < Wc; j += INGEST_WG) {
+        const float px = cx2 * ((float)j / (float)Wc - 0.5f);
+#pragma unroll
+        for (int c = 0; c < 3; c++) A[c][j] = F[3 + c] + px * F[9 + c];
+    }
+    if (tid < INGEST_MAX_ROWS) {
+        const float py = cy2 * (0.5f - ((float)(row0 + tid) + 1.0f) / (float)Hc);
+#pragma unroll
+        for (int c = 0; c < 3; c++) Bt[c][tid] = py * F[6 + c];
+    }
     const float h2 = (float)((double)H / 2), w2 = (float)((double)W / 2);
     const size_t base = (size_t)ag.map_slot * H * W;
+    uint8_t *const occ = occupancy + base;
+    // seg * 8 per body id (the reference's float sum of 1/8 multiples < 2 is exact: its integer sum)
+    auto seg8_of = [&](int r) {
+        int v = r == 0 ? 1 : 0;
+        v += (r >= ids.min_obstacle && r <= ids.max_obstacle) ? 2 : 0;
+        v += (ids.has_receptacle && r == ids.receptacle) ? 3 : 0;
+        v += (r >= ids.min_cube && r <= ids.max_cube) ? 4 : 0;
+        return v;
+    };
     {
         __syncthreads();
-        int pix[INGEST_PPT];
+        // Per point, branch-free (a point past the frame's end computes on its zero inputs and is then
+        // dropped by selects: no per-point branch, so the unrolled arrays are never copied at branch
+        // joins): cell[q] = map row << 16 | map column, or -1; key[q] as below.
+        int cell[INGEST_PPT];
         unsigned long long key[INGEST_PPT];
         int imin = INT32_MAX, imax = -1, jmin = INT32_MAX, jmax = -1;
         int i = k0 / Wc, j = k0 - i * Wc;
 #pragma unroll
         for (int q = 0; q < INGEST_PPT; q++, j = (j + 1 == Wc) ? (i++, 0) : j + 1) {
             const int k = k0 + q;
-            pix[q] = -1;
-            key[q] = 0ull;
-            if (k >= NP) continue;
+            const bool valid = k < NP;
             const float dep = c1 / (cfar - cfn * dv[q]);
-            const float px = pxT[j], py = pyT[i - row0];
+            const int ir = i - row0;  // (rows past the frame stay inside the table)
             float p[3];
-            for (int cc = 0; cc < 3; cc++) {
-                float t = F[3 + cc] + px * F[9 + cc];
-                t = t + py * F[6 + cc];
-                p[cc] = F[cc] + dep * t;
-            }
-            const int r = rv[q];
-            float seg = 0.125f * (r == 0 ? 1.0f : 0.0f);
-            seg += 0.25f * ((r >= ids.min_obstacle && r <= ids.max_obstacle) ? 1.0f : 0.0f);
-            if (ids.has_receptacle) seg += 0.375f * (r == ids.receptacle ? 1.0f : 0.0f);
-            seg += 0.5f * ((r >= ids.min_cube && r <= ids.max_cube) ? 1.0f : 0.0f);
-            int pi = np_f32_to_i32(floorf(h2 - p[1] * 96.0f)), pj = np_f32_to_i32(floorf(w2 + p[0] * 96.0f));
-            pi = pi < 0 ? 0 : (pi > H - 1 ? H - 1 : pi);
-            pj = pj < 0 ? 0 : (pj > W - 1 ? W - 1 : pj);
-            pix[q] = pi * W + pj;
-            imin = min(imin, pi), imax = max(imax, pi), jmin = min(jmin, pj), jmax = max(jmax, pj);
-            if (seg == 0.25f) occupancy[base + pix[q]] = 1;  // np.isclose(seg, obstacle) (seg values are exact)
+#pragma unroll
+            for (int c = 0; c < 3; c++) p[c] = F[c] + dep * (A[c][j] + Bt[c][ir]);
+            const int s8 = seg8_of(rv[q]);
+            int pi = ingest_clip(floorf(h2 - p[1] * 96.0f), H), pj = ingest_clip(floorf(w2 + p[0] * 96.0f), W);
+            cell[q] = valid ? (pi << 16) | pj : -1;
+            imin = valid ? min(imin, pi) : imin, imax = valid ? max(imax, pi) : imax;
+            jmin = valid ? min(jmin, pj) : jmin, jmax = valid ? max(jmax, pj) : jmax;
+            if (valid && s8 == 2) occ[(unsigned)__umul24(pi, W) + pj] = 1;  // np.isclose(seg, obstacle) (exact values)
             // np.argsort order by z: float bits made unsigned-monotone, NaN last; equal z -> later pixel
             const unsigned zb = __float_as_uint(p[2]);
             const unsigned zk = p[2] != p[2] ? 0xffffffffu : ((zb & 0x80000000u) ? ~zb : (zb | 0x80000000u));
-            key[q] = ((unsigned long long)zk << 32) | (((unsigned)(k + 1) << 4) | (unsigned)(seg * 8.0f));
+            key[q] = ((unsigned long long)zk << 32) | (((unsigned)(k + 1) << 4) | (unsigned)s8);
         }
         // runs of one map pixel inside the lane: the run's last entry carries the run's max key
 #pragma unroll
-        for (int q = 1; q < INGEST_PPT; q++)
-            if (pix[q] == pix[q - 1] && pix[q] >= 0) {
-                key[q] = key[q] > key[q - 1] ? key[q] : key[q - 1];
-                pix[q - 1] = -1;
-            }
+        for (int q = 1; q < INGEST_PPT; q++) {
+            const bool run = cell[q] == cell[q - 1] && cell[q] >= 0;
+            key[q] = run && key[q - 1] > key[q] ? key[q - 1] : key[q];
+            cell[q - 1] = run ? -1 : cell[q - 1];
+        }
         // the chunk's box of map pixels
         imin = wave_min(imin), imax = wave_max(imax), jmin = wave_min(jmin), jmax = wave_max(jmax);
         if ((tid & 63) == 0 && imax >= 0)
@@ -3308,8 +3330,8 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
         if (area > INGEST_WIN) {
             // box past the window (a forward camera's far rows: ~2-3 points per pixel, spread wide;
             // global atomics per run instead measured 3 us more per 256 frames):
-            // a direct-mapped table of HS (pixel tag, key) slots in the window's LDS.
-            // Each pixel's tag is written by its points (any one wins); points whose pixel owns the
+            // a direct-mapped table of HS (cell tag, key) slots in the window's LDS.
+            // Each cell's tag is written by its points (any one wins); points whose cell owns the
             // slot max-reduce there, the others (collisions) go straight to the global key map;
             // then one global atomic per used slot.
             constexpr int HS = INGEST_WIN * 2 / 3;  // keys (8 B) + tags (4 B) in the 32 KB window
@@ -3319,19 +3341,19 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
             __syncthreads();
 #pragma unroll
             for (int q = 0; q < INGEST_PPT; q++)
-                if (pix[q] >= 0) ht[(unsigned)pix[q] % HS] = pix[q];
+                if (cell[q] >= 0) ht[(unsigned)cell[q] % HS] = cell[q];
             __syncthreads();
 #pragma unroll
             for (int q = 0; q < INGEST_PPT; q++)
-                if (pix[q] >= 0) {
-                    const int h = (unsigned)pix[q] % HS;
-                    if (ht[h] == pix[q]) atomicMax(&hk[h], key[q]);
-                    else atomicMax(&keys[base + pix[q]], key[q]);
+                if (cell[q] >= 0) {
+                    const int h = (unsigned)cell[q] % HS;
+                    if (ht[h] == cell[q]) atomicMax(&hk[h], key[q]);
+                    else atomicMax(&keys[base + (cell[q] >> 16) * W + (cell[q] & 0xffff)], key[q]);
                 }
             __syncthreads();
             for (int e = tid; e < HS; e += INGEST_WG) {
                 const unsigned long long v = hk[e];
-                if (v) atomicMax(&keys[base + ht[e]], v);
+                if (v) atomicMax(&keys[base + (ht[e] >> 16) * W + (ht[e] & 0xffff)], v);
             }
             return;
         }
@@ -3339,17 +3361,17 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < INGEST_PPT; q++)
-            if (pix[q] >= 0) {
-                const int pi = pix[q] / W, pj = pix[q] - pi * W;
-                atomicMax(&win[(pi - bi) * bw + (pj - bj)], key[q]);
-            }
+            if (cell[q] >= 0) atomicMax(&win[((cell[q] >> 16) - bi) * bw + ((cell[q] & 0xffff) - bj)], key[q]);
         __syncthreads();
+        // the window's entries e = tid + m * INGEST_WG as (row, column) of the box, stepped without
+        // a division per entry
+        const int qs = INGEST_WG / bw, rs = INGEST_WG - qs * bw;
+        int di = tid / bw, dj = tid - di * bw;
         for (int e = tid; e < area; e += INGEST_WG) {
             const unsigned long long v = win[e];
-            if (v) {
-                const int di = e / bw;
-                atomicMax(&keys[base + (size_t)((bi + di) * W + bj + (e - di * bw))], v);
-            }
+            if (v) atomicMax(&keys[base + (size_t)((bi + di) * W + bj + dj)], v);
+            di += qs, dj += rs;
+            if (dj >= bw) dj -= bw, di++;
         }
     }
 }
