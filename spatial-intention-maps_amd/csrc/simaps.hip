@@ -42,6 +42,8 @@
 // (see geom.h for the one explicit fma).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "geom.h"
 #include "simaps.h"
 
@@ -3214,6 +3216,20 @@ __device__ __forceinline__ void ingest_load(const float *db, const int32_t *raw,
     }
 }
 
+// min (is_min) or max over the wave by DPP (quad, half-row and row mirrors, then the row
+// broadcasts); lanes of rows a broadcast leaves out keep their value (op(v, v) = v)
+__device__ __forceinline__ int wave_reduce_dpp(int v, bool is_min)
+{
+    auto op = [&](int a, int b) { return is_min ? min(a, b) : max(a, b); };
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0xb1, 0xf, 0xf, false));   // quad_perm [1, 0, 3, 2]
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x4e, 0xf, 0xf, false));   // quad_perm [2, 3, 0, 1]
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xf, 0xf, false));  // row_mirror: the row's result
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));  // row_bcast15 -> rows 1, 3
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));  // row_bcast31 -> rows 2, 3
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 // np.floor(v).astype(np.int32) then np.clip(., 0, n - 1) (envs.py:2440-2442) of an already floored
 // float32 f: the hardware convert saturates and takes NaN to 0, med3 clamps, and a value >= 2^31
 // (INT32_MIN in numpy, x86 cvttss2si) clips to 0
@@ -3236,7 +3252,7 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     // per chunk: A[c][j] = right[c] * pixel_x(j) + principal[c] (column j), Bt[c][i] = up[c] * pixel_y(i)
     // (row row0 + i): a point's ray t[c] = A[c][j] + Bt[c][i], the same float32 operations in the same
     // order as per point (capture_image, envs.py:1946-1950)
-    __shared__ float A[3][INGEST_MAX_WC], Bt[3][INGEST_MAX_ROWS];
+    __shared__ float A[3][INGEST_MAX_WC], Bt[3][INGEST_MAX_ROWS], Fs[3];
     __shared__ int box[4];  // min i, -max i, min j, -max j of the chunk's map pixels
     const int n = blockIdx.y, tid = threadIdx.x;
     const int H = cfg.H, W = cfg.W, Hc = cam.height_px, Wc = cam.width_px, NP = Hc * Wc;
@@ -3251,24 +3267,27 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     const simaps_seg_ids ids = seg_ids[ag.env];
     const float c1 = (float)(cam.far_m * cam.near_m), cfar = (float)cam.far_m, cfn = (float)(cam.far_m - cam.near_m);
     const float cx2 = (float)cam.cx2, cy2 = (float)cam.cy2;
-    // the camera frame, in every wave (uniform: no LDS round trip and no barrier before the tables)
-    float F[12];
-    camera_frame(cam_params + 9 * (size_t)n, F);
-#pragma unroll
-    for (int c = 0; c < 12; c++) F[c] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F[c])));
-    // per chunk once: the column and row tables (envs.py:1946-1947; the float32 divisions and products
-    // every point of a column / row would repeat)
+    // per chunk once, by wave 0 alone (the pass is VALU-issue bound: the other waves' issue slots
+    // go to other chunks): the camera frame and the column and row tables (envs.py:1932-1947; the
+    // float32 divisions and products every point of a column / row would repeat)
     const int row0 = (blockIdx.x * INGEST_PTS) / Wc;
-    if (tid < 4) box[tid] = INT32_MAX;
-    for (int j = tid; j < Wc; j += INGEST_WG) {
-        const float px = cx2 * ((float)j / (float)Wc - 0.5f);
+    if (tid < 64) {
+        float F[12];
+        camera_frame(cam_params + 9 * (size_t)n, F);
 #pragma unroll
-        for (int c = 0; c < 3; c++) A[c][j] = F[3 + c] + px * F[9 + c];
-    }
-    if (tid < INGEST_MAX_ROWS) {
-        const float py = cy2 * (0.5f - ((float)(row0 + tid) + 1.0f) / (float)Hc);
+        for (int c = 0; c < 12; c++) F[c] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F[c])));
+        for (int j = tid; j < Wc; j += 64) {
+            const float px = cx2 * ((float)j / (float)Wc - 0.5f);
 #pragma unroll
-        for (int c = 0; c < 3; c++) Bt[c][tid] = py * F[6 + c];
+            for (int c = 0; c < 3; c++) A[c][j] = F[3 + c] + px * F[9 + c];
+        }
+        if (tid < INGEST_MAX_ROWS) {
+            const float py = cy2 * (0.5f - ((float)(row0 + tid) + 1.0f) / (float)Hc);
+#pragma unroll
+            for (int c = 0; c < 3; c++) Bt[c][tid] = py * F[6 + c];
+        }
+        if (tid < 3) Fs[tid] = F[tid];
+        if (tid < 4) box[tid] = INT32_MAX;
     }
     const float h2 = (float)((double)H / 2), w2 = (float)((double)W / 2);
     const size_t base = (size_t)ag.map_slot * H * W;
@@ -3283,42 +3302,53 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     };
     {
         __syncthreads();
-        // Per point, branch-free (a point past the frame's end computes on its zero inputs and is then
-        // dropped by selects: no per-point branch, so the unrolled arrays are never copied at branch
-        // joins): cell[q] = map row << 16 | map column, or -1; key[q] as below.
+        float F[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) F[c] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(Fs[c])));
+        // Per point, branch-free: cell[q] = map row << 16 | map column, or -1 (no point); key[q] as
+        // below.  A lane whose 8 pixels all lie in the frame (every lane but the frame's last few)
+        // takes the TAIL = false instance: no validity selects.  (A point past the end computes on
+        // zero inputs and is dropped.)  No per-point branch, so the unrolled arrays are never copied
+        // at branch joins.
         int cell[INGEST_PPT];
         unsigned long long key[INGEST_PPT];
         int imin = INT32_MAX, imax = -1, jmin = INT32_MAX, jmax = -1;
-        int i = k0 / Wc, j = k0 - i * Wc;
+        auto points = [&](auto tail) {
+            constexpr bool TAIL = decltype(tail)::value;
+            int i = k0 / Wc, j = k0 - i * Wc;
 #pragma unroll
-        for (int q = 0; q < INGEST_PPT; q++, j = (j + 1 == Wc) ? (i++, 0) : j + 1) {
-            const int k = k0 + q;
-            const bool valid = k < NP;
-            const float dep = c1 / (cfar - cfn * dv[q]);
-            const int ir = i - row0;  // (rows past the frame stay inside the table)
-            float p[3];
+            for (int q = 0; q < INGEST_PPT; q++, j = (j + 1 == Wc) ? (i++, 0) : j + 1) {
+                const int k = k0 + q;
+                const bool valid = !TAIL || k < NP;
+                const float dep = c1 / (cfar - cfn * dv[q]);
+                const int ir = i - row0;  // (rows past the frame stay inside the table)
+                float p[3];
 #pragma unroll
-            for (int c = 0; c < 3; c++) p[c] = F[c] + dep * (A[c][j] + Bt[c][ir]);
-            const int s8 = seg8_of(rv[q]);
-            int pi = ingest_clip(floorf(h2 - p[1] * 96.0f), H), pj = ingest_clip(floorf(w2 + p[0] * 96.0f), W);
-            cell[q] = valid ? (pi << 16) | pj : -1;
-            imin = valid ? min(imin, pi) : imin, imax = valid ? max(imax, pi) : imax;
-            jmin = valid ? min(jmin, pj) : jmin, jmax = valid ? max(jmax, pj) : jmax;
-            if (valid && s8 == 2) occ[(unsigned)__umul24(pi, W) + pj] = 1;  // np.isclose(seg, obstacle) (exact values)
-            // np.argsort order by z: float bits made unsigned-monotone, NaN last; equal z -> later pixel
-            const unsigned zb = __float_as_uint(p[2]);
-            const unsigned zk = p[2] != p[2] ? 0xffffffffu : ((zb & 0x80000000u) ? ~zb : (zb | 0x80000000u));
-            key[q] = ((unsigned long long)zk << 32) | (((unsigned)(k + 1) << 4) | (unsigned)s8);
-        }
-        // runs of one map pixel inside the lane: the run's last entry carries the run's max key
+                for (int c = 0; c < 3; c++) p[c] = F[c] + dep * (A[c][j] + Bt[c][ir]);
+                const int s8 = seg8_of(rv[q]);
+                int pi = ingest_clip(floorf(h2 - p[1] * 96.0f), H), pj = ingest_clip(floorf(w2 + p[0] * 96.0f), W);
+                cell[q] = valid ? (pi << 16) | pj : -1;
+                imin = valid ? min(imin, pi) : imin, imax = valid ? max(imax, pi) : imax;
+                jmin = valid ? min(jmin, pj) : jmin, jmax = valid ? max(jmax, pj) : jmax;
+                if (valid && s8 == 2) occ[(unsigned)__umul24(pi, W) + pj] = 1;  // np.isclose(seg, obstacle) (exact values)
+                // np.argsort order by z: float bits made unsigned-monotone, NaN last; equal z -> later pixel
+                const unsigned zb = __float_as_uint(p[2]);
+                const unsigned zk = p[2] != p[2] ? 0xffffffffu : ((zb & 0x80000000u) ? ~zb : (zb | 0x80000000u));
+                key[q] = ((unsigned long long)zk << 32) | (((unsigned)(k + 1) << 4) | (unsigned)s8);
+            }
+            // runs of one map pixel inside the lane: the run's last entry carries the run's max key
 #pragma unroll
-        for (int q = 1; q < INGEST_PPT; q++) {
-            const bool run = cell[q] == cell[q - 1] && cell[q] >= 0;
-            key[q] = run && key[q - 1] > key[q] ? key[q - 1] : key[q];
-            cell[q - 1] = run ? -1 : cell[q - 1];
-        }
+            for (int q = 1; q < INGEST_PPT; q++) {
+                const bool run = cell[q] == cell[q - 1] && (!TAIL || cell[q] >= 0);
+                key[q] = run && key[q - 1] > key[q] ? key[q - 1] : key[q];
+                cell[q - 1] = run ? -1 : cell[q - 1];
+            }
+        };
+        if (k0 + INGEST_PPT <= NP) points(std::false_type{});
+        else points(std::true_type{});
         // the chunk's box of map pixels
-        imin = wave_min(imin), imax = wave_max(imax), jmin = wave_min(jmin), jmax = wave_max(jmax);
+        imin = wave_reduce_dpp(imin, true), imax = wave_reduce_dpp(imax, false);
+        jmin = wave_reduce_dpp(jmin, true), jmax = wave_reduce_dpp(jmax, false);
         if ((tid & 63) == 0 && imax >= 0)
             atomicMin(&box[0], imin), atomicMin(&box[1], -imax), atomicMin(&box[2], jmin), atomicMin(&box[3], -jmax);
         __syncthreads();
