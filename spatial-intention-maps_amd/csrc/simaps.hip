@@ -3142,7 +3142,10 @@ __device__ __forceinline__ float dot3f(const float *a, const float *b)
 // loads in flight +4..28 us: the per-chunk barrier chain wants many chunks in flight, not fewer)
 constexpr int INGEST_WG = 256, INGEST_PPT = 8, INGEST_PTS = INGEST_WG * INGEST_PPT;
 __host__ __device__ constexpr int ingest_chunks(int hc, int wc) { return (hc * wc + INGEST_PTS - 1) / INGEST_PTS; }
-constexpr int INGEST_WIN = 4096;  // LDS window entries (u64 keys) over a chunk's map-pixel box
+#ifndef SIMAPS_INGEST_WIN
+#define SIMAPS_INGEST_WIN 2048
+#endif
+constexpr int INGEST_WIN = SIMAPS_INGEST_WIN;  // LDS window entries (u64 keys) over a chunk's map-pixel box
 constexpr int INGEST_MAX_WC = 1024, INGEST_MAX_ROWS = 32;  // camera width; camera rows one chunk spans
 // A chunk's pixels k0 .. k0 + INGEST_PTS - 1 reach camera row k0 / Wc + 1 + (INGEST_PTS - 2) / Wc at most
 // (k0 % Wc = Wc - 1): its row table index must stay below INGEST_MAX_ROWS.  Smallest such width: 67.
@@ -3241,7 +3244,9 @@ __device__ __forceinline__ int ingest_clip(float f, int n)
     return f >= 2147483648.0f ? 0 : c;
 }
 
-// grid (chunks, frames)
+// grid (chunks, frames); WCS: the column tables' stride (>= the camera width; 320 holds both reference
+// cameras, 156 and 277 columns, in 4 KB: LDS decides how many chunks a CU holds)
+template <int WCS>
 __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     simaps_config cfg, simaps_camera cam, const simaps_agent *__restrict__ agents,
     const simaps_seg_ids *__restrict__ seg_ids, const double *__restrict__ cam_params,
@@ -3252,7 +3257,7 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     // per chunk: A[c][j] = right[c] * pixel_x(j) + principal[c] (column j), Bt[c][i] = up[c] * pixel_y(i)
     // (row row0 + i): a point's ray t[c] = A[c][j] + Bt[c][i], the same float32 operations in the same
     // order as per point (capture_image, envs.py:1946-1950)
-    __shared__ float A[3][INGEST_MAX_WC], Bt[3][INGEST_MAX_ROWS], Fs[3];
+    __shared__ float A[3][WCS], Bt[3][INGEST_MAX_ROWS], Fs[3];
     __shared__ int box[4];  // min i, -max i, min j, -max j of the chunk's map pixels
     const int n = blockIdx.y, tid = threadIdx.x;
     const int H = cfg.H, W = cfg.W, Hc = cam.height_px, Wc = cam.width_px, NP = Hc * Wc;
@@ -3842,8 +3847,12 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
     if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d frames per launch (grid y <= 65535)", N);
     const int nch = ingest_chunks(cam->height_px, cam->width_px);  // point-pass chunks per frame
     if ((rc = pending_faults())) return rc;  // (after the argument checks: they need no device)
-    hipLaunchKernelGGL(ingest_points_kernel, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam, agents, seg_ids,
-                       cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes);
+    if (cam->width_px <= 320)
+        hipLaunchKernelGGL(ingest_points_kernel<320>, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam, agents,
+                           seg_ids, cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes);
+    else
+        hipLaunchKernelGGL(ingest_points_kernel<INGEST_MAX_WC>, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam,
+                           agents, seg_ids, cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes);
     hipLaunchKernelGGL(ingest_resolve_kernel, dim3(INGEST_RES_G, N), dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg, agents, overhead,
                        reinterpret_cast<unsigned long long *>(keys), boxes, nch);
     const hipError_t e = hipGetLastError();
