@@ -3411,44 +3411,60 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     }
 }
 
-// grid (INGEST_RES_G, frames): the frame's box of touched map pixels (the union of the point
-// pass's chunk boxes) in INGEST_RES_WG * INGEST_RES_U pixel chunks dealt round-robin over the
-// frame's workgroups
+// grid (INGEST_RES_G, frames): per map row of the frame, only the columns its chunk boxes cover --
+// the union of the boxes that contain the row, one interval (a forward camera's boxes follow its
+// viewing wedge: ~half of the frame's bounding box).  Rows are dealt round-robin over the frame's
+// INGEST_RES_G * 4 waves, two rows in flight per wave; the lanes sweep a row's columns.  Each wave
+// reads the chunk boxes itself (lane c: box c), so no barrier.
 __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
     simaps_config cfg, const simaps_agent *__restrict__ agents, float *__restrict__ overhead,
     unsigned long long *__restrict__ keys, const unsigned *__restrict__ boxes, int nch)
 {
-    __shared__ int fbox[4];
-    const int n = blockIdx.y, tid = threadIdx.x, W = cfg.W;
-    if (tid < 64) {  // the first wave merges the chunk boxes
-        int a = INT32_MAX, bb = 0, cc = INT32_MAX, d = 0;
-        for (int k = tid; k < nch; k += 64) {
-            const uint4 c = reinterpret_cast<const uint4 *>(boxes)[(size_t)n * nch + k];
-            a = min(a, (int)c.x), bb = max(bb, (int)c.y), cc = min(cc, (int)c.z), d = max(d, (int)c.w);
+    const int n = blockIdx.y, lane = threadIdx.x & 63, W = cfg.W;
+    const int gw = blockIdx.x * (INGEST_RES_WG / 64) + (threadIdx.x >> 6), nw = INGEST_RES_G * (INGEST_RES_WG / 64);
+    const uint4 *bx = reinterpret_cast<const uint4 *>(boxes) + (size_t)n * nch;
+    // lane c < 64 holds box c (an empty box for c >= nch); more than 64 boxes (cameras over 131 k
+    // pixels) are re-read per row below
+    uint4 b0 = lane < nch ? bx[lane] : make_uint4(0x7fffffffu, 0u, 0x7fffffffu, 0u);
+    const int fi0 = wave_reduce_dpp((int)b0.x, true), fi1 = wave_reduce_dpp((int)b0.y, false);
+    int ri0 = fi0, ri1 = fi1;
+    for (int c = 64 + lane; c < nch; c += 64) ri0 = min(ri0, (int)bx[c].x), ri1 = max(ri1, (int)bx[c].y);
+    if (nch > 64) ri0 = wave_reduce_dpp(ri0, true), ri1 = wave_reduce_dpp(ri1, false);
+    // the interval [lo, hi) of row r: the hull of the boxes containing r
+    auto extent = [&](int r, int &lo, int &hi) {
+        const bool in = (int)b0.x <= r && r < (int)b0.y;
+        int a = in ? (int)b0.z : INT32_MAX, z = in ? (int)b0.w : 0;
+        for (int c = 64 + lane; c < nch; c += 64) {
+            const uint4 q = bx[c];
+            if ((int)q.x <= r && r < (int)q.y) a = min(a, (int)q.z), z = max(z, (int)q.w);
         }
-        a = wave_min(a), bb = wave_max(bb), cc = wave_min(cc), d = wave_max(d);
-        if (tid == 0) fbox[0] = a, fbox[1] = bb, fbox[2] = cc, fbox[3] = d;
-    }
-    __syncthreads();
-    const uint4 b = make_uint4(fbox[0], fbox[1], fbox[2], fbox[3]);
-    const int i0 = (int)b.x, j0 = (int)b.z, bw = (int)b.w - j0, area = ((int)b.y - i0) * bw;
-    const size_t base = (size_t)agents[n].map_slot * cfg.H * W + (size_t)i0 * W + j0;
-    constexpr int CH = INGEST_RES_WG * INGEST_RES_U;
-    for (int e0 = blockIdx.x * CH; e0 < area; e0 += INGEST_RES_G * CH) {
-        size_t idx[INGEST_RES_U];
-        unsigned long long kv[INGEST_RES_U];
+        lo = wave_reduce_dpp(a, true), hi = wave_reduce_dpp(z, false);
+        if (hi <= lo) lo = hi = 0;  // no box holds the row
+    };
+    const size_t base = (size_t)agents[n].map_slot * cfg.H * W;
+    for (int r = ri0 + gw; r < ri1; r += 2 * nw) {
+        const int r2 = r + nw;  // the second row in flight (if < ri1)
+        int lo, hi, lo2 = 0, hi2 = 0;
+        extent(r, lo, hi);
+        if (r2 < ri1) extent(r2, lo2, hi2);
+        constexpr int U = 2;  // columns per lane and row in flight: rows up to 128 wide in one pass
+        for (int c0 = 0; c0 < max(hi - lo, hi2 - lo2); c0 += 64 * U) {
+            size_t idx[2 * U];
+            unsigned long long kv[2 * U];
 #pragma unroll
-        for (int u = 0; u < INGEST_RES_U; u++) {
-            const int e = e0 + u * INGEST_RES_WG + tid, r = e / bw;
-            idx[u] = base + (size_t)r * W + (e - r * bw);
-            kv[u] = e < area ? keys[idx[u]] : 0ull;
-        }
-#pragma unroll
-        for (int u = 0; u < INGEST_RES_U; u++)
-            if (kv[u]) {
-                overhead[idx[u]] = (float)(kv[u] & 15ull) * 0.125f;
-                keys[idx[u]] = 0ull;
+            for (int u = 0; u < 2 * U; u++) {
+                const int rr = u < U ? r : r2, l = u < U ? lo : lo2, h = u < U ? hi : hi2;
+                const int c = l + c0 + (u % U) * 64 + lane;
+                idx[u] = base + (size_t)rr * W + c;
+                kv[u] = c < h ? keys[idx[u]] : 0ull;
             }
+#pragma unroll
+            for (int u = 0; u < 2 * U; u++)
+                if (kv[u]) {
+                    overhead[idx[u]] = (float)(kv[u] & 15ull) * 0.125f;
+                    keys[idx[u]] = 0ull;
+                }
+        }
     }
 }
 
