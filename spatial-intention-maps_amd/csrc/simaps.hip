@@ -3221,9 +3221,9 @@ __device__ __forceinline__ void ingest_load(const float *db, const int32_t *raw,
 
 // min (is_min) or max over the wave by DPP (quad, half-row and row mirrors, then the row
 // broadcasts); lanes of rows a broadcast leaves out keep their value (op(v, v) = v)
-__device__ __forceinline__ int wave_reduce_dpp(int v, bool is_min)
+template <class Op>
+__device__ __forceinline__ int wave_reduce_dpp(int v, Op op)
 {
-    auto op = [&](int a, int b) { return is_min ? min(a, b) : max(a, b); };
     v = op(v, __builtin_amdgcn_update_dpp(v, v, 0xb1, 0xf, 0xf, false));   // quad_perm [1, 0, 3, 2]
     v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x4e, 0xf, 0xf, false));   // quad_perm [2, 3, 0, 1]
     v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xf, 0xf, false));  // row_half_mirror
@@ -3231,6 +3231,21 @@ __device__ __forceinline__ int wave_reduce_dpp(int v, bool is_min)
     v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));  // row_bcast15 -> rows 1, 3
     v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));  // row_bcast31 -> rows 2, 3
     return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int wave_reduce_dpp(int v, bool is_min)
+{
+    return is_min ? wave_reduce_dpp(v, [](int a, int b) { return min(a, b); })
+                  : wave_reduce_dpp(v, [](int a, int b) { return max(a, b); });
+}
+// two u16 halves at once (v_pk_min_u16 / v_pk_max_u16)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int pk_min_u16(int a, int b)
+{
+    return __builtin_bit_cast(int, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ int pk_max_u16(int a, int b)
+{
+    return __builtin_bit_cast(int, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
 }
 
 // np.floor(v).astype(np.int32) then np.clip(., 0, n - 1) (envs.py:2440-2442) of an already floored
@@ -3317,7 +3332,7 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
         // at branch joins.
         int cell[INGEST_PPT];
         unsigned long long key[INGEST_PPT];
-        int imin = INT32_MAX, imax = -1, jmin = INT32_MAX, jmax = -1;
+        int cmin = -1, cmax = 0;  // the lane's (row, column) box, packed like cell: u16 halves
         auto points = [&](auto tail) {
             constexpr bool TAIL = decltype(tail)::value;
             int i = k0 / Wc, j = k0 - i * Wc;
@@ -3332,9 +3347,9 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
                 for (int c = 0; c < 3; c++) p[c] = F[c] + dep * (A[c][j] + Bt[c][ir]);
                 const int s8 = seg8_of(rv[q]);
                 int pi = ingest_clip(floorf(h2 - p[1] * 96.0f), H), pj = ingest_clip(floorf(w2 + p[0] * 96.0f), W);
-                cell[q] = valid ? (pi << 16) | pj : -1;
-                imin = valid ? min(imin, pi) : imin, imax = valid ? max(imax, pi) : imax;
-                jmin = valid ? min(jmin, pj) : jmin, jmax = valid ? max(jmax, pj) : jmax;
+                const int cq = (pi << 16) | pj;
+                cell[q] = valid ? cq : -1;
+                cmin = valid ? pk_min_u16(cmin, cq) : cmin, cmax = valid ? pk_max_u16(cmax, cq) : cmax;
                 if (valid && s8 == 2) occ[(unsigned)__umul24(pi, W) + pj] = 1;  // np.isclose(seg, obstacle) (exact values)
                 // np.argsort order by z: float bits made unsigned-monotone, NaN last; equal z -> later pixel
                 const unsigned zb = __float_as_uint(p[2]);
@@ -3352,9 +3367,9 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
         if (k0 + INGEST_PPT <= NP) points(std::false_type{});
         else points(std::true_type{});
         // the chunk's box of map pixels
-        imin = wave_reduce_dpp(imin, true), imax = wave_reduce_dpp(imax, false);
-        jmin = wave_reduce_dpp(jmin, true), jmax = wave_reduce_dpp(jmax, false);
-        if ((tid & 63) == 0 && imax >= 0)
+        cmin = wave_reduce_dpp(cmin, pk_min_u16), cmax = wave_reduce_dpp(cmax, pk_max_u16);
+        const int imin = (unsigned)cmin >> 16, jmin = cmin & 0xffff, imax = (unsigned)cmax >> 16, jmax = cmax & 0xffff;
+        if ((tid & 63) == 0 && imin <= imax)  // (a wave without points keeps cmin = 0xffff'ffff, cmax = 0)
             atomicMin(&box[0], imin), atomicMin(&box[1], -imax), atomicMin(&box[2], jmin), atomicMin(&box[3], -jmax);
         __syncthreads();
         const int bi = box[0], bj = box[2], bh = -box[1] - bi + 1, bw = -box[3] - bj + 1;
