@@ -3255,7 +3255,7 @@ __device__ __forceinline__ int ingest_clip(float f, int n)
 {
     int c;
     asm("v_cvt_i32_f32 %0, %1" : "=v"(c) : "v"(f));
-    c = min(max(c, 0), n - 1);  // (v_med3_i32)
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c) : "v"(c), "s"(n - 1));
     return f >= 2147483648.0f ? 0 : c;
 }
 
@@ -3272,7 +3272,11 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     // per chunk: A[c][j] = right[c] * pixel_x(j) + principal[c] (column j), Bt[c][i] = up[c] * pixel_y(i)
     // (row row0 + i): a point's ray t[c] = A[c][j] + Bt[c][i], the same float32 operations in the same
     // order as per point (capture_image, envs.py:1946-1950)
-    __shared__ float A[3][WCS], Bt[3][INGEST_MAX_ROWS], Fs[3];
+    // (A holds INGEST_PPT wrapped columns past Wc: A[c][Wc + t] = A[c][t], so a lane's 8 columns are
+    // consecutive table entries even where its pixels wrap to the next row; segT: seg * 8 of body
+    // ids -1 .. 254 at segT[id + 1])
+    __shared__ float A[3][WCS + INGEST_PPT], Bt[3][INGEST_MAX_ROWS], Fs[3];
+    __shared__ uint8_t segT[256];
     __shared__ int box[4];  // min i, -max i, min j, -max j of the chunk's map pixels
     const int n = blockIdx.y, tid = threadIdx.x;
     const int H = cfg.H, W = cfg.W, Hc = cam.height_px, Wc = cam.width_px, NP = Hc * Wc;
@@ -3287,6 +3291,14 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     const simaps_seg_ids ids = seg_ids[ag.env];
     const float c1 = (float)(cam.far_m * cam.near_m), cfar = (float)cam.far_m, cfn = (float)(cam.far_m - cam.near_m);
     const float cx2 = (float)cam.cx2, cy2 = (float)cam.cy2;
+    // seg * 8 per body id (the reference's float sum of 1/8 multiples < 2 is exact: its integer sum)
+    auto seg8_of = [&](int r) {
+        int v = r == 0 ? 1 : 0;
+        v += (r >= ids.min_obstacle && r <= ids.max_obstacle) ? 2 : 0;
+        v += (ids.has_receptacle && r == ids.receptacle) ? 3 : 0;
+        v += (r >= ids.min_cube && r <= ids.max_cube) ? 4 : 0;
+        return v;
+    };
     // per chunk once, by wave 0 alone (the pass is VALU-issue bound: the other waves' issue slots
     // go to other chunks): the camera frame and the column and row tables (envs.py:1932-1947; the
     // float32 divisions and products every point of a column / row would repeat)
@@ -3296,11 +3308,14 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
         camera_frame(cam_params + 9 * (size_t)n, F);
 #pragma unroll
         for (int c = 0; c < 12; c++) F[c] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F[c])));
-        for (int j = tid; j < Wc; j += 64) {
-            const float px = cx2 * ((float)j / (float)Wc - 0.5f);
+        for (int j = tid; j < Wc + INGEST_PPT; j += 64) {
+            const int jj = j < Wc ? j : j - Wc;
+            const float px = cx2 * ((float)jj / (float)Wc - 0.5f);
 #pragma unroll
             for (int c = 0; c < 3; c++) A[c][j] = F[3 + c] + px * F[9 + c];
         }
+#pragma unroll
+        for (int e = tid; e < 256; e += 64) segT[e] = (uint8_t)seg8_of(e - 1);
         if (tid < INGEST_MAX_ROWS) {
             const float py = cy2 * (0.5f - ((float)(row0 + tid) + 1.0f) / (float)Hc);
 #pragma unroll
@@ -3312,14 +3327,6 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     const float h2 = (float)((double)H / 2), w2 = (float)((double)W / 2);
     const size_t base = (size_t)ag.map_slot * H * W;
     uint8_t *const occ = occupancy + base;
-    // seg * 8 per body id (the reference's float sum of 1/8 multiples < 2 is exact: its integer sum)
-    auto seg8_of = [&](int r) {
-        int v = r == 0 ? 1 : 0;
-        v += (r >= ids.min_obstacle && r <= ids.max_obstacle) ? 2 : 0;
-        v += (ids.has_receptacle && r == ids.receptacle) ? 3 : 0;
-        v += (r >= ids.min_cube && r <= ids.max_cube) ? 4 : 0;
-        return v;
-    };
     {
         __syncthreads();
         float F[3];
@@ -3333,19 +3340,37 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
         int cell[INGEST_PPT];
         unsigned long long key[INGEST_PPT];
         int cmin = -1, cmax = 0;  // the lane's (row, column) box, packed like cell: u16 halves
+        // body ids all in the seg table's range -1 .. 254 (wave-uniform): a table look-up per point
+        unsigned idor = 0;
+#pragma unroll
+        for (int q = 0; q < INGEST_PPT; q++) idor |= (unsigned)(rv[q] + 1);
+        const bool ids_ok = __builtin_amdgcn_ballot_w64(idor >= 256u) == 0;
         auto points = [&](auto tail) {
             constexpr bool TAIL = decltype(tail)::value;
-            int i = k0 / Wc, j = k0 - i * Wc;
+            const int i0 = k0 / Wc, j0 = k0 - i0 * Wc, ir0 = i0 - row0;  // (rows past the frame stay inside the table)
+            // a full lane's 8 columns are the consecutive table entries j0 .. j0 + 7 (wrapped copies
+            // past Wc); its points from q = Wc - j0 on lie in the next row
+            float B0[3], B1[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) B0[c] = Bt[c][ir0], B1[c] = Bt[c][ir0 + 1];
+            int i = i0, j = j0;
 #pragma unroll
             for (int q = 0; q < INGEST_PPT; q++, j = (j + 1 == Wc) ? (i++, 0) : j + 1) {
                 const int k = k0 + q;
                 const bool valid = !TAIL || k < NP;
                 const float dep = c1 / (cfar - cfn * dv[q]);
-                const int ir = i - row0;  // (rows past the frame stay inside the table)
                 float p[3];
+                if constexpr (TAIL) {
 #pragma unroll
-                for (int c = 0; c < 3; c++) p[c] = F[c] + dep * (A[c][j] + Bt[c][ir]);
-                const int s8 = seg8_of(rv[q]);
+                    for (int c = 0; c < 3; c++) p[c] = F[c] + dep * (A[c][j] + Bt[c][i - row0]);
+                } else {
+                    const bool nxt = q >= Wc - j0;
+#pragma unroll
+                    for (int c = 0; c < 3; c++) p[c] = F[c] + dep * (A[c][j0 + q] + (nxt ? B1[c] : B0[c]));
+                }
+                int s8;
+                if (ids_ok) s8 = segT[rv[q] + 1];
+                else s8 = seg8_of(rv[q]);
                 int pi = ingest_clip(floorf(h2 - p[1] * 96.0f), H), pj = ingest_clip(floorf(w2 + p[0] * 96.0f), W);
                 const int cq = (pi << 16) | pj;
                 cell[q] = valid ? cq : -1;
@@ -3878,7 +3903,7 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
     if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d frames per launch (grid y <= 65535)", N);
     const int nch = ingest_chunks(cam->height_px, cam->width_px);  // point-pass chunks per frame
     if ((rc = pending_faults())) return rc;  // (after the argument checks: they need no device)
-    if (cam->width_px <= 320)
+    if (cam->width_px + INGEST_PPT <= 320)
         hipLaunchKernelGGL(ingest_points_kernel<320>, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam, agents,
                            seg_ids, cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes);
     else
