@@ -3152,7 +3152,14 @@ constexpr int INGEST_MAX_WC = 1024, INGEST_MAX_ROWS = 32;  // camera width; came
 constexpr bool ingest_width_ok(int wc) { return wc >= 1 && wc <= INGEST_MAX_WC && 1 + (INGEST_PTS - 2) / wc < INGEST_MAX_ROWS; }
 constexpr int ingest_min_width(int wc = 1) { return ingest_width_ok(wc) ? wc : ingest_min_width(wc + 1); }
 static_assert(ingest_min_width() == 67, "include/simaps.h documents the camera width range [67, 1024]");
-constexpr int INGEST_RES_WG = 256, INGEST_RES_U = 8, INGEST_RES_G = 8;  // resolve: 8 workgroups per frame, 8 keys per thread in flight
+#ifndef SIMAPS_INGEST_RES_G
+#define SIMAPS_INGEST_RES_G 8
+#endif
+#ifndef SIMAPS_INGEST_RES_ROWS
+#define SIMAPS_INGEST_RES_ROWS 2
+#endif
+// resolve: INGEST_RES_G workgroups per frame, INGEST_RES_ROWS rows in flight per wave
+constexpr int INGEST_RES_WG = 256, INGEST_RES_G = SIMAPS_INGEST_RES_G, INGEST_RES_ROWS = SIMAPS_INGEST_RES_ROWS;
 
 // Camera.capture_image's frame (envs.py:1932-1940) in float32: position, principal, up, right.
 __device__ __forceinline__ void camera_frame(const double *P, float *F)
@@ -3482,24 +3489,26 @@ __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
         if (hi <= lo) lo = hi = 0;  // no box holds the row
     };
     const size_t base = (size_t)agents[n].map_slot * cfg.H * W;
-    for (int r = ri0 + gw; r < ri1; r += 2 * nw) {
-        const int r2 = r + nw;  // the second row in flight (if < ri1)
-        int lo, hi, lo2 = 0, hi2 = 0;
-        extent(r, lo, hi);
-        if (r2 < ri1) extent(r2, lo2, hi2);
-        constexpr int U = 2;  // columns per lane and row in flight: rows up to 128 wide in one pass
-        for (int c0 = 0; c0 < max(hi - lo, hi2 - lo2); c0 += 64 * U) {
-            size_t idx[2 * U];
-            unsigned long long kv[2 * U];
+    constexpr int R = INGEST_RES_ROWS, U = 2;  // rows in flight; columns per lane and row in flight
+    for (int r = ri0 + gw; r < ri1; r += R * nw) {
+        int lo[R], hi[R], wmax = 0;
 #pragma unroll
-            for (int u = 0; u < 2 * U; u++) {
-                const int rr = u < U ? r : r2, l = u < U ? lo : lo2, h = u < U ? hi : hi2;
-                const int c = l + c0 + (u % U) * 64 + lane;
-                idx[u] = base + (size_t)rr * W + c;
-                kv[u] = c < h ? keys[idx[u]] : 0ull;
+        for (int t = 0; t < R; t++) {
+            lo[t] = hi[t] = 0;
+            if (r + t * nw < ri1) extent(r + t * nw, lo[t], hi[t]);
+            wmax = max(wmax, hi[t] - lo[t]);
+        }
+        for (int c0 = 0; c0 < wmax; c0 += 64 * U) {
+            size_t idx[R * U];
+            unsigned long long kv[R * U];
+#pragma unroll
+            for (int u = 0; u < R * U; u++) {
+                const int t = u / U, c = lo[t] + c0 + (u % U) * 64 + lane;
+                idx[u] = base + (size_t)(r + t * nw) * W + c;
+                kv[u] = c < hi[t] ? keys[idx[u]] : 0ull;
             }
 #pragma unroll
-            for (int u = 0; u < 2 * U; u++)
+            for (int u = 0; u < R * U; u++)
                 if (kv[u]) {
                     overhead[idx[u]] = (float)(kv[u] & 15ull) * 0.125f;
                     keys[idx[u]] = 0ull;
