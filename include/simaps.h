@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SIMAPS_ABI_VERSION 5
+#define SIMAPS_ABI_VERSION 6
 
 /* error codes */
 #define SIMAPS_OK 0
@@ -238,11 +238,14 @@ int simaps_path_mode(int mode);
  *   agents[n].map_slot), from depth [N][Hc][Wc] float32 (pybullet depth buffer) and seg_raw
  *   [N][Hc][Wc] int32 (body ids), cam_params [N][9] fp64 = _get_camera_params(robot pose)
  *   (position, target, up; envs.py:1962-2008), seg_ids [E] per env.  keys: uint64 [M, H, W]
- *   scratch, all zero on entry and left zero; boxes: uint32 [N, simaps_ingest_chunks(Hc, Wc), 4]
- *   scratch (any contents).  The frames' map slots must be distinct.  All DEVICE.  Points with
- *   equal z on one pixel: the later camera pixel wins (the reference's np.argsort leaves that
- *   order unspecified).
- *   SIMAPS_EUNSUPPORTED: camera width outside [67, 1024], Hc * Wc >= 2^28, N > 65535
+ *   scratch tagged with `epoch`: all zero before the first launch, then never cleared by the
+ *   library -- each launch passes an epoch in [1, 255] larger than every earlier launch's on this
+ *   key map since it was last zeroed (when the epoch would wrap, zero the key map and restart at
+ *   1); boxes: uint32 [N, simaps_ingest_chunks(Hc, Wc), 4] scratch (any contents).  The frames'
+ *   map slots must be distinct.  All DEVICE.  Points with equal z on one pixel: the later camera
+ *   pixel wins (the reference's np.argsort leaves that order unspecified).
+ *   SIMAPS_EINVAL: epoch outside [1, 255].
+ *   SIMAPS_EUNSUPPORTED: camera width outside [67, 1024], Hc * Wc >= 2^20, N > 65535
  *   (two launches on `stream`: a point pass over chunks of 2048 camera pixels with per-chunk LDS
  *   max-reduction that also records each chunk's box of touched map pixels, then one sweep of each
  *   frame's box). */
@@ -253,7 +256,7 @@ int simaps_ingest_chunks(int height_px, int width_px);
 
 int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, const simaps_agent *agents,
                   const simaps_seg_ids *seg_ids, const double *cam_params, const float *depth, const int32_t *seg_raw,
-                  float *overhead, uint8_t *occupancy, uint64_t *keys, uint32_t *boxes, void *stream);
+                  float *overhead, uint8_t *occupancy, uint64_t *keys, uint32_t *boxes, int epoch, void *stream);
 
 /* Batched GridGraph(grid).shortest_path_image(source):
  *   grids [B, H, W] uint8 (nonzero = free), sources [B, 2] int32 (row, col), out dists [B, H, W]

@@ -3120,23 +3120,25 @@ __device__ __forceinline__ float dot3f(const float *a, const float *b)
 
 // Two passes, no recomputation and no reset pass:
 //   ingest_points_kernel  grid (chunks of INGEST_PTS camera pixels, frames): each point once -- its
-//                         map pixel, its obstacle bit (occupancy byte store) and its key (monotone z
-//                         bits | camera pixel + 1 | seg code).  The keys are max-reduced per map
-//                         pixel in LDS over the chunk's bounding box of map pixels (direct-mapped,
-//                         no hashing), then ONE global 64-bit atomicMax per touched pixel of the box.
-//                         A chunk's 2048 points hit only 14-1021 distinct pixels (the near rows of a
-//                         forward camera ~30), so atomics straight from the points serialised on a
-//                         few L2 lines (547 us per 256 frames); an LDS hash table cost 22 us of
-//                         init / scan on top of the reduction (95 us).  A box larger than the LDS
-//                         window uses a direct-mapped (pixel tag, key) table in the same LDS.  The seg
-//                         value (a sum of 1/8 multiples < 2, exact in f32) travels as seg * 8 in the
-//                         key's low 4 bits, so the winner's value needs no second look-up.
-//                         Each chunk also stores its box (boxes[n][chunk]).
-//   ingest_resolve_kernel 8 workgroups per frame: a sweep of the frame's box (the union of its chunk
-//                         boxes) of the slot's key map, not the whole map (a forward camera's box is
-//                         ~34 % of it): a nonzero key writes overhead = code / 8 and is zeroed again.
-// HBM per frame: 8 B per camera pixel (depth + seg) + 8 B per pixel of the box (key sweep) + the
-// pixel writes; the atomics resolve in L2 (a frame's key map is <= 0.4 MB).
+//                         map pixel, its obstacle bit (occupancy byte store) and its key
+//                         (launch epoch 8 bits | monotone z bits 32 | camera pixel + 1 20 | seg code
+//                         4).  The keys are max-reduced per map pixel in LDS over the chunk's
+//                         bounding box of map pixels (direct-mapped, no hashing), then ONE global
+//                         64-bit atomicMax per touched pixel of the box.  A chunk's 2048 points hit
+//                         only 14-1021 distinct pixels (the near rows of a forward camera ~30), so
+//                         atomics straight from the points serialised on a few L2 lines (547 us per
+//                         256 frames); an LDS hash table cost 22 us of init / scan on top of the
+//                         reduction (95 us).  A box larger than the LDS window uses a direct-mapped
+//                         (cell tag, key) table in the same LDS.  The seg value (a sum of 1/8
+//                         multiples < 2, exact in f32) travels as seg * 8 in the key's low 4 bits, so
+//                         the winner's value needs no second look-up.  Each chunk also stores its box
+//                         (boxes[n][chunk]).
+//   ingest_resolve_kernel 8 workgroups per frame: per map row, the columns the chunk boxes cover, of
+//                         the slot's key map: a key of this launch's epoch writes overhead = code / 8.
+//                         Keys of earlier launches carry smaller epochs, so every key of this launch
+//                         beats them in the atomicMax and nothing is ever zeroed again (the caller
+//                         clears the key map when the epoch wraps, include/simaps.h).
+// HBM per frame: 8 B per camera pixel (depth + seg) + 8 B per swept key + the pixel writes.
 // (measured alternatives, 256 frames: 128- / 64-thread chunks +4 / +21 us, an 8192-entry window
 // +30 us (LDS occupancy), workgroups looping over several chunks of a frame with the next chunk's
 // loads in flight +4..28 us: the per-chunk barrier chain wants many chunks in flight, not fewer)
@@ -3273,7 +3275,7 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
     simaps_config cfg, simaps_camera cam, const simaps_agent *__restrict__ agents,
     const simaps_seg_ids *__restrict__ seg_ids, const double *__restrict__ cam_params,
     const float *__restrict__ depth, const int32_t *__restrict__ seg_raw, uint8_t *__restrict__ occupancy,
-    unsigned long long *__restrict__ keys, unsigned *__restrict__ boxes)
+    unsigned long long *__restrict__ keys, unsigned *__restrict__ boxes, unsigned epoch)
 {
     __shared__ unsigned long long win[INGEST_WIN];
     // per chunk: A[c][j] = right[c] * pixel_x(j) + principal[c] (column j), Bt[c][i] = up[c] * pixel_y(i)
@@ -3386,7 +3388,7 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
                 // np.argsort order by z: float bits made unsigned-monotone, NaN last; equal z -> later pixel
                 const unsigned zb = __float_as_uint(p[2]);
                 const unsigned zk = p[2] != p[2] ? 0xffffffffu : ((zb & 0x80000000u) ? ~zb : (zb | 0x80000000u));
-                key[q] = ((unsigned long long)zk << 32) | (((unsigned)(k + 1) << 4) | (unsigned)s8);
+                key[q] = ((unsigned long long)epoch << 56) | ((unsigned long long)zk << 24) | (((unsigned)(k + 1) << 4) | (unsigned)s8);
             }
             // runs of one map pixel inside the lane: the run's last entry carries the run's max key
 #pragma unroll
@@ -3465,7 +3467,7 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
 // reads the chunk boxes itself (lane c: box c), so no barrier.
 __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
     simaps_config cfg, const simaps_agent *__restrict__ agents, float *__restrict__ overhead,
-    unsigned long long *__restrict__ keys, const unsigned *__restrict__ boxes, int nch)
+    const unsigned long long *__restrict__ keys, const unsigned *__restrict__ boxes, int nch, unsigned epoch)
 {
     const int n = blockIdx.y, lane = threadIdx.x & 63, W = cfg.W;
     const int gw = blockIdx.x * (INGEST_RES_WG / 64) + (threadIdx.x >> 6), nw = INGEST_RES_G * (INGEST_RES_WG / 64);
@@ -3509,10 +3511,7 @@ __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
             }
 #pragma unroll
             for (int u = 0; u < R * U; u++)
-                if (kv[u]) {
-                    overhead[idx[u]] = (float)(kv[u] & 15ull) * 0.125f;
-                    keys[idx[u]] = 0ull;
-                }
+                if ((unsigned)(kv[u] >> 56) == epoch) overhead[idx[u]] = (float)(kv[u] & 15ull) * 0.125f;
         }
     }
 }
@@ -3895,7 +3894,7 @@ int simaps_ingest_chunks(int height_px, int width_px)
 
 int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, const simaps_agent *agents,
                   const simaps_seg_ids *seg_ids, const double *cam_params, const float *depth, const int32_t *seg_raw,
-                  float *overhead, uint8_t *occupancy, uint64_t *keys, uint32_t *boxes, void *stream)
+                  float *overhead, uint8_t *occupancy, uint64_t *keys, uint32_t *boxes, int epoch, void *stream)
 {
     int rc = check_cfg(cfg);
     if (rc) return rc;
@@ -3908,18 +3907,19 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
     const int np = cam->height_px * cam->width_px;
     if (!ingest_width_ok(cam->width_px))
         return fail(SIMAPS_EUNSUPPORTED, "camera width %d outside [%d, %d]", cam->width_px, ingest_min_width(), INGEST_MAX_WC);
-    if (np >= (1 << 28)) return fail(SIMAPS_EUNSUPPORTED, "camera frame of %d pixels (key packs pixel + 1 in 28 bits)", np);
+    if (np >= (1 << 20)) return fail(SIMAPS_EUNSUPPORTED, "camera frame of %d pixels (key packs pixel + 1 in 20 bits)", np);
+    if (epoch < 1 || epoch > 255) return fail(SIMAPS_EINVAL, "epoch %d not in [1, 255]", epoch);
     if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d frames per launch (grid y <= 65535)", N);
     const int nch = ingest_chunks(cam->height_px, cam->width_px);  // point-pass chunks per frame
     if ((rc = pending_faults())) return rc;  // (after the argument checks: they need no device)
     if (cam->width_px + INGEST_PPT <= 320)
         hipLaunchKernelGGL(ingest_points_kernel<320>, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam, agents,
-                           seg_ids, cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes);
+                           seg_ids, cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes, (unsigned)epoch);
     else
         hipLaunchKernelGGL(ingest_points_kernel<INGEST_MAX_WC>, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam,
-                           agents, seg_ids, cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes);
+                           agents, seg_ids, cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes, (unsigned)epoch);
     hipLaunchKernelGGL(ingest_resolve_kernel, dim3(INGEST_RES_G, N), dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg, agents, overhead,
-                       reinterpret_cast<unsigned long long *>(keys), boxes, nch);
+                       reinterpret_cast<const unsigned long long *>(keys), boxes, nch, (unsigned)epoch);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "ingest launch: %s", hipGetErrorString(e));
     return 0;

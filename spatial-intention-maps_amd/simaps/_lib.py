@@ -28,7 +28,7 @@ ROBOT_DTYPE = np.dtype([('x', '<f8'), ('y', '<f8'), ('heading', '<f8'), ('target
                         ('history_len', '<i4')], align=True)
 ENV_DTYPE = np.dtype([('receptacle_x', '<f8'), ('receptacle_y', '<f8'), ('has_receptacle', '<i4'),
                       ('robot_off', '<i4'), ('num_robots', '<i4'), ('reserved', '<i4')], align=True)
-ABI_VERSION = 5  # include/simaps.h SIMAPS_ABI_VERSION
+ABI_VERSION = 6  # include/simaps.h SIMAPS_ABI_VERSION
 AGENT_DTYPE = np.dtype([('env', '<i4'), ('robot', '<i4'), ('map_slot', '<i4')], align=True)
 assert ROBOT_DTYPE.itemsize == 72 and ENV_DTYPE.itemsize == 32 and AGENT_DTYPE.itemsize == 12
 
@@ -85,7 +85,7 @@ def _load(path=LIB_PATH):
     L.simaps_sp_distance.restype = i32
     L.simaps_shortest_path.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.simaps_shortest_path.restype = i32
-    L.simaps_ingest.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(Camera), i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.simaps_ingest.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(Camera), i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp]
     L.simaps_ingest.restype = i32
     L.simaps_path_mode.argtypes = [i32]
     L.simaps_path_mode.restype = i32

@@ -446,8 +446,9 @@ class StateBatch:
             for f in ('min_obstacle', 'max_obstacle', 'receptacle', 'min_cube', 'max_cube'):
                 ids[e][f] = d[f]
             ids[e]['has_receptacle'] = sc['receptacle_position'] is not None
-        if getattr(self, '_keys', None) is None:
+        if getattr(self, '_keys', None) is None:  # (epoch-tagged from here on: launch_ingest)
             self._keys = torch.zeros((self.N, self.H, self.W), dtype=torch.int64, device=self.device)
+            self._epoch = 0
         nch = _lib.lib.simaps_ingest_chunks(spec.height_px, spec.width_px)  # point-pass chunks per frame
         if nch < 0:
             _lib.check(nch)
@@ -462,10 +463,17 @@ class StateBatch:
         if prep['n'] == 0:
             return
         s, cur = launch_stream(self.device, stream)
+        # the key map's launch epoch (include/simaps.h simaps_ingest): 1..255, then the map is zeroed
+        # (on the launch stream, before the launch) and the count restarts
+        self._epoch = getattr(self, '_epoch', 0) + 1
+        if self._epoch > 255:
+            with torch.cuda.stream(s):
+                self._keys.zero_()
+            self._epoch = 1
         _lib.check(_lib.lib.simaps_ingest(
             self.cfg, prep['cam'], prep['n'], _lib.ptr(prep['agents']), _lib.ptr(prep['ids']), _lib.ptr(prep['params']),
             _lib.ptr(prep['depth']), _lib.ptr(prep['seg']), _lib.ptr(self.overhead), _lib.ptr(self.occupancy),
-            _lib.ptr(self._keys), _lib.ptr(self._boxes), _lib.stream_handle(s)))
+            _lib.ptr(self._keys), _lib.ptr(self._boxes), self._epoch, _lib.stream_handle(s)))
         hold(s, cur, prep['ids'], prep['params'], prep['depth'], prep['seg'], prep['agents'], self.overhead,
              self.occupancy, self._keys, self._boxes)
 

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(_lib.lib, name), name
         assert isinstance(getattr(_lib.lib, name), ctypes._CFuncPtr)
     assert set(_lib.EXPORTED) == set(declared_symbols())
-    assert _lib.lib.simaps_abi_version() == 5
+    assert _lib.lib.simaps_abi_version() == 6
 
 
 def test_struct_layouts_match_header():
@@ -94,7 +94,7 @@ def test_statebatch_refuses_cpu_device():
 
 def test_ingest_chunk_count_and_argument_checks():
     """simaps_ingest_chunks sizes the boxes scratch (one entry per 2048 camera pixels); simaps_ingest
-    refuses bad cameras, NULL buffers and unsupported widths before any launch."""
+    refuses bad cameras, NULL buffers, unsupported widths and epochs outside [1, 255] before any launch."""
     import ctypes
     from simaps import _lib, batch, camera, synthetic
     L = _lib.lib
@@ -104,10 +104,12 @@ def test_ingest_chunk_count_and_argument_checks():
     c = batch.make_config(synthetic.config_flags('lifting_4-small_divider'), 0.5, 1.0)
     spec = camera.CAMERAS['forward']
     cam = _lib.Camera(spec.height_px, spec.width_px, spec.near, spec.far, spec.cx2, spec.cy2)
-    assert L.simaps_ingest(c, cam, 0, *([None] * 9), None) == 0                     # nothing to do
-    assert L.simaps_ingest(c, cam, 1, *([None] * 9), None) == _lib.EINVAL           # NULL buffers
+    assert L.simaps_ingest(c, cam, 0, *([None] * 9), 1, None) == 0                  # nothing to do
+    assert L.simaps_ingest(c, cam, 1, *([None] * 9), 1, None) == _lib.EINVAL        # NULL buffers
     bad = _lib.Camera(spec.height_px, spec.width_px, spec.far, spec.near, spec.cx2, spec.cy2)
-    assert L.simaps_ingest(c, bad, 1, *([None] * 9), None) == _lib.EINVAL           # near >= far
+    assert L.simaps_ingest(c, bad, 1, *([None] * 9), 1, None) == _lib.EINVAL        # near >= far
     p = ctypes.c_void_p(8)  # never dereferenced: the width check comes first
     wide = _lib.Camera(8, 2000, spec.near, spec.far, spec.cx2, spec.cy2)
-    assert L.simaps_ingest(c, wide, 1, *([p] * 9), None) == _lib.EUNSUPPORTED
+    assert L.simaps_ingest(c, wide, 1, *([p] * 9), 1, None) == _lib.EUNSUPPORTED
+    for epoch in (0, 256):  # the key map's launch epoch (refused before any launch)
+        assert L.simaps_ingest(c, cam, 1, *([p] * 9), epoch, None) == _lib.EINVAL

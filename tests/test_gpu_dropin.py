@@ -22,6 +22,11 @@ def V():
     return synthetic, vector_env
 
 
+def _key_epochs(b):
+    """The launch epochs (top byte) present in a StateBatch's ingest key map."""
+    return set(int(x) for x in np.unique(b._keys.cpu().numpy().view(np.uint64) >> np.uint64(56)))
+
+
 def _bitwise(a, b):
     a, b = np.asarray(a), np.asarray(b)
     return a.shape == b.shape and np.array_equal(a.view(np.int32), b.view(np.int32))
@@ -247,7 +252,7 @@ def test_ingest_reference_goldens(V):
         for a, k in enumerate(keys):
             assert _bitwise(ov[a], z[k + '_overhead']), k
             assert np.array_equal(oc[a], z[k + '_occupancy']), k
-        assert int(b._keys.abs().sum()) == 0          # scratch left zeroed
+        assert _key_epochs(b) <= {0, b._epoch}        # keys: untouched, or this (first) launch's epoch
 
 
 @pytest.mark.parametrize('kind', ['forward', 'overhead'])
@@ -276,17 +281,23 @@ def test_ingest_then_get_state_vs_oracle(V, kind):
 
 def test_ingest_full_size_two_frames_vs_oracle(V):
     """The BASELINE launch size (64 envs x 4 agents = 256 frames, 22 point chunks each) ingested
-    twice in a row (the second frame lands on the first's maps): every agent's overhead / occupancy
-    bitwise vs the oracle, and the key scratch back to zero after each launch."""
+    three times in a row (each frame lands on the previous one's maps, whose keys carry an older
+    epoch; the third launch wraps the epoch, so the key map is zeroed first): every agent's
+    overhead / occupancy bitwise vs the oracle, and no key newer than its launch's epoch."""
     synthetic, vector_env = V
     from simaps import batch, camera
     scenes = [synthetic.make_scene('lifting_4-small_divider', 400 + e) for e in range(64)]
     b = batch.StateBatch(scenes)
     spec = camera.CAMERAS['forward']
-    for rep in range(2):
+    for rep in range(3):
         frames = [synthetic.camera_images(scenes[e], a, 'forward', seed=97 * rep + 5 * e + a) for e, a in b.agents]
+        if rep == 2:
+            b._epoch = 255  # the next launch wraps: zero the key map, epoch 1
         b.ingest(np.stack([f[0] for f in frames]), np.stack([f[1] for f in frames]), camera='forward')
-        assert int(b._keys.abs().sum()) == 0
+        assert b._epoch == (rep + 1 if rep < 2 else 1)
+        # keys untouched since the last zeroing, or of this or an earlier launch's epoch; after the
+        # wrap only this launch's
+        assert max(_key_epochs(b)) == b._epoch and (rep < 2 or _key_epochs(b) <= {0, 1})
         for n, (e, a) in enumerate(b.agents):
             s, r = scenes[e], scenes[e]['robots'][a]
             O.ingest(s['overhead'][a], s['occupancy'][a], frames[n][0], frames[n][1],
