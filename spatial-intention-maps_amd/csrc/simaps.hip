@@ -3418,19 +3418,23 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
             // Each cell's tag is written by its points (any one wins); points whose cell owns the
             // slot max-reduce there, the others (collisions) go straight to the global key map;
             // then one global atomic per used slot.
-            constexpr int HS = INGEST_WIN * 2 / 3;  // keys (8 B) + tags (4 B) in the 32 KB window
+            constexpr int HS = INGEST_WIN * 2 / 3;  // keys (8 B) + tags (4 B) in the window's LDS
             unsigned long long *hk = win;
             int *ht = reinterpret_cast<int *>(win + HS);
+            // slot: the cell's index in the box (row-major) mod HS -- neighbouring cells of a row
+            // take neighbouring slots (the packed cell itself mod HS would fold rows 16 columns apart
+            // onto one slot)
+            auto slot = [&](int c) { return (unsigned)(((c >> 16) - bi) * bw + ((c & 0xffff) - bj)) % HS; };
             for (int e = tid; e < HS; e += INGEST_WG) hk[e] = 0ull, ht[e] = -1;
             __syncthreads();
 #pragma unroll
             for (int q = 0; q < INGEST_PPT; q++)
-                if (cell[q] >= 0) ht[(unsigned)cell[q] % HS] = cell[q];
+                if (cell[q] >= 0) ht[slot(cell[q])] = cell[q];
             __syncthreads();
 #pragma unroll
             for (int q = 0; q < INGEST_PPT; q++)
                 if (cell[q] >= 0) {
-                    const int h = (unsigned)cell[q] % HS;
+                    const int h = slot(cell[q]);
                     if (ht[h] == cell[q]) atomicMax(&hk[h], key[q]);
                     else atomicMax(&keys[base + (cell[q] >> 16) * W + (cell[q] & 0xffff)], key[q]);
                 }

@@ -637,3 +637,27 @@ def test_path_launch_in_graph_capture(V):
         for n, c in enumerate(cnt):
             assert c >= 2 and np.array_equal(xy[n, :c], got[0][n, :c]), n
     assert (got[1] > 2).sum() >= 8  # detours
+
+
+def test_path_scratch_growth(V):
+    """The early-exit kernels' per-stream fixpoint scratch grows with the launch (a small launch
+    first, then one ~30x larger on the same stream, then the small one again): every launch equals
+    the compact kernel's paths."""
+    synthetic, _ = V
+    from simaps import _lib, batch
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 300 + e) for e in range(80)]
+    b = batch.StateBatch(scenes)
+    rs = np.random.RandomState(5)
+    rl, rw = scenes[0]['room_length'], scenes[0]['room_width']
+    psrc = np.array([scenes[e]['robots'][a]['position'][:2] for e, a in b.agents])
+    ptgt = np.stack([rs.uniform(0.05, rl / 2, b.N) * -np.sign(psrc[:, 0]), rs.uniform(-rw / 2, rw / 2, b.N)], -1)
+    prev = _lib.lib.simaps_path_mode(1)
+    try:
+        want = b.shortest_paths(psrc, ptgt)
+        _lib.lib.simaps_path_mode(2)
+        for n in (10, b.N, 10):
+            got = b.shortest_paths(psrc[:n], ptgt[:n], slots=list(range(n)))
+            assert got == want[:n], n
+    finally:
+        _lib.lib.simaps_path_mode(prev)
+    assert sum(len(p) > 2 for p in want) >= 50  # detours: the SPFA runs
