@@ -2703,7 +2703,10 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         // live entries queue[qh .. qt) (mod cells); front == queue[qh]; second == queue[qh + 1] when
         // count >= 2 (prefetched one pop ahead, so the SLF front's distance is read in the same round
         // as the popped vertex's edges instead of after them)
-        int qh = 0, qt = 1, count = 1, front = su, second = su;
+        // (front / second start from the uniform su as SGPR values: a VGPR start would make the
+        // loop carry them in VGPRs, with a move and a readfirstlane each per pop)
+        const int su_s = __builtin_amdgcn_readfirstlane(su);
+        int qh = 0, qt = 1, count = 1, front = su_s, second = su_s;
         // (the wave's stores below are made by every lane with the same address and value: no exec
         // masking around them)
         lds_float *Ld = (lds_float *)dist;
