@@ -113,3 +113,19 @@ def test_ingest_chunk_count_and_argument_checks():
     assert L.simaps_ingest(c, wide, 1, *([p] * 9), 1, None) == _lib.EUNSUPPORTED
     for epoch in (0, 256):  # the key map's launch epoch (refused before any launch)
         assert L.simaps_ingest(c, cam, 1, *([p] * 9), epoch, None) == _lib.EINVAL
+
+
+def test_path_mode_setter():
+    """simaps_path_mode returns the previous mode, accepts 0 (automatic = early exit), 1 (compact)
+    and 2 (early exit) and refuses anything else without changing the mode (host-side only)."""
+    from simaps import _lib
+    L = _lib.lib
+    prev = L.simaps_path_mode(1)
+    try:
+        assert L.simaps_path_mode(2) == 1
+        assert L.simaps_path_mode(0) == 2
+        for bad in (-1, 3):
+            assert L.simaps_path_mode(bad) == _lib.EINVAL
+        assert L.simaps_path_mode(0) == 0  # unchanged by the refused calls
+    finally:
+        L.simaps_path_mode(prev)
