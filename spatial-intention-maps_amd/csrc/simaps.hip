@@ -2734,8 +2734,10 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     const int q2 = qh + 1 == cells ? 0 : qh + 1;
                     const int v = u + doff;
                     // one round of reads (in-order LDS sees this wave's earlier writes); the ballots below
-                    // consume them together.  Lane 8's v is u: its pin read is u's (parent bits to keep).
-                    const float du = Ld[u], dv = Ld[v];
+                    // consume them together.  Lane 8's v is u: its pin read is u's (parent bits to keep)
+                    // and its distance read is u's (no separate read of dist[u]).
+                    const float dv = Ld[v];
+                    const float du = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), 8));
                     const int pv = Li[v];
                     // the front's distance before this pop's relaxations (F0 is a queue entry, < cells, when
                     // count >= 1; otherwise unused, and clamped so the read stays inside the array)
