@@ -2747,7 +2747,8 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     // (lanes >= 8: v = u, so nd = du + 1 > dv: never `better`; no lane test needed)
                     const bool better = nd < dv;
                     const uint64_t imp = __builtin_amdgcn_ballot_w64(better);
-                    const uint64_t notq = __builtin_amdgcn_ballot_w64(!(pv & 0x10));
+                    // not queued: bit 4 clear, i.e. pv < 16 (a pin byte is at most 0x18: one compare)
+                    const uint64_t notq = __builtin_amdgcn_ballot_w64(pv < 16);
                     Li[u] = (uint8_t)(__builtin_amdgcn_readlane(pv, 8) & 0xf);  // u leaves the queue (pyx:92)
                     int nf = F0, nsecond = __builtin_amdgcn_readfirstlane(third);
                     if (imp) {
