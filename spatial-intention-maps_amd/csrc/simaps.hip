@@ -2656,6 +2656,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         const bool fr = rr >= 1 && rr <= h && cc >= 1 && cc <= w && b_test(S.freeb[rr - 1], cc - 1);
         dist[k] = fr ? (EARLY ? INFINITY : INFR) : -INFINITY;  // (EARLY: the sweeps' initial state)
         pin[k] = 0;
+        queue[k] = 0;  // (every ring slot holds a cell index: the prefetched `second` needs no clamp)
     }
     const int su = (sh.src_s[0][0] - sh.i0 + 1) * pw + (sh.src_s[0][1] - sh.j0 + 1);
     const int tv = (sh.src_s[1][0] - sh.i0 + 1) * pw + (sh.src_s[1][1] - sh.j0 + 1);
@@ -2706,7 +2707,8 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         // (front / second start from the uniform su as SGPR values: a VGPR start would make the
         // loop carry them in VGPRs, with a move and a readfirstlane each per pop)
         const int su_s = __builtin_amdgcn_readfirstlane(su);
-        int qh = 0, qt = 1, count = 1, front = su_s, second = su_s;
+        // (qn: the slot after qh, carried so that a pop computes one ring wrap, not two)
+        int qh = 0, qn = 1, qt = 1, count = 1, front = su_s, second = su_s;
         // (the wave's stores below are made by every lane with the same address and value: no exec
         // masking around them)
         lds_float *Ld = (lds_float *)dist;
@@ -2725,13 +2727,15 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         // (EARLY) an early-exit check
         if (count > 0)
             for (;;) {
+                int left = lim - pops;  // pops of this round (the common pop's one exit test: min(count, left))
                 for (;;) {
                     // (front / second are wave-uniform: keep them in SGPRs across the loop)
                     const int u = __builtin_amdgcn_readfirstlane(front);
-                    qh = qh + 1 == cells ? 0 : qh + 1;
+                    qh = qn;
                     count--;                           // entries queue[qh .. qt) after the pop
                     const int F0 = __builtin_amdgcn_readfirstlane(second);  // the next front (valid if count >= 1)
                     const int q2 = qh + 1 == cells ? 0 : qh + 1;
+                    qn = q2;
                     const int v = u + doff;
                     // one round of reads (in-order LDS sees this wave's earlier writes); the ballots below
                     // consume them together.  Lane 8's v is u: its pin read is u's (parent bits to keep)
@@ -2739,9 +2743,9 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     const float dv = Ld[v];
                     const float du = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), 8));
                     const int pv = Li[v];
-                    // the front's distance before this pop's relaxations (F0 is a queue entry, < cells, when
-                    // count >= 1; otherwise unused, and clamped so the read stays inside the array)
-                    const float dF0 = Ld[(unsigned)F0 < (unsigned)cells ? F0 : 0];
+                    // the front's distance before this pop's relaxations (F0 is a ring slot's content, a cell
+                    // index, always: unused when count == 0)
+                    const float dF0 = Ld[F0];
                     const int third = Lq[q2];          // queue[qh + 1]: the next pop's second (if count >= 2)
                     const float nd = du + wl;
                     // (lanes >= 8: v = u, so nd = du + 1 > dv: never `better`; no lane test needed)
@@ -2836,9 +2840,10 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     }
                     front = nf;
                     second = nsecond;
-                    ++pops;
-                    if (count <= 0 || pops >= lim) break;
+                    --left;
+                    if (min(count, left) <= 0) break;  // (count, left >= 0)
                 }
+                pops = lim - left;
                 if (count <= 0 || pops >= SIMAPS_POP_CAP) break;
                 // (EARLY only: lim < SIMAPS_POP_CAP) early exit: every 32 pops, is the target at its final
                 // distance and then every vertex of its parent chain?  The chain is walked in LDS (one
