@@ -2581,6 +2581,9 @@ __device__ __forceinline__ bool line_free(const SH &sh, const SsspScratch &S, in
 #ifndef SIMAPS_POP_CAP  // the diagnostic build (tests/test_gpu_faults.py) lowers it to exercise the fault path
 #define SIMAPS_POP_CAP (1 << 24)
 #endif
+#ifndef SIMAPS_SPFA_RING  // > 0: the diagnostic ring build (tests/test_gpu_faults.py) -- a queue ring of at most
+#define SIMAPS_SPFA_RING 0  // this many slots, so that the ring wraps many times per query (the product's
+#endif                      // ring has one slot per cell and rarely wraps); a live queue past it is a fault
 constexpr int PNT = 256;  // path workgroup: 4 waves (build_cspace needs >= 4 for its row blocks)
 constexpr int PATH_SMALL_CELLS = 4608;  // >= (44 + 2) * 95: every small_* room
 struct PathHdr {
@@ -2701,12 +2704,13 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         const uint8_t pbits = (uint8_t)((lane + 1) | 0x10);  // a relaxed head: parent edge `lane`, queued
         if (lane == 0) { dist[su] = 0.0f; queue[0] = (uint16_t)su; pin[su] = 0x10; }
         __builtin_amdgcn_wave_barrier();
-        // live entries queue[qh .. qt) (mod cells); front == queue[qh]; second == queue[qh + 1] when
+        // live entries queue[qh .. qt) (mod ring); front == queue[qh]; second == queue[qh + 1] when
         // count >= 2 (prefetched one pop ahead, so the SLF front's distance is read in the same round
         // as the popped vertex's edges instead of after them)
         // (front / second start from the uniform su as SGPR values: a VGPR start would make the
         // loop carry them in VGPRs, with a move and a readfirstlane each per pop)
         const int su_s = __builtin_amdgcn_readfirstlane(su);
+        const int ring = SIMAPS_SPFA_RING > 0 && SIMAPS_SPFA_RING < cells ? SIMAPS_SPFA_RING : cells;
         // (qn: the slot after qh, carried so that a pop computes one ring wrap, not two)
         int qh = 0, qn = 1, qt = 1, count = 1, front = su_s, second = su_s;
         // (the wave's stores below are made by every lane with the same address and value: no exec
@@ -2734,7 +2738,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     qh = qn;
                     count--;                           // entries queue[qh .. qt) after the pop
                     const int F0 = __builtin_amdgcn_readfirstlane(second);  // the next front (valid if count >= 1)
-                    const int q2 = qh + 1 == cells ? 0 : qh + 1;
+                    const int q2 = qh + 1 == ring ? 0 : qh + 1;
                     qn = q2;
                     const int v = u + doff;
                     // one round of reads (in-order LDS sees this wave's earlier writes); the ballots below
@@ -2784,7 +2788,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                                 Lq[qt] = (uint16_t)content;
                                 if (sw) { Lq[qh] = (uint16_t)vp; nf = vp; }
                                 if (count == 1) nsecond = content;  // the tail slot was queue[qh + 1]
-                                qt = qt + 1 == cells ? 0 : qt + 1;
+                                qt = qt + 1 == ring ? 0 : qt + 1;
                                 count++;
                             } else {
                                 const bool isP = (push >> lane) & 1;
@@ -2825,14 +2829,14 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                                     if (sw) content = prev >= 0 ? prev : Fq;
                                     newfront = __builtin_amdgcn_readlane(v, 63 - __builtin_clzll(swm));
                                 }
-                                const int slot = qt + rank < cells ? qt + rank : qt + rank - cells;
+                                const int slot = qt + rank < ring ? qt + rank : qt + rank - ring;
                                 if (isP) Lq[slot] = (uint16_t)content;
                                 if (sF0) Lq[qh] = (uint16_t)newfront;  // after the lanes' stores (in the empty case qh is p1's slot)
                                 if (count <= 1) {  // the pushes wrote queue[qh + 1]: the next pop's second
                                     const uint64_t at = __ballot(isP && slot == q2);
                                     if (at) nsecond = __builtin_amdgcn_readlane(content, __builtin_ctzll(at));
                                 }
-                                qt = qt + np < cells ? qt + np : qt + np - cells;
+                                qt = qt + np < ring ? qt + np : qt + np - ring;
                                 count += np;
                                 nf = newfront;
                             }
@@ -2841,6 +2845,8 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     front = nf;
                     second = nsecond;
                     --left;
+                    if constexpr (SIMAPS_SPFA_RING > 0)
+                        if (count > ring && lane == 0) sh.fault |= SIMAPS_FAULT_ROUNDS;  // (diagnostic ring overflowed)
                     if (min(count, left) <= 0) break;  // (count, left >= 0)
                 }
                 pops = lim - left;
