@@ -45,10 +45,14 @@ class VectorEnvObservations:
         batches and returns a structure of views built once per ring slot (no per-call allocation
         or per-robot view creation: ~0.2 ms of host time per 256 stacks).  The states of a call are
         then overwritten R calls later -- copy what must live longer (the reference returns fresh
-        arrays; the default R = 0 keeps that)."""
+        arrays; the default R = 0 keeps that).  With numpy=True the ring slots also hold a pinned
+        host copy: one asynchronous device->host copy per call into page-locked memory, returned as
+        NumPy views (a fresh pageable copy per call otherwise)."""
         self.batch = _batch.StateBatch(scenes, device=device, layout=layout)
         self._ring = [None] * int(reuse_outputs)
         self._ring_k = 0
+        self._hring = [None] * int(reuse_outputs)  # (device batch, pinned host batch, NumPy views)
+        self._hring_k = 0
         self.groups = [robot_groups(s) for s in scenes]
         self.slot = {ea: n for n, ea in enumerate(self.batch.agents)}
         self.num_envs = len(scenes)
@@ -100,6 +104,22 @@ class VectorEnvObservations:
                 self._ring[k] = (buf, [[[rows[q] for q in g] for g in env] for env in self._all_slots])
             buf, views = self._ring[k]
             self.batch.render(out=buf, stream=stream)
+            return views
+        if (all_robots or awaiting is None) and self._hring and numpy:
+            k = self._hring_k
+            self._hring_k = (k + 1) % len(self._hring)
+            if self._hring[k] is None:
+                buf = self.batch.alloc_state()
+                host = torch.empty(buf.shape, dtype=buf.dtype, pin_memory=True)
+                rows = self.batch.as_hwc(host).numpy()
+                self._hring[k] = (buf, host, [[[rows[q] for q in g] for g in env] for env in self._all_slots])
+            buf, host, views = self._hring[k]
+            s = stream if stream is not None else torch.cuda.current_stream(self.batch.device)
+            self.batch.render(out=buf, stream=s)
+            with torch.cuda.stream(s):
+                host.copy_(buf, non_blocking=True)
+            s.synchronize()
+            _lib.check_faults()  # the copy completed: a faulting launch raises here
             return views
         if all_robots or awaiting is None:  # every robot: the batch's own agent list, structure precomputed
             out = self.batch.as_hwc(self.batch.render(stream=stream))

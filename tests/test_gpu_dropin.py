@@ -60,6 +60,40 @@ def test_get_state_structure_and_awaiting_subset(V, layout):
                 assert _bitwise(x.cpu().numpy(), O.agent_state(s, a))
 
 
+@pytest.mark.parametrize('layout', ['hwc', 'chw'])
+def test_reuse_outputs_rings(V, layout):
+    """reuse_outputs=2: the all-robots get_state renders into a ring of two device batches (views
+    built once), and with numpy=True into a ring of pinned host copies; every call's states equal
+    the oracle's bitwise, the same slot's views come back every second call (overwritten in
+    place), and the awaiting-subset path is unaffected."""
+    synthetic, vector_env = V
+    cfg = 'lifting_2_throwing_2-large_empty'
+    scenes = [synthetic.make_scene(cfg, 520 + e) for e in range(3)]
+    want = {(e, a): O.agent_state(s, a) for e, s in enumerate(scenes) for a in range(len(s['robots']))}
+    obs = vector_env.VectorEnvObservations(scenes, layout=layout, reuse_outputs=2)
+    seen_dev, seen_host = [], []
+    for call in range(4):
+        dev = obs.get_state()
+        host = obs.get_state(numpy=True)
+        torch.cuda.synchronize()
+        for e, s in enumerate(scenes):
+            for gd, gh, idx in zip(dev[e], host[e], vector_env.robot_groups(s)):
+                for xd, xh, a in zip(gd, gh, idx):
+                    assert isinstance(xd, torch.Tensor) and isinstance(xh, np.ndarray)
+                    assert xh.shape == (96, 96, 5) and xh.dtype == np.float32
+                    assert _bitwise(xd.cpu().numpy(), want[(e, a)]) and _bitwise(xh, want[(e, a)]), (call, e, a)
+        seen_dev.append(dev[0][0][0].data_ptr())
+        seen_host.append(host[0][0][0].__array_interface__['data'][0])
+    assert seen_dev[0] == seen_dev[2] != seen_dev[1] == seen_dev[3]
+    assert seen_host[0] == seen_host[2] != seen_host[1] == seen_host[3]
+    awaiting = [[a % 2 == 0 for a in range(len(s['robots']))] for s in scenes]
+    sub = obs.get_state(awaiting=awaiting, numpy=True)
+    for e, s in enumerate(scenes):
+        for g, idx in zip(sub[e], vector_env.robot_groups(s)):
+            for x, a in zip(g, idx):
+                assert (x is None) == (not awaiting[e][a]) and (x is None or _bitwise(x, want[(e, a)]))
+
+
 def test_get_state_nobody_awaiting(V):
     """A step where no robot awaits an action: every entry None, nothing launched, and the next
     step renders normally."""
