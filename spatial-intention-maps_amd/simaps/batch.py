@@ -439,13 +439,11 @@ class StateBatch:
         if tuple(dep.shape) != want or tuple(seg.shape) != want:
             raise ValueError('depth and seg_raw must be %s' % (want,))
         poses = [self.pose_host[self._robot_off[e] + a] for e, a in (self.agents[k] for k in idx)]
-        params = np.array([spec.params(p[0], p[1], p[2]) for p in poses], dtype=np.float64).reshape(n, 9)
+        params = spec.params_batch(poses).reshape(n, 9)
         ids = np.zeros(len(self.scenes), dtype=_lib.SEG_IDS_DTYPE)
-        for e, sc in enumerate(self.scenes):
-            d = (seg_ids[e] if seg_ids is not None else synthetic.SEG_IDS)
-            for f in ('min_obstacle', 'max_obstacle', 'receptacle', 'min_cube', 'max_cube'):
-                ids[e][f] = d[f]
-            ids[e]['has_receptacle'] = sc['receptacle_position'] is not None
+        for f in ('min_obstacle', 'max_obstacle', 'receptacle', 'min_cube', 'max_cube'):
+            ids[f] = [seg_ids[e][f] for e in range(len(self.scenes))] if seg_ids is not None else synthetic.SEG_IDS[f]
+        ids['has_receptacle'] = [sc['receptacle_position'] is not None for sc in self.scenes]
         if getattr(self, '_keys', None) is None:  # (epoch-tagged from here on: launch_ingest)
             self._keys = torch.zeros((self.N, self.H, self.W), dtype=torch.int64, device=self.device)
             self._epoch = 0

@@ -11,6 +11,8 @@ runs on the GPU (simaps_ingest).
 """
 import math
 
+import numpy as np
+
 from . import constants as K
 
 ROBOT_HEIGHT = 0.07          # Robot.HEIGHT (envs.py:809)
@@ -43,6 +45,33 @@ class CameraSpec:
                   math.cos(math.radians(90 + -30)) * math.sin(heading),
                   math.sin(math.radians(90 + -30)))
         return [float(v) for v in pos + tgt + up]
+
+    def params_batch(self, poses):
+        """params() of every (x, y, heading) in `poses` as an [n, 9] float64 array, bitwise equal:
+        cos / sin come from Python's math per robot (numpy's SIMD kernels may round differently),
+        the rest is the same IEEE products and sums, elementwise."""
+        p = np.asarray(poses, dtype=np.float64).reshape(-1, 3)
+        x, y = p[:, 0], p[:, 1]
+        ch = np.array([math.cos(h) for h in p[:, 2].tolist()], dtype=np.float64)
+        sh = np.array([math.sin(h) for h in p[:, 2].tolist()], dtype=np.float64)
+        out = np.empty((len(p), 9), dtype=np.float64)
+        if self.name == 'overhead':
+            out[:, 0], out[:, 1], out[:, 2] = x, y, 1.0
+            out[:, 3], out[:, 4], out[:, 5] = x, y, 0.0
+            out[:, 6], out[:, 7], out[:, 8] = ch, sh, 0.0
+        else:
+            off = ROBOT_BACKPACK_OFFSET + ROBOT_TOP_LENGTH + 0.002
+            toff = ROBOT_HEIGHT * math.tan(math.radians(90 + -30))
+            cu = math.cos(math.radians(90 + -30))
+            out[:, 0] = x + off * ch
+            out[:, 1] = y + off * sh
+            out[:, 2] = ROBOT_HEIGHT
+            out[:, 3] = out[:, 0] + toff * ch
+            out[:, 4] = out[:, 1] + toff * sh
+            out[:, 5] = 0.0
+            out[:, 6], out[:, 7] = cu * ch, cu * sh
+            out[:, 8] = math.sin(math.radians(90 + -30))
+        return out
 
 
 # ForwardFacingCamera (use_partial_observations, envs.py:2019-2022, 1980-1985) / OverheadCamera (1965-1969)

@@ -249,3 +249,17 @@ def test_rotate_rounding_changes_reference_states(cfg):
         got = O.AgentOracle(dict(scene, rotate_rounding='fma'), a).get_state()
         differ += not np.array_equal(got.view(np.int32), z[pre + 'state'].view(np.int32))
     assert differ >= 4, differ
+
+
+def test_camera_params_batch_bitwise():
+    """CameraSpec.params_batch (what StateBatch.prepare_ingest packs) equals the per-robot params()
+    restatement of _get_camera_params (envs.py:1974-2008) bitwise, both cameras, including headings
+    on exact multiples of pi / 2 and -0."""
+    from simaps import camera
+    rs = np.random.RandomState(11)
+    poses = np.stack([rs.uniform(-3, 3, 4096), rs.uniform(-3, 3, 4096), rs.uniform(-7, 7, 4096)], 1)
+    poses[:6, 2] = [0.0, -0.0, np.pi, -np.pi, np.pi / 2, -np.pi / 2]
+    for kind, spec in camera.CAMERAS.items():
+        want = np.array([spec.params(*p) for p in poses.tolist()], dtype=np.float64)
+        got = spec.params_batch(poses)
+        assert got.shape == (4096, 9) and np.array_equal(got.view(np.int64), want.view(np.int64)), kind
