@@ -178,6 +178,24 @@ class VectorEnvObservations:
         return [[[float(x) for x in d[self.slot[(e, a)], :len(positions[e][a])]] for a in range(len(positions[e]))]
                 for e in range(self.num_envs)]
 
+    # -- movement paths -------------------------------------------------------
+    def shortest_path(self, requests, stream=None):
+        """Mapper.shortest_path(source_position, target_position) (envs.py:2186-2187 ->
+        OccupancyMap.shortest_path, 2478-2505), as Robot.store_new_action calls it (875-876), for a
+        batch: requests [((env, robot), source_position, target_position), ...] -> one waypoint list
+        per request on that robot's own map, like the reference's: the caller's source / target
+        objects at the two ends (envs.py:2486, 2500-2503), (x, y, 0) tuples between.  One launch;
+        a robot may appear in several requests."""
+        if not requests:
+            return []
+        slots = [self.slot[(int(ea[0]), int(ea[1]))] for ea, _, _ in requests]
+        src = np.array([[float(s[0]), float(s[1])] for _, s, _ in requests], dtype=np.float64)
+        tgt = np.array([[float(t[0]), float(t[1])] for _, _, t in requests], dtype=np.float64)
+        paths = self.batch.shortest_paths(src, tgt, slots=slots, stream=stream)
+        for p, (_, s, t) in zip(paths, requests):
+            p[0], p[-1] = s, t
+        return paths
+
 
 class GridGraph:
     """shortest_paths.pyx GridGraph (pyx:10-167) on the device: 8-connected grid over cells with

@@ -241,6 +241,38 @@ def test_shortest_path_reference_goldens(V, path_mode):
     assert nontrivial >= 40
 
 
+def test_dropin_shortest_path_reference_goldens(V):
+    """VectorEnvObservations.shortest_path (Mapper.shortest_path, envs.py:2186-2187, as
+    Robot.store_new_action calls it, 875-876) against the reference's paths.npz: the waypoints
+    between the ends exactly, the caller's own source / target objects at the ends (envs.py:2486,
+    2500-2503), and repeated robots in one batch."""
+    synthetic, vector_env = V
+    z = G.load('paths.npz')
+    groups = {}
+    for k in z.files:
+        if not k.endswith('_path') or k.startswith('demo'):
+            continue
+        key = k[:-len('_path')]
+        head, q = key.rsplit('_q', 1)
+        cfg, rest = head.rsplit('_e', 1)
+        e, a = (int(x) for x in rest.split('_a'))
+        groups.setdefault(cfg, []).append((e, a, key))
+    n = 0
+    for cfg, items in groups.items():
+        obs = vector_env.VectorEnvObservations([synthetic.make_scene(cfg, 60 + e) for e in range(2)])
+        reqs = [((e, a), tuple(z[k + '_src'].tolist()) + (0.0123,), list(z[k + '_tgt'].tolist())) for e, a, k in items]
+        got = obs.shortest_path(reqs)
+        assert len(got) == len(items)
+        for (e, a, key), (_, s, t), path in zip(items, reqs, got):
+            want = z[key + '_path']
+            assert path[0] is s and path[-1] is t, key
+            assert np.array_equal(np.array([p[:2] for p in path]), want), key
+            assert all(len(p) == 3 and p[2] == 0 for p in path[1:-1]), key
+            n += 1
+    assert n >= 200
+    assert obs.shortest_path([]) == []
+
+
 def test_maze_paths_reference_goldens(V, path_mode):
     """Movement paths on the maze environments (large_doors / tunnels / rooms) vs the reference's
     own OccupancyMap.shortest_path: long detours through doors and tunnels, exactly."""
