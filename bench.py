@@ -55,7 +55,7 @@ def rank_envs(rank, envs_per_rank, world=1, total_envs=None):
     return list(range(lo, lo + q + (1 if rank < r else 0)))
 
 
-def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu'):
+def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu', own=None):
     """The bench contract's timed region: `warmup` untimed steps, then barrier + sync, EXACTLY
     `steps` steps, sync + barrier; returns the wall time, max-reduced over ranks (every rank gets
     the job time).  step(k) runs step k (k < 0 for warmup); sync() waits for the device."""
@@ -75,6 +75,8 @@ def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu'):
     if coll:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if own is not None:
+        own.append(elapsed)  # this rank's own timed region (the rank report)
     return max_over_ranks([elapsed], world, reduce_device)[0]
 
 
@@ -98,6 +100,37 @@ def sum_over_ranks(values, world, device='cpu'):
     t = torch.tensor(values, dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(x) for x in t.cpu()]
+
+
+def device_identity(device=None):
+    """Which physical GPU this rank renders on: index, name, PCI domain:bus:device (or the device
+    UUID when torch does not expose the PCI ids); {'device': 'cpu'} without a GPU (gloo tests)."""
+    import torch
+    if device is None or getattr(device, 'type', device) == 'cpu' or not torch.cuda.is_available():
+        return {'device': 'cpu'}
+    idx = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    p = torch.cuda.get_device_properties(idx)
+    out = {'device': 'cuda:%d' % idx, 'name': p.name}
+    if all(hasattr(p, a) for a in ('pci_domain_id', 'pci_bus_id', 'pci_device_id')):
+        out['pci'] = '%04x:%02x:%02x' % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+    elif getattr(p, 'uuid', None) is not None:
+        out['pci'] = 'uuid:%s' % p.uuid
+    return out
+
+
+def rank_report(row, world):
+    """every rank's own counters (rank, device identity, stacks per step, its timed
+    seconds, its kernel ms, ...) all-gathered to every rank, with the process group's own view of
+    the job -- its world size and backend -- so that an N-GPU bench line shows by itself that N
+    ranks ran on N distinct devices.  Without a process group: the one row, world 1, backend None."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return {'world_size': 1, 'backend': None, 'ranks': [row], 'distinct_devices': 1}
+    rows = [None] * dist.get_world_size()
+    dist.all_gather_object(rows, row)
+    devs = {r.get('pci') or '%s/%s/%s' % (r.get('host'), r.get('device'), r.get('rank')) for r in rows}
+    return {'world_size': dist.get_world_size(), 'backend': str(dist.get_backend()), 'ranks': rows,
+            'distinct_devices': len(devs)}
 
 
 def gather_states(out, reps, world, rank, return_data=False):
@@ -170,7 +203,8 @@ def main():
     strong = args.total_envs is not None
     if strong and args.total_envs < world:
         raise SystemExit('--total-envs must give every rank at least one env')
-    scenes = [synthetic.make_scene(args.config, e) for e in rank_envs(rank, args.envs, world, args.total_envs)]
+    env_ids = rank_envs(rank, args.envs, world, args.total_envs)
+    scenes = [synthetic.make_scene(args.config, e) for e in env_ids]
     b = batch.StateBatch(scenes, device='cuda', layout=args.layout)
     out = b.alloc_state()
     stream = torch.cuda.current_stream()
@@ -187,8 +221,14 @@ def main():
         if k == args.steps - 1:
             ev1.record(stream)
 
-    elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, red)
-    kern_ms = max_over_ranks([ev0.elapsed_time(ev1) / args.steps], world, red)[0]
+    own = []
+    elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, red, own)
+    own_ms = ev0.elapsed_time(ev1) / args.steps
+    kern_ms = max_over_ranks([own_ms], world, red)[0]
+    import socket
+    ranks = rank_report(dict(device_identity(torch.device('cuda', local)), rank=rank, local_rank=local,
+                             host=socket.gethostname(), env_range=[env_ids[0], env_ids[-1]],
+                             stacks_per_step=b.N, steps=args.steps, seconds=own[0], kernel_ms=own_ms), world)
 
     stacks_per_step = int(sum_over_ranks([b.N], world, red)[0])
     value = stacks_per_step * args.steps / elapsed
@@ -227,6 +267,7 @@ def main():
                          'algorithmic_bytes_per_stack': B},
         }
         res['config'].update({'total_envs': args.total_envs} if strong else {'envs_per_gpu': args.envs})
+        res['distributed'] = ranks
         if gather is not None:
             res['gather'] = gather
         if world == 1 and not args.no_cpu_baseline:

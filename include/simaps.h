@@ -229,8 +229,9 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
  * the previous mode): 0 automatic (= 2), 1 compact (the SPFA runs to an empty queue), 2 early exit
  * (the SSSP fixpoint by directional sweeps first, then the SPFA only until every vertex of the
  * target's parent chain has its final distance -- whose parent then can no longer change; the
- * fixpoint is parked in a library-owned device buffer per stream, grown outside graph capture -- a
- * launch that would need to grow it during capture takes the compact kernels).  Both return the
+ * fixpoint is parked in device scratch taken from the default memory pool in stream order on the
+ * launch stream and returned right after the launch -- a launch being captured into a graph takes
+ * the compact kernels instead).  Both return the
  * reference's waypoints exactly. */
 int simaps_path_mode(int mode);
 
@@ -241,11 +242,16 @@ int simaps_path_mode(int mode);
  *   scratch tagged with `epoch`: all zero before the first launch, then never cleared by the
  *   library -- each launch passes an epoch in [1, 255] larger than every earlier launch's on this
  *   key map since it was last zeroed (when the epoch would wrap, zero the key map and restart at
- *   1); boxes: uint32 [N, simaps_ingest_chunks(Hc, Wc), 4] scratch (any contents).  The frames'
+ *   1).  epoch 0 is the zeroing mode: the key map must be all zero on entry, and the launch zeroes
+ *   every key it wrote before it ends (one store per touched key more), so it is all zero on exit
+ *   -- the only mode allowed while `stream` is being captured into a graph, whose replays all
+ *   reuse the captured epoch; boxes: uint32 [N, simaps_ingest_chunks(Hc, Wc), 4] scratch (any
+ *   contents).  The frames'
  *   map slots must be distinct.  All DEVICE.  Points with equal z on one pixel: the later camera
  *   pixel wins (the reference's np.argsort leaves that order unspecified).
- *   SIMAPS_EINVAL: epoch outside [1, 255].
- *   SIMAPS_EUNSUPPORTED: camera width outside [67, 1024], Hc * Wc >= 2^20, N > 65535
+ *   SIMAPS_EINVAL: epoch outside [0, 255].
+ *   SIMAPS_EUNSUPPORTED: camera width outside [67, 1024], Hc * Wc >= 2^20, N > 65535, or an epoch
+ *   other than 0 while `stream` is capturing
  *   (two launches on `stream`: a point pass over chunks of 2048 camera pixels with per-chunk LDS
  *   max-reduction that also records each chunk's box of touched map pixels, then one sweep of each
  *   frame's box). */

@@ -387,7 +387,7 @@ class AgentOracle:
         self.occupancy = scene['occupancy'][agent]
         self.overhead_wo = scene['overhead'][agent]
         self.receptacle = scene['receptacle_position']
-        self.rounding = scene.get('rotate_rounding', 'fma')  # host BLAS out_center rounding (oracle_c.c)
+        self.rounding = K.scene_rotate_rounding(scene)  # host BLAS out_center rounding (oracle_c.c)
         self._update()
 
     # OccupancyMap.update (envs.py:2445-2460), minus the point scatter (occupancy is the input)

@@ -3378,7 +3378,7 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
             // past Wc); its points from q = Wc - j0 on lie in the next row
             float B0[3], B1[3];
 #pragma unroll
-            for (int c = 0; c < 3; c++) B0[c] = Bt[c][ir0], B1[c] = Bt[c][ir0 + 1];
+            for (int c = 0; c < 3; c++) B0[c] = Bt[c][ir0], B1[c] = Bt[c][min(ir0 + 1, INGEST_MAX_ROWS - 1)];  // (B1 only matters below the last row)
             int i = i0, j = j0;
 #pragma unroll
             for (int q = 0; q < INGEST_PPT; q++, j = (j + 1 == Wc) ? (i++, 0) : j + 1) {
@@ -3486,9 +3486,13 @@ __global__ void __launch_bounds__(INGEST_WG) ingest_points_kernel(
 // viewing wedge: ~half of the frame's bounding box).  Rows are dealt round-robin over the frame's
 // INGEST_RES_G * 4 waves, two rows in flight per wave; the lanes sweep a row's columns.  Each wave
 // reads the chunk boxes itself (lane c: box c), so no barrier.
+// ZERO (simaps_ingest's epoch 0, the graph-replayable mode): the launch's keys carry tag 1 on a key
+// map that is all zero on entry, and every nonzero key read here is zeroed again, so the map is all
+// zero on exit -- every replay of a captured launch starts from the same state.
+template <bool ZERO>
 __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
     simaps_config cfg, const simaps_agent *__restrict__ agents, float *__restrict__ overhead,
-    const unsigned long long *__restrict__ keys, const unsigned *__restrict__ boxes, int nch, unsigned epoch)
+    unsigned long long *__restrict__ keys, const unsigned *__restrict__ boxes, int nch, unsigned epoch)
 {
     const int n = blockIdx.y, lane = threadIdx.x & 63, W = cfg.W;
     const int gw = blockIdx.x * (INGEST_RES_WG / 64) + (threadIdx.x >> 6), nw = INGEST_RES_G * (INGEST_RES_WG / 64);
@@ -3531,8 +3535,10 @@ __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
                 kv[u] = c < hi[t] ? keys[idx[u]] : 0ull;
             }
 #pragma unroll
-            for (int u = 0; u < R * U; u++)
+            for (int u = 0; u < R * U; u++) {
                 if ((unsigned)(kv[u] >> 56) == epoch) overhead[idx[u]] = (float)(kv[u] & 15ull) * 0.125f;
+                if (ZERO && kv[u]) keys[idx[u]] = 0ull;
+            }
         }
     }
 }
@@ -3660,49 +3666,47 @@ bool path_early(int /*n*/, bool /*small*/)
     return g_path_mode.load() != 1;
 }
 
-// Device scratch of the early-exit path kernels (the SSSP fixpoint, CELLS f32 per query), one buffer
-// per (device, stream): launches on one stream are ordered, so its buffer is never shared by two live
-// kernels.  Grown (never shrunk) after the stream drains.  A launch being captured into a graph gets
-// none -- the graph would keep the pointer past a later growth -- and takes the compact kernels (same
+// Device scratch of the early-exit path kernels (the SSSP fixpoint, CELLS f32 per query): stream-
+// ordered, taken from the device's default memory pool right before the launch (hipMallocAsync on the
+// launch stream) and handed back right after it (hipFreeAsync on the same stream), so no buffer is
+// ever shared between launches, threads or streams, and nothing is synchronised.  The pool keeps what
+// it was given (release threshold raised once per device), so after the first launches this is a
+// pool hit.  A launch being captured into a graph gets none and takes the compact kernels (same
 // results) instead.
 struct PathScratch {
-    int dev;
-    hipStream_t st;
-    void *p;
-    size_t bytes;
+    float *p = nullptr;
+    hipStream_t st = nullptr;
+    PathScratch() = default;
+    PathScratch(const PathScratch &) = delete;
+    PathScratch &operator=(const PathScratch &) = delete;
+    ~PathScratch()
+    {
+        if (p) (void)hipFreeAsync(p, st);  // ordered after the launch that uses it
+    }
 };
-std::mutex g_scratch_mu;
-std::vector<PathScratch> g_scratch;
-float *path_scratch(hipStream_t st, size_t bytes)
+std::once_flag g_pool_once[64];
+void path_scratch(PathScratch &ps, hipStream_t st, size_t bytes)
 {
     int dev = 0;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipGetDevice(&dev) != hipSuccess || hipStreamIsCapturing(st, &cap) != hipSuccess ||
         cap != hipStreamCaptureStatusNone)
-        return nullptr;
-    std::lock_guard<std::mutex> lock(g_scratch_mu);
-    PathScratch *e = nullptr;
-    for (auto &x : g_scratch)
-        if (x.dev == dev && x.st == st) e = &x;
-    if (e && e->bytes >= bytes) return (float *)e->p;
-    if (!e) {
-        g_scratch.push_back(PathScratch{dev, st, nullptr, 0});
-        e = &g_scratch.back();
+        return;
+    if (dev >= 0 && dev < 64)
+        std::call_once(g_pool_once[dev], [dev] {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+                uint64_t keep = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+            }
+        });
+    void *p = nullptr;
+    if (hipMallocAsync(&p, bytes, st) != hipSuccess) {
+        (void)hipGetLastError();  // (no scratch: the compact kernels run instead)
+        return;
     }
-    if (e->p) {
-        if (hipStreamSynchronize(st) != hipSuccess) return nullptr;  // its last kernel may still read it
-        (void)hipFree(e->p);
-        e->p = nullptr;
-        e->bytes = 0;
-    }
-    size_t n = (size_t)1 << 20;
-    while (n < bytes) n *= 2;
-    if (hipMalloc(&e->p, n) != hipSuccess) {
-        e->p = nullptr;
-        return nullptr;
-    }
-    e->bytes = n;
-    return (float *)e->p;
+    ps.p = (float *)p;
+    ps.st = st;
 }
 
 int check_cfg(const simaps_config *c)
@@ -3884,7 +3888,9 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
     const Geometry geo = make_geometry();
     const bool small = (cfg->room_h + 2) * ((cfg->room_w + 2) | 1) <= PATH_SMALL_CELLS;
     const hipStream_t st = (hipStream_t)stream;
-    float *scratch = path_early(N, small) ? path_scratch(st, (size_t)N * SIMAPS_MAX_ROOM_CELLS * sizeof(float)) : nullptr;
+    PathScratch ps;
+    if (path_early(N, small)) path_scratch(ps, st, (size_t)N * SIMAPS_MAX_ROOM_CELLS * sizeof(float));
+    float *scratch = ps.p;
 #define SIMAPS_PATH_LAUNCH(C, E)                                                                       \
     hipLaunchKernelGGL((path_kernel<C, E>), dim3(N), dim3(PNT), 0, st, *cfg, geo, agents, envs, robots, occupancy, sources, \
                        targets, max_points, out_xy, out_count, scratch, g_fault_dev)
@@ -3929,7 +3935,17 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
     if (!ingest_width_ok(cam->width_px))
         return fail(SIMAPS_EUNSUPPORTED, "camera width %d outside [%d, %d]", cam->width_px, ingest_min_width(), INGEST_MAX_WC);
     if (np >= (1 << 20)) return fail(SIMAPS_EUNSUPPORTED, "camera frame of %d pixels (key packs pixel + 1 in 20 bits)", np);
-    if (epoch < 1 || epoch > 255) return fail(SIMAPS_EINVAL, "epoch %d not in [1, 255]", epoch);
+    if (epoch < 0 || epoch > 255) return fail(SIMAPS_EINVAL, "epoch %d not in [0, 255]", epoch);
+    {   // a captured launch replays its epoch: only the zeroing mode (epoch 0) leaves nothing behind
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing((hipStream_t)stream, &cap) != hipSuccess)
+            return fail(SIMAPS_EHIP, "hipStreamIsCapturing failed");
+        if (cap != hipStreamCaptureStatusNone && epoch != 0)
+            return fail(SIMAPS_EUNSUPPORTED, "ingest with epoch %d under stream capture: every replay would reuse "
+                        "the epoch; pass epoch 0 (zeroing mode) on an all-zero key map", epoch);
+    }
+    const bool zero_mode = epoch == 0;
+    if (zero_mode) epoch = 1;
     if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d frames per launch (grid y <= 65535)", N);
     const int nch = ingest_chunks(cam->height_px, cam->width_px);  // point-pass chunks per frame
     if ((rc = pending_faults())) return rc;  // (after the argument checks: they need no device)
@@ -3939,8 +3955,12 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
     else
         hipLaunchKernelGGL(ingest_points_kernel<INGEST_MAX_WC>, dim3(nch, N), dim3(INGEST_WG), 0, (hipStream_t)stream, *cfg, *cam,
                            agents, seg_ids, cam_params, depth, seg_raw, occupancy, reinterpret_cast<unsigned long long *>(keys), boxes, (unsigned)epoch);
-    hipLaunchKernelGGL(ingest_resolve_kernel, dim3(INGEST_RES_G, N), dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg, agents, overhead,
-                       reinterpret_cast<const unsigned long long *>(keys), boxes, nch, (unsigned)epoch);
+    if (zero_mode)
+        hipLaunchKernelGGL(ingest_resolve_kernel<true>, dim3(INGEST_RES_G, N), dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg,
+                           agents, overhead, reinterpret_cast<unsigned long long *>(keys), boxes, nch, (unsigned)epoch);
+    else
+        hipLaunchKernelGGL(ingest_resolve_kernel<false>, dim3(INGEST_RES_G, N), dim3(INGEST_RES_WG), 0, (hipStream_t)stream, *cfg,
+                           agents, overhead, reinterpret_cast<unsigned long long *>(keys), boxes, nch, (unsigned)epoch);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "ingest launch: %s", hipGetErrorString(e));
     return 0;
@@ -3960,7 +3980,9 @@ int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *s
     if (const int rc = pending_faults()) return rc;
     const bool small = (wh + 2) * ((ww + 2) | 1) <= PATH_SMALL_CELLS;
     const hipStream_t st = (hipStream_t)stream;
-    float *scratch = path_early(B, small) ? path_scratch(st, (size_t)B * SIMAPS_MAX_ROOM_CELLS * sizeof(float)) : nullptr;
+    PathScratch ps;
+    if (path_early(B, small)) path_scratch(ps, st, (size_t)B * SIMAPS_MAX_ROOM_CELLS * sizeof(float));
+    float *scratch = ps.p;
 #define SIMAPS_GRID_PATH_LAUNCH(C, E)                                                                  \
     hipLaunchKernelGGL((grid_path_kernel<C, E>), dim3(B), dim3(PNT), 0, st, H, W, grids, sources, targets, wi0, wj0, wh, \
                        ww, max_points, out_ij, out_count, scratch, g_fault_dev)

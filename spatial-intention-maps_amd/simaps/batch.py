@@ -182,7 +182,7 @@ class StateBatch:
         s0 = scenes[0]
         for s in scenes:
             if (s['H'], s['W'], s['room_width'], s['room_length']) != (s0['H'], s0['W'], s0['room_width'], s0['room_length']) \
-                    or s['flags'] != s0['flags'] or s.get('rotate_rounding', 'fma') != s0.get('rotate_rounding', 'fma'):
+                    or s['flags'] != s0['flags'] or K.scene_rotate_rounding(s) != K.scene_rotate_rounding(s0):
                 raise ValueError('one StateBatch holds one configuration (grid + flags + rotate rounding)')
         if agents is None:
             agents = [(e, a) for e, s in enumerate(scenes) for a in range(len(s['robots']))]
@@ -192,7 +192,7 @@ class StateBatch:
         self.flags = s0['flags']
         self.H, self.W = s0['H'], s0['W']
         self.cfg = make_config(self.flags, s0['room_width'], s0['room_length'], layout,
-                               s0.get('rotate_rounding', 'fma'))
+                               K.scene_rotate_rounding(s0))
         self.num_robots = len(s0['robots'])
         if self.flags['use_intention_channels'] and any(len(s['robots']) != self.num_robots for s in scenes):
             raise ValueError('intention channels need the same robot count in every env of a batch')
@@ -267,7 +267,7 @@ class StateBatch:
         self._stage_ev[k] = ev
         self.robots_d = dev[:R * _lib.ROBOT_DTYPE.itemsize]
         self.paths_d = dev[self._rob_bytes:]
-        self.pose_host = pose
+        self.pose_host = pose.copy()  # the poses packed above (the caller may update its array in place)
 
     def set_maps(self, occupancy=None, overhead=None, slots=None):
         """Replace the per-agent global maps -- what Mapper.update / OccupancyMap.update produce each
@@ -457,21 +457,58 @@ class StateBatch:
         return {'n': n, 'cam': cam, 'agents': agents_d, 'ids': _to_dev(ids, self.device),
                 'params': torch.from_numpy(params).to(self.device), 'depth': dep, 'seg': seg}
 
+    def reset_ingest_keys(self, stream=None):
+        """Zero the ingest key map now (on `stream`).  Call it before capturing ingest() into a CUDA
+        graph after eager ingests: otherwise the capture has to include that zeroing, and every
+        replay pays it."""
+        if getattr(self, '_keys', None) is None:
+            return
+        s, cur = launch_stream(self.device, stream)
+        self._wait_last_ingest(s)
+        with torch.cuda.stream(s):
+            self._keys.zero_()
+        hold(s, cur, self._keys)
+        self._epoch = 0
+
+    def _wait_last_ingest(self, s):
+        ev = getattr(self, '_ingest_ev', None)
+        if ev is not None:
+            s.wait_event(ev)  # the key map may still be in use by a launch on another stream
+
     def launch_ingest(self, prep, stream=None):
         if prep['n'] == 0:
             return
         s, cur = launch_stream(self.device, stream)
-        # the key map's launch epoch (include/simaps.h simaps_ingest): 1..255, then the map is zeroed
-        # (on the launch stream, before the launch) and the count restarts
-        self._epoch = getattr(self, '_epoch', 0) + 1
-        if self._epoch > 255:
-            with torch.cuda.stream(s):
-                self._keys.zero_()
-            self._epoch = 1
+        with torch.cuda.stream(s):
+            capturing = torch.cuda.is_current_stream_capturing()
+        # The key map's launch epoch (include/simaps.h simaps_ingest).  Eager launches count 1..255;
+        # at the wrap the map is zeroed on the launch stream first (after the last launch that used
+        # it) and the count restarts.  A launch captured into a graph replays its epoch, so it takes
+        # the zeroing mode (epoch 0: the map is all zero before and after the launch); once one was
+        # captured, the eager launches take it too, since a replay may follow any of them.
+        if capturing:
+            self._zero_mode = True
+        if getattr(self, '_zero_mode', False):
+            if getattr(self, '_epoch', 0) != 0:  # keys of earlier eager launches (captured: every replay)
+                self._wait_last_ingest(s)
+                with torch.cuda.stream(s):
+                    self._keys.zero_()
+            self._epoch = epoch = 0
+        else:
+            self._epoch = getattr(self, '_epoch', 0) + 1
+            if self._epoch > 255:
+                self._wait_last_ingest(s)
+                with torch.cuda.stream(s):
+                    self._keys.zero_()
+                self._epoch = 1
+            epoch = self._epoch
         _lib.check(_lib.lib.simaps_ingest(
             self.cfg, prep['cam'], prep['n'], _lib.ptr(prep['agents']), _lib.ptr(prep['ids']), _lib.ptr(prep['params']),
             _lib.ptr(prep['depth']), _lib.ptr(prep['seg']), _lib.ptr(self.overhead), _lib.ptr(self.occupancy),
-            _lib.ptr(self._keys), _lib.ptr(self._boxes), self._epoch, _lib.stream_handle(s)))
+            _lib.ptr(self._keys), _lib.ptr(self._boxes), epoch, _lib.stream_handle(s)))
+        if not capturing:
+            self._ingest_ev = torch.cuda.Event()
+            self._ingest_ev.record(s)
         hold(s, cur, prep['ids'], prep['params'], prep['depth'], prep['seg'], prep['agents'], self.overhead,
              self.occupancy, self._keys, self._boxes)
 

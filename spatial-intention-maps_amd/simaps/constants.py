@@ -117,6 +117,21 @@ def room_dims(env_name):
 ROTATE_ROUNDINGS = ('fma', 'plain')
 
 
+_HOST_ROUNDING = []
+
+
+def scene_rotate_rounding(scene):
+    """The rotate rounding a scene renders with: its own 'rotate_rounding' entry (synthetic scenes,
+    the reference adapter and the golden fixtures record it), else this process's numpy rounding --
+    what the reference's scipy.ndimage.rotate would use here (measured once per process)."""
+    r = scene.get('rotate_rounding')
+    if r is not None:
+        return r
+    if not _HOST_ROUNDING:
+        _HOST_ROUNDING.append(host_rotate_rounding())
+    return _HOST_ROUNDING[0]
+
+
 def host_rotate_rounding():
     """'fma' or 'plain': how THIS process's numpy rounds rot_matrix @ v, i.e. what
     scipy.ndimage.rotate does on this host.  Measured on rotation matrices / half-integer

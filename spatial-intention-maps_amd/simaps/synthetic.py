@@ -313,6 +313,7 @@ def make_scene(config_name, env_idx, seed_base=1234, observe_all=False):
         'room_width': room_width, 'flags': flags, 'robot_config': cfg['robot_config'], 'H': H, 'W': W,
         'receptacle_position': receptacle, 'robots': robots,
         'occupancy': occupancy, 'overhead': overhead, 'seg_truth': seg,
+        'rotate_rounding': 'fma',  # the synthetic scenes render with the fused form
     }
 
 

@@ -246,13 +246,13 @@ def gen_rot_scenes(envs):
         write_scene_golden(envs, 'rot-%s_%s' % (host, cfg), scenes, lambda sc: list(range(len(sc['robots']))))
 
 
-def gen_rotate():
+def write_rotate(rs):
     """rotate.npz (FMA host) / rotate_plain.npz (plain host): ndimage.rotate(order=0, reshape=True)
-    index maps of this host, named by the rounding its numpy matmul uses for out_center."""
+    index maps of this host, named by the rounding its numpy matmul uses for out_center (recorded as
+    'rounding' in the file), so a run on either kind of host never overwrites the other's fixture.
+    Draws the heading sample from `rs` (gen_micro's stream, after its trig draws)."""
     from scipy import ndimage
     host = K.host_rotate_rounding()
-    rs = np.random.RandomState(20240601)
-    rs.uniform(-400, 400, 4000)  # (the trig draws of gen_micro: same angle set as rotate.npz)
 
     def idx_map(n, angle):
         ids = np.arange(n * n, dtype=np.float64).reshape(n, n)
@@ -273,9 +273,20 @@ def gen_rotate():
         rot['sha_%d' % n] = np.stack(hashes)
         for q in range(6):
             rot['full_%d_%d' % (n, q)] = idx_map(n, float(angles[q * 97]))
-    name = 'rotate.npz' if host == 'fma' else 'rotate_%s.npz' % host
+    name = rotate_fixture_name(host)
     np.savez_compressed(os.path.join(HERE, name), **rot)
     print('wrote', name)
+
+
+def rotate_fixture_name(rounding):
+    return 'rotate.npz' if rounding == 'fma' else 'rotate_%s.npz' % rounding
+
+
+def gen_rotate():
+    """Only the rotate fixture of this host (same angle set as gen_micro's)."""
+    rs = np.random.RandomState(20240601)
+    rs.uniform(-400, 400, 4000)  # (the trig draws of gen_micro)
+    write_rotate(rs)
 
 
 def gen_micro(envs, sp):
@@ -290,27 +301,9 @@ def gen_micro(envs, sp):
     np.savez_compressed(os.path.join(HERE, 'trig.npz'), angle=ang,
                         cosdg=special.cosdg(ang), sindg=special.sindg(ang))
 
-    # --- ndimage.rotate(order=0, reshape=True) index maps for the two input sizes ---
-    def idx_map(n, angle):
-        ids = np.arange(n * n, dtype=np.float64).reshape(n, n)
-        r = ndimage.rotate(ids, angle, order=0, cval=-1.0)
-        return r.astype(np.int32)
-    heads = rs.uniform(-math.pi, math.pi, 1500)
-    angles = np.concatenate([[90 - math.degrees(h) for h in heads[:750]],
-                             [math.degrees(h) - 90 for h in heads[750:]],
-                             np.arange(-360, 360.5, 0.5), [0.0, 45.0, -45.0, 135.0, 90.0, -90.0, 180.0]])
-    rot = {'angle': angles}
-    for n in (96, 136):
-        shapes, hashes = [], []
-        for t in angles:
-            m = idx_map(n, float(t))
-            shapes.append(m.shape)
-            hashes.append(np.frombuffer(hashlib.sha256(m.tobytes()).digest(), dtype=np.uint8))
-        rot['shape_%d' % n] = np.array(shapes, dtype=np.int32)
-        rot['sha_%d' % n] = np.stack(hashes)
-        for q in range(6):
-            rot['full_%d_%d' % (n, q)] = idx_map(n, float(angles[q * 97]))
-    np.savez_compressed(os.path.join(HERE, 'rotate.npz'), **rot)
+    # --- ndimage.rotate(order=0, reshape=True) index maps for the two input sizes: the file named
+    # by this host's rounding only (write_rotate) ---
+    write_rotate(rs)
 
     # --- distance_transform_edt(return_indices) feature transform, tie-heavy inputs ---
     edt = {}

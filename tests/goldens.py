@@ -23,6 +23,7 @@ def scene_cases():
         e = 0
         while 'e%d_scene' % e in z.files:
             scene = json.loads(str(z['e%d_scene' % e]))
+            scene.setdefault('rotate_rounding', 'fma')  # (the round-1/2 fixtures: made on a fused-dgemv host)
             # (robots that have not acted yet carry None paths / target: the reset goldens)
             scene['robots'] = [dict(r, position=tuple(r['position']),
                                     target_ee=None if r['target_ee'] is None else tuple(r['target_ee']),

@@ -94,7 +94,7 @@ def test_statebatch_refuses_cpu_device():
 
 def test_ingest_chunk_count_and_argument_checks():
     """simaps_ingest_chunks sizes the boxes scratch (one entry per 2048 camera pixels); simaps_ingest
-    refuses bad cameras, NULL buffers, unsupported widths and epochs outside [1, 255] before any launch."""
+    refuses bad cameras, NULL buffers, unsupported widths and epochs outside [0, 255] before any launch."""
     import ctypes
     from simaps import _lib, batch, camera, synthetic
     L = _lib.lib
@@ -111,7 +111,7 @@ def test_ingest_chunk_count_and_argument_checks():
     p = ctypes.c_void_p(8)  # never dereferenced: the width check comes first
     wide = _lib.Camera(8, 2000, spec.near, spec.far, spec.cx2, spec.cy2)
     assert L.simaps_ingest(c, wide, 1, *([p] * 9), 1, None) == _lib.EUNSUPPORTED
-    for epoch in (0, 256):  # the key map's launch epoch (refused before any launch)
+    for epoch in (-1, 256):  # the key map's launch epoch: 0 (zeroing mode) .. 255; refused before any launch
         assert L.simaps_ingest(c, cam, 1, *([p] * 9), epoch, None) == _lib.EINVAL
 
 

@@ -374,6 +374,91 @@ def test_ingest_full_size_two_frames_vs_oracle(V):
         assert _bitwise(ov[n], scenes[e]['overhead'][a]) and np.array_equal(oc[n], scenes[e]['occupancy'][a]), (e, a)
 
 
+def test_ingest_graph_capture_replays(V):
+    """an ingest captured into a graph replays its epoch, so it runs in the zeroing mode
+    (epoch 0).  An eager launch leaves old-epoch keys, the capture then also zeroes the key map,
+    replays with new frames copied into the captured inputs (and an eager launch in between, which
+    now takes the zeroing mode too) all equal the oracle applied in the same order, and the key map
+    is all zero after each launch."""
+    synthetic, vector_env = V
+    from simaps import batch, camera
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 620 + e) for e in range(3)]
+    b = batch.StateBatch(scenes)
+    spec = camera.CAMERAS['forward']
+
+    def frames(seed):
+        f = [synthetic.camera_images(scenes[e], a, 'forward', seed=seed + 5 * e + a) for e, a in b.agents]
+        return np.stack([x[0] for x in f]), np.stack([x[1] for x in f]).astype(np.int32)
+
+    def oracle_apply(dep, seg):
+        for n, (e, a) in enumerate(b.agents):
+            s, r = scenes[e], scenes[e]['robots'][a]
+            O.ingest(s['overhead'][a], s['occupancy'][a], dep[n], seg[n],
+                     spec.params(r['position'][0], r['position'][1], r['heading']), spec, synthetic.SEG_IDS,
+                     s['receptacle_position'] is not None)
+
+    def check():
+        ov, oc = b.overhead.cpu().numpy(), b.occupancy.cpu().numpy()
+        for n, (e, a) in enumerate(b.agents):
+            assert _bitwise(ov[n], scenes[e]['overhead'][a]) and np.array_equal(oc[n], scenes[e]['occupancy'][a]), (e, a)
+
+    d0, s0 = frames(11)
+    b.ingest(d0, s0)                                    # eager, epoch 1: old-epoch keys stay
+    oracle_apply(d0, s0)
+    assert b._epoch == 1 and 1 in _key_epochs(b)
+    d1, s1 = frames(23)
+    prep = b.prepare_ingest(d1, s1)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        b.launch_ingest(prep)                           # captured: key map zeroing + epoch 0 launch
+    assert b._epoch == 0 and b._zero_mode
+    g.replay()
+    torch.cuda.synchronize()
+    oracle_apply(d1, s1)
+    check()
+    assert _key_epochs(b) == {0}
+    d2, s2 = frames(37)
+    b.ingest(d2, s2)                                    # eager after a capture: zeroing mode
+    oracle_apply(d2, s2)
+    assert b._epoch == 0 and _key_epochs(b) == {0}
+    d3, s3 = frames(41)
+    prep['depth'].copy_(torch.from_numpy(d3))
+    prep['seg'].copy_(torch.from_numpy(s3))
+    g.replay()
+    torch.cuda.synchronize()
+    oracle_apply(d3, s3)
+    check()
+    assert _key_epochs(b) == {0}
+
+
+def test_ingest_epoch_under_capture_refused(V):
+    """The C ABI refuses an epoch-tagged (non-zero epoch) ingest on a capturing stream
+    (SIMAPS_EUNSUPPORTED, nothing launched) and accepts epoch 0."""
+    synthetic, vector_env = V
+    from simaps import _lib, batch
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 640)]
+    b = batch.StateBatch(scenes)
+    f = [synthetic.camera_images(scenes[0], a, 'forward', seed=a) for e, a in b.agents]
+    prep = b.prepare_ingest(np.stack([x[0] for x in f]), np.stack([x[1] for x in f]).astype(np.int32))
+    torch.cuda.synchronize()
+
+    def call(epoch):
+        return _lib.lib.simaps_ingest(
+            b.cfg, prep['cam'], prep['n'], _lib.ptr(prep['agents']), _lib.ptr(prep['ids']), _lib.ptr(prep['params']),
+            _lib.ptr(prep['depth']), _lib.ptr(prep['seg']), _lib.ptr(b.overhead), _lib.ptr(b.occupancy),
+            _lib.ptr(b._keys), _lib.ptr(b._boxes), epoch, _lib.stream_handle(torch.cuda.current_stream()))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        rc_tagged = call(7)
+        rc_zero = call(0)
+    assert rc_tagged == _lib.EUNSUPPORTED and b'epoch' in _lib.lib.simaps_last_error()
+    assert rc_zero == 0
+    g.replay()
+    torch.cuda.synchronize()
+    assert _key_epochs(b) == {0}
+
+
 def test_gridgraph_shortest_path_reference_goldens(V, path_mode):
     """GridGraph.shortest_path (pyx:121-154) on raw cells against the reference itself: the demo
     sample (free / blocked / equal ends) and random grids with free values 1, 2, 255 (line of sight
@@ -668,9 +753,9 @@ def test_periodic_remap_successive_frames(V):
 
 
 def test_path_launch_in_graph_capture(V):
-    """A path launch captured into a graph gets no early-exit scratch (the graph would keep its pointer
-    past a later growth) and runs the compact kernel: the replay equals the eager launches of both
-    kernels, for targets across the divider (detours: the SPFA runs)."""
+    """A path launch captured into a graph gets no early-exit scratch (it is taken from the memory
+    pool in stream order per eager launch) and runs the compact kernel: the replay equals the eager
+    launches of both kernels, for targets across the divider (detours: the SPFA runs)."""
     synthetic, _ = V
     from simaps import _lib, batch
     scenes = [synthetic.make_scene('lifting_4-small_divider', 70 + e) for e in range(8)]
@@ -706,9 +791,9 @@ def test_path_launch_in_graph_capture(V):
 
 
 def test_path_scratch_growth(V):
-    """The early-exit kernels' per-stream fixpoint scratch grows with the launch (a small launch
-    first, then one ~30x larger on the same stream, then the small one again): every launch equals
-    the compact kernel's paths."""
+    """The early-exit kernels' fixpoint scratch (stream-ordered pool memory per launch) follows the
+    launch size (a small launch first, then one ~30x larger on the same stream, then the small one
+    again): every launch equals the compact kernel's paths."""
     synthetic, _ = V
     from simaps import _lib, batch
     scenes = [synthetic.make_scene('lifting_4-small_divider', 300 + e) for e in range(80)]

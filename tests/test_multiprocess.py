@@ -49,11 +49,19 @@ def _worker(rank, world, port, envs_per_rank, out_dir):
             calls.append(k)
             time.sleep(delay)
 
-        el = bench.timed_steps(step, steps=5, warmup=2, sync=lambda: None, world=world)
+        own = []
+        el = bench.timed_steps(step, steps=5, warmup=2, sync=lambda: None, world=world, own=own)
         mx = bench.max_over_ranks([float(rank), -float(rank)], world)
+        # the bench line's per-rank report: all-gathered rows + the group's view
+        row = dict(bench.device_identity('cpu'), rank=rank, local_rank=rank, host='h', env_range=[ids[0], ids[-1]],
+                   stacks_per_step=4 * len(ids), steps=5, seconds=own[0], kernel_ms=0.0, pci='cpu-rank%d' % rank)
+        rep = bench.rank_report(row, world)
+        import json
+        with open(os.path.join(out_dir, 'rep%d.json' % rank), 'w') as f:
+            json.dump(rep, f)
         np.save(os.path.join(out_dir, 'r%d.npy' % rank),
                 np.array([el, mx[0], mx[1], len(calls), sum(k >= 0 for k in calls), ids[0], ids[-1],
-                          float(robots['x'].sum())]))
+                          float(robots['x'].sum()), own[0]]))
     finally:
         dist.destroy_process_group()
 
@@ -64,13 +72,30 @@ def test_gloo_world2_sharding_and_timing(tmp_path):
     mp.spawn(_worker, args=(world, _free_port(), E, str(tmp_path)), nprocs=world, join=True)
     r = [np.load(os.path.join(tmp_path, 'r%d.npy' % k)) for k in range(world)]
     for k in range(world):
-        el, mx0, mx1, ncalls, ntimed, first, last, _ = r[k]
+        el, mx0, mx1, ncalls, ntimed, first, last, _, _ = r[k]
         assert el >= 5 * 0.02 * 0.9          # the slow rank's 5 timed steps dominate on both ranks
         assert mx0 == world - 1 and mx1 == 0  # element-wise max over ranks
         assert ncalls == 7 and ntimed == 5    # exactly K timed steps after W warmup steps
         assert (first, last) == (k * E, k * E + E - 1)
     assert abs(r[0][0] - r[1][0]) < 1e-12    # one job time, identical on every rank
     assert r[0][7] != r[1][7]                # different envs (seeds) on different ranks
+    assert r[0][0] == max(r[0][8], r[1][8])  # the job time is the max of the ranks' own times
+    import json
+    reps = [json.load(open(os.path.join(tmp_path, 'rep%d.json' % k))) for k in range(world)]
+    assert reps[0] == reps[1]                # every rank holds the same gathered report
+    rep = reps[0]
+    assert rep['world_size'] == world and rep['backend'] == 'gloo' and rep['distinct_devices'] == world
+    assert [row['rank'] for row in rep['ranks']] == list(range(world))
+    for k, row in enumerate(rep['ranks']):
+        assert row['env_range'] == [k * E, k * E + E - 1] and row['stacks_per_step'] == 4 * E
+        assert abs(row['seconds'] - r[k][8]) < 1e-12 and row['device'] == 'cpu'
+
+
+def test_rank_report_without_process_group():
+    sys.path.insert(0, ROOT)
+    import bench
+    rep = bench.rank_report({'rank': 0, 'device': 'cpu'}, 1)
+    assert rep == {'world_size': 1, 'backend': None, 'ranks': [{'rank': 0, 'device': 'cpu'}], 'distinct_devices': 1}
 
 
 def test_rank_envs_partition():

@@ -4,6 +4,7 @@ The goldens were produced by running the reference's own code (tests/golden/make
 These tests pin the oracle; the GPU tests then check the HIP path against the oracle.
 """
 import hashlib
+import os
 import math
 
 import numpy as np
@@ -31,8 +32,7 @@ ROTATE_GOLDENS = [('rotate.npz', 'fma'), ('rotate_plain.npz', 'plain')]
 @pytest.mark.parametrize('name,rounding', ROTATE_GOLDENS)
 def test_rotate_index_maps(n, name, rounding):
     g = G.load(name)
-    if 'rounding' in g.files:
-        assert str(g['rounding']) == rounding
+    assert str(g['rounding']) == rounding
     for k, a in enumerate(g['angle']):
         i0, i1, v = O.rotate_index_map(n, float(a), rounding)
         m = np.where(v, i0 * n + i1, -1).astype(np.int32)
@@ -41,6 +41,21 @@ def test_rotate_index_maps(n, name, rounding):
     for q in range(6):
         i0, i1, v = O.rotate_index_map(n, float(g['angle'][q * 97]), rounding)
         assert np.array_equal(np.where(v, i0 * n + i1, -1), g['full_%d_%d' % (n, q)])
+
+
+def test_rotate_fixtures_named_by_their_rounding():
+    """Every rotate fixture records the host rounding that produced it, and its file name is the one
+    make_goldens.write_rotate gives that rounding, so regenerating the goldens on either kind of host
+    writes only its own file (the no-argument run on a plain host overwrote rotate.npz)."""
+    import glob
+    src = open(os.path.join(G.GOLDEN, 'make_goldens.py')).read()
+    assert "np.savez_compressed(os.path.join(HERE, 'rotate.npz')" not in src  # only write_rotate writes it
+    files = sorted(glob.glob(os.path.join(G.GOLDEN, 'rotate*.npz')))
+    assert {os.path.basename(f) for f in files} == {n for n, _ in ROTATE_GOLDENS}
+    for f in files:
+        r = str(np.load(f)['rounding'])
+        assert r in K.ROTATE_ROUNDINGS
+        assert os.path.basename(f) == ('rotate.npz' if r == 'fma' else 'rotate_%s.npz' % r)
 
 
 def test_rotate_roundings_differ_on_the_goldens():
