@@ -1102,12 +1102,20 @@ __device__ __forceinline__ void mark_range(uint64_t *m, int a, int b)  // bits a
     mark_lines(m, a <= 63 ? bits64(a, min(b, 63)) : 0ull, b >= 64 ? bits64(max(a, 64) - 64, b - 64) : 0ull);
 }
 
+// SSSP_CHECK: the rounds end with the fixpoint check below (sssp_check) instead of inline marks.
+#ifdef SIMAPS_SSSP_CHECK
+constexpr bool SSSP_CHECK = true;   // (A/B build: measured slower)
+#else
+constexpr bool SSSP_CHECK = false;  // the product: inline marks + a confirming round
+#endif
+
 // One sweep of direction dir_in over source dm's array; true if it improved a cell.  With nparts > 1
 // (compile-time pitch only) the sweep covers part `part` of the direction's steps: it relaxes out of
 // the lines of steps [s0, s1) (their dirty bits are its own) and into the line of step s1, which the
 // next part relaxes out of -- marked dirty for it when this part improved that line.
+constexpr bool SSSP_INLINE_MARKS = !SSSP_CHECK;
 __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_in, uint64_t (*dm)[2], int &steps,
-                                      int part = 0, int nparts = 1)
+                                      int part = 0, int nparts = 1, bool marks = SSSP_INLINE_MARKS)
 {
     lds_float *D = (lds_float *)Dg;  // the distance arrays live in LDS: keep ds_* addressing
     // wave-uniform loop bounds: scalar loop control, no exec-mask merges at the back edge
@@ -1155,7 +1163,7 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
         }
         steps += o.steps;
         if (!o.lanes) return false;
-        if (lane == 0) {
+        if (marks && lane == 0) {
             const int a = fwd ? o.imin : len - 1 - o.imax, b = fwd ? o.imax : len - 1 - o.imin;
             mark_range(dm[dir ^ 1], max(a, 0), min(b, 127));
             if (s1 < len && o.imax >= s1) {  // improved the next part's first line: its to relax out of
@@ -1179,10 +1187,122 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
     case 2: chg = h <= 63 ? sweep_t<2, 1, 0>(D, w, h, pw) : sweep_t<2, 2, 0>(D, w, h, pw); break;
     default: chg = h <= 63 ? sweep_t<3, 1, 0>(D, w, h, pw) : sweep_t<3, 2, 0>(D, w, h, pw); break;
     }
-    if (chg && lane == 0)
+    if (marks && chg && lane == 0)
         for (int d2 = 0; d2 < 4; d2++)
             if (d2 != dir) mark_range(dm[d2], 0, (d2 < 2 ? h : w) - 1);
     return chg;
+}
+
+// ---- the fixpoint check (round 4) -----------------------------------------------------------------
+// After a round's sweeps (behind their barrier), one lane-parallel pass tests EVERY edge into every
+// cell, fl(|d_u| + w) < d_v -- the relaxation a sweep step performs -- which is the fixpoint
+// condition itself.  A cell with a violated edge marks every line such an edge can come out of
+// (the rows above / below for the down / up sweeps, which relax the straight and both diagonal
+// edges out of a row; the columns left / right for the right / left sweeps).  The next round
+// sweeps only from those lines, and a round whose check finds no violated edge has reached the unique f32 fixpoint, so
+// no confirmation round runs and a sweep leaves no marks behind (SSSP_CHECK; the inline marks
+// are supersets: a lowered line is re-swept in the opposite direction whether or not anything
+// there can improve).  Modelled first (tools/sssp_sched_sim.py: -29 % of the slowest sweep chain
+// at an assumed ~1,500-cycle check) and built: bitwise, 3 rounds instead of 4 and -35 % line steps
+// on the BASELINE config, but the check itself costs ~2.2 us per round in the kernel (~25 VALU
+// per row on SIMDs shared with the render waves) plus a second barrier, so every config measured
+// slower.  Kept as the SIMAPS_SSSP_CHECK A/B build, not the product.
+// Threads t of n (n = 64 * waves, this source's group): lane l owns columns 2l + 1, 2l + 2
+// (w <= 126), wave q a block of rows; returns true (uniform per wave) if this wave found a violation.
+__device__ __forceinline__ uint64_t spread_even(uint32_t x)  // bit i -> bit 2i
+{
+    uint64_t v = x;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    v = (v | (v << 1)) & 0x5555555555555555ull;
+    return v;
+}
+__device__ __forceinline__ bool sssp_check(const float *Dg, int h, int w, int pw, uint64_t (*dm)[2], int t, int n)
+{
+    const lds_float *D = (const lds_float *)Dg;
+    const int lane = t & 63, q = t >> 6, nw = n >> 6;
+    h = __builtin_amdgcn_readfirstlane(h);
+    w = __builtin_amdgcn_readfirstlane(w);
+    pw = __builtin_amdgcn_readfirstlane(pw);
+    // array rows [r0, r1), <= 32 of them (wave-uniform: scalar loop control)
+    const int r0 = __builtin_amdgcn_readfirstlane(1 + q * h / nw), r1 = __builtin_amdgcn_readfirstlane(1 + (q + 1) * h / nw);
+    const bool on0 = 2 * lane + 1 <= w, on1 = 2 * lane + 2 <= w;
+    const int c0 = on0 ? 2 * lane + 1 : 1;  // (idle lanes alias lane 0's cells, masked below)
+    const float s2 = SQRT2F, NI = -INFINITY;
+    // A cell's best candidate over its 8 edges, min(|d_u| + w_uv), against its own value; a violated
+    // cell (r, c) marks the down sweep at row r - 1, the up sweep at row r + 1, the right sweep at
+    // column c - 1 and the left sweep at column c + 1 -- every line a violated edge into it can come
+    // out of (a superset: a sweep that finds nothing there stops after one quiet group).  Per row, the
+    // eight |x| + w of its four cells serve both as its vertical candidates for the rows above and
+    // below and as its horizontal ones.
+    struct RowC {
+        float x0, x1;      // the row's two cells
+        float v0, v1;      // what the row offers the cells (same columns) of the rows above / below
+        float h0, h1;      // the best horizontal candidate of each of its two cells
+    };
+    auto row = [&](int rr) {
+        const lds_float *p = D + rr * pw + c0 - 1;  // columns c0 - 1 .. c0 + 2
+        const float a = p[0], b = p[1], c = p[2], d = p[3];
+        const float a1 = fabsf(a) + 1.0f, b1 = fabsf(b) + 1.0f, c1 = fabsf(c) + 1.0f, d1 = fabsf(d) + 1.0f;
+        const float as = fabsf(a) + s2, bs = fabsf(b) + s2, cs = fabsf(c) + s2, ds = fabsf(d) + s2;
+        RowC o;
+        o.x0 = on0 ? b : NI;  // -inf: never improvable
+        o.x1 = on1 ? c : NI;
+        o.v0 = __builtin_fminf(__builtin_fminf(as, b1), cs);
+        o.v1 = __builtin_fminf(__builtin_fminf(bs, c1), ds);
+        o.h0 = __builtin_fminf(a1, c1);
+        o.h1 = __builtin_fminf(b1, d1);
+        return o;
+    };
+    // rows of this wave in chunks of CK: the CK + 2 rows' loads are issued together (row indices
+    // clamped into the array: a chunk past the wave's last row re-reads row r1, unused), then the
+    // rows' candidates, then the CK checks -- one LDS round trip per chunk instead of one per row
+    constexpr int CK = 8;
+    uint32_t rbits = 0;      // bit (r - r0): row r holds a violated cell
+    uint32_t cvb = 0;        // bit 0 / 1: this lane's column c0 / c0 + 1 holds a violated cell
+    for (int rb = r0; rb < r1; rb += CK) {
+        RowC R[CK + 2];
+#pragma unroll
+        for (int k = 0; k < CK + 2; k++) R[k] = row(min(rb - 1 + k, r1));
+#pragma unroll
+        for (int k = 1; k <= CK; k++) {
+            const int r = rb - 1 + k;
+            const bool e0 = __builtin_fminf(__builtin_fminf(R[k - 1].v0, R[k + 1].v0), R[k].h0) < R[k].x0;
+            const bool e1 = __builtin_fminf(__builtin_fminf(R[k - 1].v1, R[k + 1].v1), R[k].h1) < R[k].x1;
+            const uint32_t e = r < r1 ? (uint32_t)e0 | ((uint32_t)e1 << 1) : 0u;
+            cvb |= e;
+            rbits |= (e != 0u ? 1u : 0u) << (r - r0);
+        }
+    }
+    const bool cv0 = cvb & 1u, cv1 = (cvb >> 1) & 1u;
+    // rows: OR over the wave (DPP reductions), then the marks; columns: ballots
+    uint32_t rb = rbits;
+    rb |= __builtin_amdgcn_update_dpp(0, rb, 0x111, 0xf, 0xf, false);  // row_shr:1
+    rb |= __builtin_amdgcn_update_dpp(0, rb, 0x112, 0xf, 0xf, false);  // row_shr:2
+    rb |= __builtin_amdgcn_update_dpp(0, rb, 0x114, 0xf, 0xf, false);  // row_shr:4
+    rb |= __builtin_amdgcn_update_dpp(0, rb, 0x118, 0xf, 0xf, false);  // row_shr:8
+    rb |= __builtin_amdgcn_update_dpp(0, rb, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    rb |= __builtin_amdgcn_update_dpp(0, rb, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    const uint32_t rows = (uint32_t)__builtin_amdgcn_readlane((int)rb, 63);
+    const uint64_t b0 = __ballot(cv0), b1 = __ballot(cv1);
+    const bool any = (rows | b0 | b1) != 0;
+    if (lane == 0 && any) {
+        // violated row r (bit r - r0) -> down bit (r - 1) - 1 = r - 2, up bit (r + 1) - 1 = r
+        const unsigned __int128 R = (unsigned __int128)rows << (r0 - 1);  // bit r - 1 (r >= 1)
+        const unsigned __int128 Dn = R >> 1, Up = R << 1;
+        // violated column c (lane l: 2l + 1 from b0, 2l + 2 from b1), bit c - 1 = 2l / 2l + 1 -> the
+        // right sweep at column c - 1 (bit c - 2), the left sweep at column c + 1 (bit c)
+        const unsigned __int128 Cc = ((unsigned __int128)spread_even((uint32_t)(b0 >> 32)) << 64 | spread_even((uint32_t)b0)) |
+                                     (((unsigned __int128)spread_even((uint32_t)(b1 >> 32)) << 64 | spread_even((uint32_t)b1)) << 1);
+        const unsigned __int128 Rt = Cc >> 1, Lt = Cc << 1;
+        mark_lines(dm[0], (uint64_t)Dn, (uint64_t)(Dn >> 64));
+        mark_lines(dm[1], (uint64_t)Up, (uint64_t)(Up >> 64));
+        mark_lines(dm[2], (uint64_t)Rt, (uint64_t)(Rt >> 64));
+        mark_lines(dm[3], (uint64_t)Lt, (uint64_t)(Lt >> 64));
+    }
+    return any;
 }
 
 // group g: free cells +inf, blocked / border -inf, sources 0 (one pass over the rect rows)
@@ -1257,7 +1377,8 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
 #endif
         // waves go to SIMD (wave % 4): source 1's directions are rotated by 2 so that every SIMD
         // hosts one row sweep and one column sweep (the long ones would otherwise share two SIMDs)
-        if (sh.src_ok[s] && sweep(dist + s * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3, sh.dirty[s], steps) && (tid & 63) == 0)
+        if (sh.src_ok[s] && sweep(dist + s * DIST_FLOATS, h, w, pw, (wave + 2 * s) & 3, sh.dirty[s], steps) && (tid & 63) == 0 &&
+            !SSSP_CHECK)
             changed[round % 3] = 1;
 #ifdef SIMAPS_PHASE_STAMPS
         if (round == 0 && wave == 0) STAMP_NB(22);
@@ -1266,6 +1387,21 @@ __device__ __forceinline__ void sssp_rounds(Shared &sh, float *dist, int nsrc, c
         if (round == 0 && wave == 0) STAMP_CLK(45);
 #endif
         gs.sync();
+        if (SSSP_CHECK) {  // every edge; the violated ones mark the next round's lines
+#ifdef SIMAPS_PHASE_STAMPS
+            if (tid == 0 && round == 0) STAMP_NB(56);
+#endif
+            if (sh.src_ok[s] && sssp_check(dist + s * DIST_FLOATS, h, w, pw, sh.dirty[s], tid & 255, 256) && (tid & 63) == 0)
+                changed[round % 3] = 1;
+#ifdef SIMAPS_PHASE_STAMPS
+            if (tid == 0 && round == 0) STAMP_NB(57);
+            if (tid == 192 && round == 0) STAMP_NB(63);
+#endif
+            gs.sync();
+#ifdef SIMAPS_PHASE_STAMPS
+            if (tid == 0 && round == 0) STAMP_NB(78);
+#endif
+        }
         if (!changed[round % 3] || round >= max_rounds) {
             if ((tid & 255) == 0)  // cap hit: 1 << 20 (status bit 1)
                 __hip_atomic_fetch_max(&sh.rounds, round >= max_rounds ? 1 << 20 : round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1375,9 +1511,14 @@ __device__ __forceinline__ void sssp_rounds_split(Shared &sh, float *dist)
     int steps = 0;
     for (int round = 0;; round++) {
         if (tid == 0) changed[(round + 1) % 3] = 0;
-        if (sh.src_ok[0] && sweep(dist, h, w, pw, dir, sh.dirty[0], steps, part, nparts) && (tid & 63) == 0)
+        if (sh.src_ok[0] && sweep(dist, h, w, pw, dir, sh.dirty[0], steps, part, nparts) && (tid & 63) == 0 && !SSSP_CHECK)
             changed[round % 3] = 1;
         gs.sync();
+        if (SSSP_CHECK) {
+            if (sh.src_ok[0] && sssp_check(dist, h, w, pw, sh.dirty[0], tid, 64 * SPLIT_WAVES) && (tid & 63) == 0)
+                changed[round % 3] = 1;
+            gs.sync();
+        }
         if (!changed[round % 3] || round >= max_rounds) {
             if (tid == 0)
                 __hip_atomic_fetch_max(&sh.rounds, round >= max_rounds ? 1 << 20 : round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2683,8 +2824,12 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         int steps = 0, round = 0;
         for (;; round++) {
             if (tid == 0) sh.changed[(round + 1) % 3] = 0;
-            if (sweep(dist, h, w, pw, wave, sh.dirty, steps) && lane == 0) sh.changed[round % 3] = 1;
+            if (sweep(dist, h, w, pw, wave, sh.dirty, steps) && lane == 0 && !SSSP_CHECK) sh.changed[round % 3] = 1;
             lds_barrier();
+            if (SSSP_CHECK) {
+                if (sssp_check(dist, h, w, pw, sh.dirty, tid, PNT) && lane == 0) sh.changed[round % 3] = 1;
+                lds_barrier();
+            }
             if (!sh.changed[round % 3] || round >= h * w + 16) break;
         }
         if (tid == 0 && round >= h * w + 16) sh.fault |= SIMAPS_FAULT_ROUNDS;

@@ -57,6 +57,8 @@ def main():
            'join_us': us(4, 0),
            'distance_us': {'values': us(16, 5), 'block_min': us(17, 16), 'stores': us(6, 17), 'all': us(6, 5)},
            'sweep_rounds_us': {'round_%d' % r: us(19 + r, 18 + r) for r in range(3)},
+           'check_r0_us': {'w0_sweep_end': us(24, 18), 'w3_sweep_end': us(27, 18), 'check_start': us(56, 18),
+                           'w0_check_end': us(57, 18), 'w3_check_end': us(63, 18), 'after_barrier': us(78, 18)},
            'wave_sweep_r0_us': {'start': [us(32 + w, 18) for w in range(8)], 'end': [us(24 + w, 18) for w in range(8)]},
            'clock_mhz_sweep_w0': float(np.median((st[:, 45] - st[:, 44]) / ((st[:, 24] - st[:, 18]) / 100.0)))
            if (st[:, 45] > 0).any() else None,

@@ -180,7 +180,7 @@ def simulate(free, src, rule, cost, c_barrier, c_check):
         per_round.append({nm: s.steps for nm, s in sweeps.items()})
         for nm, s in sweeps.items():
             steps[nm] += s.steps
-        if rule == 'marks':
+        if rule in ('marks', 'perp_final'):
             nxt = {k: set() for k in DIRS}
             any_imp = False
             for nm, s in sweeps.items():
@@ -188,10 +188,18 @@ def simulate(free, src, rule, cost, c_barrier, c_check):
                 pa, pb = ('right', 'left') if vert else ('down', 'up')
                 for line, cells in s.improved_lines:
                     any_imp = True
-                    nxt[OPP[nm]].add(line)
+                    if rule == 'marks':
+                        nxt[OPP[nm]].add(line)
                     nxt[pa].update(cells.tolist())
                     nxt[pb].update(cells.tolist())
-            if not any_imp:
+            if rule == 'perp_final' and not any(nxt.values()):
+                # no marks left: the exact check decides (perpendicular marks only miss edges back
+                # into the line a sweep came from)
+                total += c_check
+                nxt = violations(dist, free, 'vert')
+                if not any(nxt.values()):
+                    break
+            elif not any_imp:
                 break
             masks = nxt
         else:
@@ -215,7 +223,7 @@ def main():
     args = ap.parse_args()
     import oracle
     from simaps import synthetic
-    res = {r: [] for r in ('marks', 'check', 'check_both', 'check_spec')}
+    res = {r: [] for r in ('marks', 'check', 'check_both', 'check_spec', 'perp_final')}
     detail = {r: [] for r in res}
     for e in range(args.envs):
         sc = synthetic.make_scene(args.config, e)
@@ -251,7 +259,7 @@ def main():
                      'cycles_p90': float(np.percentile(v, 90)),
                      'rounds_median': float(np.median([d['rounds'] for d in detail[rule]])),
                      'steps_median': {k: float(np.median([d['steps'][k] for d in detail[rule]])) for k in DIRS}}
-    for rule in ('check', 'check_both', 'check_spec'):
+    for rule in ('check', 'check_both', 'check_spec', 'perp_final'):
         out[rule + '_vs_marks_median'] = out[rule]['cycles_median'] / out['marks']['cycles_median']
         out[rule + '_vs_marks_max'] = out[rule]['cycles_max'] / out['marks']['cycles_max']
     print(json.dumps(out))
