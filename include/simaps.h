@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SIMAPS_ABI_VERSION 6
+#define SIMAPS_ABI_VERSION 7
 
 /* error codes */
 #define SIMAPS_OK 0
@@ -164,6 +164,12 @@ typedef struct simaps_debug {
     int32_t *status;   /* [N] bit0: no free cell (sp channels undefined in the reference); bit1: SSSP
                         round cap hit (bug guard); bit2: barrier timeout; bit3: descriptor clamped;
                         bits 8+: SSSP rounds to convergence */
+    void *rec_cache;   /* NOT a debug output: with use_shortest_path_to_receptacle_map, each rendered
+                        agent's converged receptacle distance array is kept in its map slot's record
+                        (simaps_rec_cache_bytes(cfg) bytes per slot, slot agents[n].map_slot) for
+                        simaps_sp_lookup -- the reference's GridGraph cache that get_state fills for
+                        Mapper.distance_to_receptacle (envs.py:2189-2194, shortest_paths.pyx:116-119,
+                        156-163).  Valid until the slot's occupancy map changes; the caller tracks that. */
 } simaps_debug;
 
 int simaps_abi_version(void);
@@ -214,7 +220,26 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
  *   Both ends are snapped to the nearest free cspace cell exactly like the reference (scipy EDT). */
 int simaps_sp_distance(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
                        const simaps_robot *robots, const uint8_t *occupancy, const double *sources,
-                       const double *targets, int Q, double *out, void *stream);
+                       const double *targets, int Q, double *out, void *rec_cache, void *stream);
+/*   rec_cache (may be NULL): as simaps_debug.rec_cache -- when every source is its env's receptacle
+ *   position, each agent's distance array from it is also kept in its map slot's record, so later
+ *   lookups from the receptacle can use simaps_sp_lookup (the cache of the reference's
+ *   GridGraph._spfa_with_cache, shortest_paths.pyx:116-119). */
+
+/* Bytes of one map slot's record in a receptacle distance cache (simaps_debug.rec_cache): a 16-byte
+ * header and the room rect's (room_h + 2) x ((room_w + 2) | 1) float32 distance array. */
+int simaps_rec_cache_bytes(const simaps_config *cfg);
+
+/* Mapper.distance_to_receptacle (envs.py:2190-2194, shortest-path partial rewards) answered from the
+ * cache, as the reference answers it from the GridGraph that get_state filled: per agent n, the
+ *   record of slot agents[n].map_slot (written by simaps_get_state / simaps_sp_distance for the
+ *   slot's current map), targets [N][Q][2] fp64 (x, y), out [N][Q] fp64 -- the same values as
+ *   simaps_sp_distance with the receptacle as the source: each target snapped to its nearest free
+ *   cspace cell (scipy EDT, rebuilt from the cached array only for targets on blocked pixels), the
+ *   float32 distance / 96, unreachable -> -1 / 96.  All DEVICE.  A record of another map is not
+ *   detected: the caller keeps the cache in step with the maps. */
+int simaps_sp_lookup(const simaps_config *cfg, int N, const simaps_agent *agents, const void *rec_cache,
+                     const double *targets, int Q, double *out, void *stream);
 
 /* Batched OccupancyMap.shortest_path(source_position, target_position) on agent n's own map:
  *   sources [N][2], targets [N][2] fp64 (x, y); out_xy [N][max_points][2] fp64 waypoints (first =

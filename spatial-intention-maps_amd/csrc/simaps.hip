@@ -364,6 +364,40 @@ __device__ __forceinline__ float div96(float v)
 
 // distance-array pitch: (w + 2) | 1 floats (odd: column-wise sweeps hit at most 2-way bank conflicts)
 __device__ __forceinline__ int sssp_pitch(int w) { return (w + 2) | 1; }
+
+// ---- receptacle distance cache (simaps_debug.rec_cache, simaps_sp_lookup) -------------------------
+// One record per map slot: int4 header {1, receptacle snapped to a free cell, h, w}, then the room
+// rect's distance array as the sweeps leave it: (h + 2) x pitch float32, border and blocked cells
+// -inf, free unreachable cells +inf (so a cell is free iff its value is above -inf).
+constexpr int REC_HDR = 16;
+__host__ __device__ __forceinline__ int rec_cache_bytes(int h, int w)
+{
+    return (REC_HDR + (h + 2) * ((w + 2) | 1) * 4 + 255) & ~255;
+}
+// Threads t of n write slot record `rec` from the LDS array `dist`.  freeb == nullptr: the array is
+// in the record's format (get_state, before any finish pass); else its blocked cells hold +inf
+// (after sssp_finish) and the rect's free bits decide.
+__device__ __forceinline__ void rec_export(char *rec, const float *dist, int h, int w, int src_ok, const B128 *freeb, int t,
+                                           int n)
+{
+    const int pw = (w + 2) | 1, cells = (h + 2) * pw;
+    float *d = reinterpret_cast<float *>(rec + REC_HDR);
+    if (!freeb) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(dist);  // (LDS array and record: 16-aligned)
+        float4 *d4 = reinterpret_cast<float4 *>(d);
+        for (int k = t; k < cells / 4; k += n) d4[k] = s4[k];
+        for (int k = (cells & ~3) + t; k < cells; k += n) d[k] = dist[k];
+    } else {
+        for (int r = t / 128; r < h + 2; r += n / 128) {  // (row, column) walk: no division per cell
+            const bool row_in = r >= 1 && r <= h;
+            for (int c = t % 128; c < pw; c += 128) {
+                const bool fr = row_in && c >= 1 && c <= w && b_test(freeb[r - 1], c - 1);
+                d[r * pw + c] = fr ? dist[r * pw + c] : -INFINITY;
+            }
+        }
+    }
+    if (t == 0) *reinterpret_cast<int4 *>(rec) = make_int4(1, src_ok, h, w);
+}
 // byte offset (from distance array 0) of the distance phase's cell table when it lives in that
 // array's unused tail (tail_cells: the table, 96 * 96 u16, fits after the room's cells)
 __device__ __forceinline__ int tail_cells_off(int h, int w) { return ((h + 2) * sssp_pitch(w) * 4 + 15) & ~15; }
@@ -679,8 +713,9 @@ __device__ __forceinline__ void build_cspace(SsspScratch &S, const OccLoad<G> *L
 // ------------------------------------------------------------------------------------------------
 // Phase: snap the query pixels to the closest free cell (scipy EDT feature transform at q)
 // ------------------------------------------------------------------------------------------------
-template <class SH>  // Shared (get_state / sp_distance) or PathHdr (path kernels)
-__device__ __forceinline__ void snap_sources(SH &sh, SsspScratch &S, int nsrc, const Group &g)
+template <class SH, class SC>  // Shared (get_state / sp_distance) or PathHdr (path kernels) / LookupHdr;
+                               // SsspScratch or any struct with the rect's freeb rows
+__device__ __forceinline__ void snap_sources(SH &sh, SC &S, int nsrc, const Group &g)
 {
     const int tid = g.t;
     const int h = sh.h, w = sh.w, i0 = sh.i0, j0 = sh.j0;
@@ -2228,10 +2263,16 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
     }
     if (nsrc == 0) return;
     sssp_rounds(sh, dist, nsrc, g);
+    // the receptacle source's converged array -> its map slot's cache record (source 0 = the
+    // receptacle when use_shortest_path_to_receptacle_map; envs.py:2071-2113 order)
+    char *rec = dbg.rec_cache && cfg.use_shortest_path_to_receptacle_map
+                    ? reinterpret_cast<char *>(dbg.rec_cache) + (size_t)ag.map_slot * rec_cache_bytes(h, w)
+                    : nullptr;
     if (nsrc == 2 && G == 512 && !dbg.dist) {
         // each source's four waves take its maximum as soon as its own rounds end (the arrays are
         // independent), overlapping the other source's remaining rounds
         const int s = t >> 8;
+        if (rec && s == 0) rec_export(rec, dist, h, w, sh.src_ok[0], nullptr, t & 255, 256);
         const float m = max_finite_part(dist + s * DIST_FLOATS, (h + 2) * sssp_pitch(w), t & 255, 256);
         if ((t & 63) == 0) sh.red[s][(t >> 6) & 3] = m;
         g.sync();
@@ -2241,6 +2282,7 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
         return;
     }
     g.sync();  // each source ran its own rounds: both arrays are final only now
+    if (rec) rec_export(rec, dist, h, w, sh.src_ok[0], nullptr, t, g.n);
     if (t == 0) STAMP_NB(49);
     if (dbg.dist) {  // debug: the raw distances (unreachable -> +inf, read as sh.unreach like -inf)
         sssp_finish(sh, dist, nsrc, g);
@@ -2418,26 +2460,32 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             const int *mc = reinterpret_cast<const int *>(sh.mwin + 120 + 4 * 4);
             const int mt0 = mt[0], mt1 = mt[1], mt2 = mt[2], mt3 = mt[3];
             const int mc0 = mc[0], mc1 = mc[1], mc2 = mc[2], mc3 = mc[3];
-            for (int rp = sub; 2 * rp <= bi1 - bi0; rp += wpr) {
+            // one box pixel: its stamp code (0: none) -- the fp64 source index (rot_src), the mask
+            // window bits; pos = crop-relative pixel or -1 outside the crop
+            auto stamp = [&](int rp, int &pos) -> unsigned {
                 const int gi = bi0 + 2 * rp + (ln >> 5), gj = bj0 + (ln & 31);
                 unsigned code = 0;
-                if (gi <= bi1 && gj <= bj1) {
-                    int m0, m1;
-                    const bool in = rot_src(R, LW, gi - st_i, gj - st_j, m0, m1);
-                    if (in) {
-                        const int r = m0 - mt0, cc = m1 - mt1;
-                        if ((unsigned)r < (unsigned)mt2 && (unsigned)cc < (unsigned)mt3 && ((sh.mwin[type * 24 + r] >> cc) & 1u))
-                            code = code0;
-                        const int r2 = m0 - mc0, c2 = m1 - mc1;
-                        if (cube && (unsigned)r2 < (unsigned)mc2 && (unsigned)c2 < (unsigned)mc3 && ((sh.mwin[4 * 24 + r2] >> c2) & 1u))
-                            code |= 1u << 5;
-                    }
-                }
+                int m0 = 0, m1 = 0;
+                const bool in = gi <= bi1 && gj <= bj1 && rot_src(R, LW, gi - st_i, gj - st_j, m0, m1);
+                const int r = m0 - mt0, cc = m1 - mt1, r2 = m0 - mc0, c2 = m1 - mc1;
+                const bool okm = in && (unsigned)r < (unsigned)mt2 && (unsigned)cc < (unsigned)mt3;
+                const bool okc = in && cube && (unsigned)r2 < (unsigned)mc2 && (unsigned)c2 < (unsigned)mc3;
+                const unsigned wm = sh.mwin[type * 24 + (okm ? r : 0)], wc = sh.mwin[4 * 24 + (okc ? r2 : 0)];
+                if (okm && ((wm >> cc) & 1u)) code = code0;
+                if (okc && ((wc >> c2) & 1u)) code |= 1u << 5;
                 const int ca = gi - ci0, cb = gj - cj0;
-                if (code && (unsigned)ca < (unsigned)CROP && (unsigned)cb < (unsigned)CROP) {
-                    const int pos = ca * CROP + cb;
-                    atomicOr(&cmap32[pos >> 2], code << (8 * (pos & 3)));
-                }
+                pos = (unsigned)ca < (unsigned)CROP && (unsigned)cb < (unsigned)CROP ? ca * CROP + cb : -1;
+                return code;
+            };
+            // two box-row pairs per iteration: their fp64 chains are independent, so they overlap
+            // (one pair per iteration left each wave's stamps a serial latency chain)
+            const int nrp = (bi1 - bi0) / 2 + 1;
+            for (int rp = sub; rp < nrp; rp += 2 * wpr) {
+                int pa, pb = -1;
+                const unsigned ka = stamp(rp, pa);
+                const unsigned kb = rp + wpr < nrp ? stamp(rp + wpr, pb) : 0u;
+                if (ka && pa >= 0) atomicOr(&cmap32[pa >> 2], ka << (8 * (pa & 3)));
+                if (kb && pb >= 0) atomicOr(&cmap32[pb >> 2], kb << (8 * (pb & 3)));
             }
         }
         g.sync();
@@ -2481,6 +2529,104 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
 #ifdef SIMAPS_PHASE_STAMPS
     if (tid == 0 && blockIdx.x < MAX_STAMP_WG) g_stamps[blockIdx.x * NSTAMP + 10] = (unsigned long long)sh.rounds;
 #endif
+}
+
+// ------------------------------------------------------------------------------------------------
+// Reward lookups from the receptacle distance cache (simaps_sp_lookup)
+// ------------------------------------------------------------------------------------------------
+// Mapper.distance_to_receptacle (envs.py:2190-2194) between two map updates is answered by the
+// reference from its GridGraph cache (shortest_paths.pyx:116-119, 156-163), which get_state filled
+// with the receptacle-source SPFA: here the slot's cached array.  Per agent, one lane per target: a
+// target pixel inside the rect whose cached value is above -inf is free = its own snapped cell
+// (EDT distance 0, the common case) and reads its value; the others need the EDT snap, whose free
+// bits are rebuilt from the cached array once per agent (only if some target needs them) and which
+// runs two targets at a time (snap_sources).  Same values as sp_distance_kernel, bitwise.
+struct LookupHdr {
+    int h, w, i0, j0;
+    int src_q[2][2], src_s[2][2], src_ok[2];
+};
+struct LookupScratch {
+    B128 freeb[MAX_ROWS];
+};
+constexpr int LNT = 128;  // two waves: snap_sources' two slots
+__global__ void __launch_bounds__(LNT) sp_lookup_kernel(simaps_config cfg, const simaps_agent *__restrict__ agents,
+                                                        const char *__restrict__ rec_cache, int rec_bytes,
+                                                        const double *__restrict__ targets, int Q,
+                                                        double *__restrict__ out)
+{
+    __shared__ LookupHdr sh;
+    __shared__ LookupScratch S;
+    __shared__ uint64_t slow_mask;
+    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int H = cfg.H, W = cfg.W, h = cfg.room_h, w = cfg.room_w, i0 = cfg.room_i0, j0 = cfg.room_j0;
+    const int pw = sssp_pitch(w);
+    const simaps_agent ag = agents[n];
+    const char *rec = rec_cache + (size_t)ag.map_slot * rec_bytes;
+    const int src_ok = reinterpret_cast<const int *>(rec)[1];
+    const float *D = reinterpret_cast<const float *>(rec + REC_HDR);
+    if (tid == 0) {
+        sh.h = h;
+        sh.w = w;
+        sh.i0 = i0;
+        sh.j0 = j0;
+    }
+    // dists[target] (pyx:156-163) as a Python float / 96; unreachable -> -1 (pyx:110-112)
+    auto lookup = [&](int si, int sj) {
+        float d = -1.0f;
+        if (src_ok) {
+            const float v = D[(si - i0 + 1) * pw + (sj - j0 + 1)];
+            if (fabsf(v) != INFINITY) d = v;
+        }
+        return (double)d / PPM;
+    };
+    bool built = false;  // the free bits (uniform)
+    for (int c0 = 0; c0 < Q; c0 += 64) {
+        const int cn = Q - c0 < 64 ? Q - c0 : 64;
+        if (tid < 64) {
+            bool slow = false;
+            if (tid < cn) {
+                const double *t = targets + 2 * ((size_t)n * Q + c0 + tid);
+                int qi, qj;
+                pos_to_pix(t[0], t[1], H, W, qi, qj);
+                const int qr = qi - i0, qc = qj - j0;
+                const bool in = qr >= 0 && qr < h && qc >= 0 && qc < w;
+                if (in && D[(qr + 1) * pw + qc + 1] != -INFINITY)
+                    out[(size_t)n * Q + c0 + tid] = lookup(qi, qj);
+                else
+                    slow = true;
+            }
+            const uint64_t m = __ballot(slow);
+            if (tid == 0) slow_mask = m;
+        }
+        lds_barrier();
+        const uint64_t sm = slow_mask;
+        if (sm && !built) {  // free bits of the rect rows, lane l -> columns l and l + 64
+            for (int r = tid >> 6; r < h; r += LNT / 64) {
+                const float *row = D + (r + 1) * pw + 1;
+                const uint64_t lo = __ballot(lane < w && row[lane] != -INFINITY);
+                const uint64_t hi = __ballot(lane + 64 < w && row[lane + 64] != -INFINITY);
+                if (lane == 0) S.freeb[r] = B128{lo, hi};
+            }
+            built = true;
+            lds_barrier();
+        }
+        for (uint64_t m = sm; m;) {
+            int q[2] = {0, 0}, nq = 0;
+            while (m && nq < 2) {
+                q[nq++] = c0 + __builtin_ctzll(m);
+                m &= m - 1;
+            }
+            if (tid < nq) {
+                const double *t = targets + 2 * ((size_t)n * Q + q[tid]);
+                pos_to_pix(t[0], t[1], H, W, sh.src_q[tid][0], sh.src_q[tid][1]);
+            }
+            lds_barrier();
+            snap_sources(sh, S, nq, Group{tid, LNT, nullptr, LNT / 64});
+            if (tid < nq) out[(size_t)n * Q + q[tid]] = sh.src_ok[tid] ? lookup(sh.src_s[tid][0], sh.src_s[tid][1]) : -1.0 / PPM;
+            lds_barrier();
+        }
+        if (c0 + 64 < Q) lds_barrier();  // every wave has read slow_mask before the next chunk rewrites it
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2551,7 +2697,7 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
                                                          const uint8_t *__restrict__ occupancy,
                                                          const double *__restrict__ sources,
                                                          const double *__restrict__ targets, int Q,
-                                                         double *__restrict__ out, unsigned *fault)
+                                                         double *__restrict__ out, char *rec_cache, unsigned *fault)
 {
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     Shared &sh = *reinterpret_cast<Shared *>(smem);
@@ -2581,6 +2727,8 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
     const bool src_ok = sh.src_ok[0];
     sssp(sh, S, dist, 1);  // the source's distance image (GridGraph._spfa_with_cache, pyx:116-119)
     if (tid == 0) post_faults(fault, group_faults(sh.bar, sh.rounds, 1) | (sh.flag[1] ? SIMAPS_FAULT_DESCRIPTOR : 0u));
+    if (rec_cache)  // the source is the receptacle (the caller's contract): keep the array for simaps_sp_lookup
+        rec_export(rec_cache + (size_t)ag.map_slot * rec_cache_bytes(sh.h, sh.w), dist, sh.h, sh.w, src_ok, S.freeb, tid, NT);
     const int pw = sssp_pitch(sh.w);
     // dists[target] (pyx:156-163) as a Python float / LOCAL_MAP_PIXELS_PER_METER; unreachable -> -1
     // (pyx:110-112)
@@ -3800,6 +3948,14 @@ Geometry make_geometry()
     return g;
 }
 
+// The robot geometry never changes: computed once per process (the mask tables are ~2,000 fp64
+// mask_bit evaluations, which every launch used to repeat on the host).
+const Geometry &geometry()
+{
+    static const Geometry g = make_geometry();
+    return g;
+}
+
 // Path kernel choice: the early-exit variant (SSSP fixpoint first, then the SPFA only until the target's
 // parent chain is final) unless simaps_path_mode(1) forces the compact one.  Same LDS footprint and
 // the same pop loop, so it pays only its sweeps (~15 us small rooms, ~26 us large) and chain checks:
@@ -3967,7 +4123,7 @@ int simaps_robot_mask(int type, int with_cube, float *out)
 {
     if (type < 0 || type > 3 || !out) return fail(SIMAPS_EINVAL, "bad robot type / output");
     if (with_cube && type != SIMAPS_LIFTING) return fail(SIMAPS_EINVAL, "lifted cube mask is LiftingRobot only");
-    const Geometry g = make_geometry();
+    const Geometry &g = geometry();
     for (int i = 0; i < LW; i++)
         for (int j = 0; j < LW; j++) out[i * LW + j] = mask_bit(g, type, with_cube != 0, i, j) ? 1.0f : 0.0f;
     return 0;
@@ -3978,7 +4134,7 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
                      float *state, int num_robots_per_env, const simaps_debug *dbg, void *stream)
 {
     int rc = check_cfg(cfg);
-    const Geometry geo = make_geometry();
+    const Geometry &geo = geometry();
     for (int t = 0; t < 4; t++)
         if (geo.cspace_r[t] > RMAX) return fail(SIMAPS_EUNSUPPORTED, "cspace radius %d > %d", geo.cspace_r[t], RMAX);
     if (rc) return rc;
@@ -4000,9 +4156,32 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
     return 0;
 }
 
+int simaps_rec_cache_bytes(const simaps_config *cfg)
+{
+    const int rc = check_cfg(cfg);
+    if (rc) return rc;
+    return rec_cache_bytes(cfg->room_h, cfg->room_w);
+}
+
+int simaps_sp_lookup(const simaps_config *cfg, int N, const simaps_agent *agents, const void *rec_cache,
+                     const double *targets, int Q, double *out, void *stream)
+{
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (N < 0 || Q < 0) return fail(SIMAPS_EINVAL, "N < 0 or Q < 0");
+    if (N == 0 || Q == 0) return 0;
+    if (!agents || !rec_cache || !targets || !out) return fail(SIMAPS_EINVAL, "NULL buffer");
+    if ((rc = pending_faults())) return rc;
+    hipLaunchKernelGGL(sp_lookup_kernel, dim3(N), dim3(LNT), 0, (hipStream_t)stream, *cfg, agents,
+                       reinterpret_cast<const char *>(rec_cache), rec_cache_bytes(cfg->room_h, cfg->room_w), targets, Q, out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "sp_lookup launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
 int simaps_sp_distance(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
                        const simaps_robot *robots, const uint8_t *occupancy, const double *sources,
-                       const double *targets, int Q, double *out, void *stream)
+                       const double *targets, int Q, double *out, void *rec_cache, void *stream)
 {
     int rc = check_cfg(cfg);
     if (rc) return rc;
@@ -4011,9 +4190,9 @@ int simaps_sp_distance(const simaps_config *cfg, int N, const simaps_agent *agen
     if (!agents || !envs || !robots || !occupancy || !sources || !targets || !out)
         return fail(SIMAPS_EINVAL, "NULL buffer");
     if ((rc = pending_faults())) return rc;
-    const Geometry geo = make_geometry();
+    const Geometry &geo = geometry();
     hipLaunchKernelGGL(sp_distance_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, geo, agents, envs, robots,
-                       occupancy, sources, targets, Q, out, g_fault_dev);
+                       occupancy, sources, targets, Q, out, reinterpret_cast<char *>(rec_cache), g_fault_dev);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "sp_distance launch: %s", hipGetErrorString(e));
     return 0;
@@ -4030,7 +4209,7 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
     if (!agents || !envs || !robots || !occupancy || !sources || !targets || !out_xy || !out_count)
         return fail(SIMAPS_EINVAL, "NULL buffer");
     if ((rc = pending_faults())) return rc;
-    const Geometry geo = make_geometry();
+    const Geometry &geo = geometry();
     const bool small = (cfg->room_h + 2) * ((cfg->room_w + 2) | 1) <= PATH_SMALL_CELLS;
     const hipStream_t st = (hipStream_t)stream;
     PathScratch ps;

@@ -207,11 +207,23 @@ class StateBatch:
         self._type_group = np.array([(_lib.TYPE_IDS[r['type']], r['group_index']) for s in scenes for r in s['robots']],
                                     dtype=np.int32).reshape(-1, 2)
         self.layout = layout
+        # receptacle distance cache (receptacle_distances): one record per map slot, allocated on first
+        # use; a record is current while its slot's map version equals the version it was made at
+        self._rec = None
+        self._map_ver = np.zeros(self.N, dtype=np.int64)
+        self._rec_ver = np.full(self.N, -1, dtype=np.int64)
 
     def set_descriptors(self, scenes):
         """Upload a new per-step scene descriptor (poses, controller state, paths)."""
         robots, envs, ag, paths = pack_descriptors(scenes, self.agents)
         self.scenes = scenes
+        if hasattr(self, '_rec_ver'):
+            self._rec_ver[:] = -1  # new scenes may move a receptacle: no cached array stays valid
+        # per map slot: its env's receptacle (x, y) (receptacle_distances' SSSP source)
+        env_of = np.asarray([e for e, _ in self.agents], dtype=np.int64)
+        self._slot_has_rec = np.asarray([scenes[e]['receptacle_position'] is not None for e in env_of], dtype=bool)
+        self._slot_rec_xy = np.asarray([scenes[e]['receptacle_position'][:2] if scenes[e]['receptacle_position'] is not None
+                                        else (0.0, 0.0) for e in env_of], dtype=np.float64).reshape(-1, 2)
         # (ingest takes the camera poses from here)
         self.pose_host = np.stack([robots['x'], robots['y'], robots['heading']], 1) if len(robots) else np.zeros((0, 3))
         self._robot_off = envs['robot_off'].astype(np.int64)
@@ -274,6 +286,8 @@ class StateBatch:
         step (envs.py:2056-2062, 2447-2450) -- for every map slot, or for `slots` only.  Inputs are
         [n, H, W] arrays / tensors (uint8 occupancy, float32 overhead-without-robots)."""
         idx = None if slots is None else torch.as_tensor(list(slots), dtype=torch.long, device=self.device)
+        if occupancy is not None:  # the cspace follows the occupancy map: cached receptacle arrays go stale
+            self._map_ver[slice(None) if slots is None else np.asarray(list(slots), dtype=np.int64)] += 1
         for name, dst, dt in (('occupancy', self.occupancy, torch.uint8), ('overhead', self.overhead, torch.float32)):
             src = occupancy if name == 'occupancy' else overhead
             if src is None:
@@ -339,24 +353,29 @@ class StateBatch:
         if n == 0:
             return out
         dbg = None
-        if debug is not None:
+        rec = self._rec if self._rec is not None and self.flags['use_shortest_path_to_receptacle_map'] else None
+        if debug is not None or rec is not None:
+            debug = debug or {}
             for k, v in debug.items():
                 if v is not None and (v.shape[0] != n or not v.is_contiguous() or v.device != self.device):
                     raise ValueError('debug[%r] must be contiguous with leading dim %d on %s' % (k, n, self.device))
             dbg = _lib.Debug(*(debug[k].data_ptr() if debug.get(k) is not None else None
-                               for k in ('cspace', 'sources', 'dist', 'status')))
+                               for k in ('cspace', 'sources', 'dist', 'status')), None if rec is None else rec.data_ptr())
         s, cur = launch_stream(self.device, stream)
         _lib.check(_lib.lib.simaps_get_state(
             self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d),
             _lib.ptr(self.paths_d), _lib.ptr(self.occupancy), _lib.ptr(self.overhead), _lib.ptr(out),
             self.num_robots if self.flags['use_intention_channels'] else 0,
             None if dbg is None else dbg, _lib.stream_handle(s)))
-        hold(s, cur, out, agents_d, self.envs_d, self.robots_d, self.paths_d, self.occupancy, self.overhead,
+        hold(s, cur, out, agents_d, self.envs_d, self.robots_d, self.paths_d, self.occupancy, self.overhead, rec,
              *(debug.values() if debug else ()))
+        if rec is not None:  # every rendered slot's receptacle array is now its current map's
+            sl = np.arange(self.N) if slots is None else np.asarray(list(slots), dtype=np.int64)
+            self._rec_ver[sl] = self._map_ver[sl]
         return out
 
 
-    def shortest_path_distances(self, sources, targets, slots=None, stream=None):
+    def shortest_path_distances(self, sources, targets, slots=None, stream=None, _rec=None):
         """OccupancyMap.shortest_path_distance(source, target) (envs.py:2507-2512) on each agent's own
         map: sources [n, 2] and targets [n, Q, 2] fp64 (x, y) positions for map slots `slots` (all
         agents if None) -> [n, Q] float64 device tensor (metres; -1/96 where unreachable)."""
@@ -372,8 +391,70 @@ class StateBatch:
         s, cur = launch_stream(self.device, stream)
         _lib.check(_lib.lib.simaps_sp_distance(
             self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d), _lib.ptr(self.occupancy),
-            _lib.ptr(src), _lib.ptr(tgt), Q, _lib.ptr(out), _lib.stream_handle(s)))
-        hold(s, cur, src, tgt, out, agents_d, self.envs_d, self.robots_d, self.occupancy)
+            _lib.ptr(src), _lib.ptr(tgt), Q, _lib.ptr(out), _lib.ptr(_rec), _lib.stream_handle(s)))
+        hold(s, cur, src, tgt, out, agents_d, self.envs_d, self.robots_d, self.occupancy, _rec)
+        return out
+
+    def enable_receptacle_cache(self):
+        """Allocate the receptacle distance cache (one simaps_rec_cache_bytes record per map slot): from
+        now on render() keeps every rendered agent's receptacle array (with
+        use_shortest_path_to_receptacle_map) and receptacle_distances() answers from it."""
+        if self._rec is None:
+            nb = _lib.lib.simaps_rec_cache_bytes(self.cfg)
+            _lib.check(min(nb, 0))
+            self._rec = torch.empty((self.N, nb), dtype=torch.uint8, device=self.device)
+            self._rec_ver[:] = -1
+        return self._rec
+
+    def receptacle_distances(self, targets, slots=None, stream=None, cache=True):
+        """Mapper.distance_to_receptacle with shortest-path partial rewards (envs.py:2190-2194) on each
+        agent's own map: targets [n, Q, 2] fp64 (x, y) for map slots `slots` (all if None) -> [n, Q]
+        float64 device tensor (metres; -1/96 unreachable).  Like the reference, which answers from the
+        GridGraph cache get_state filled (shortest_paths.pyx:116-119, 156-163): slots whose cached
+        receptacle array belongs to their current map (render() since the last map change) are a
+        lookup (simaps_sp_lookup); the others run the full SSSP from the receptacle (simaps_sp_distance)
+        and keep their array for the next call.  cache=False: always the full SSSP, nothing kept."""
+        sl = np.arange(self.N, dtype=np.int64) if slots is None else np.asarray(list(slots), dtype=np.int64)
+        n = len(sl)
+        tgt = torch.as_tensor(targets, dtype=torch.float64).to(self.device).contiguous()
+        if tgt.dim() != 3 or tgt.shape[0] != n or tgt.shape[2] != 2:
+            raise ValueError('targets must be [%d, Q, 2]' % n)
+        if not self._slot_has_rec[sl].all():
+            raise ValueError('distance_to_receptacle needs a receptacle (not a rescue env)')
+        if not cache:
+            return self.shortest_path_distances(self._slot_rec_xy[sl], tgt, slots=slots, stream=stream)
+        rec = self.enable_receptacle_cache()
+        hit = self._rec_ver[sl] == self._map_ver[sl]
+        Q = tgt.shape[1]
+        s, cur = launch_stream(self.device, stream)
+        with torch.cuda.stream(s):  # (every launch, copy and allocation below on the launch stream)
+            out = torch.empty((n, Q), dtype=torch.float64, device=self.device)
+            if n == 0 or Q == 0:
+                return out
+            if hit.all():  # the common case: one lookup launch straight into `out`
+                groups = [(None, out)]
+            else:
+                groups = [(np.nonzero(~hit)[0], None), (np.nonzero(hit)[0], None)]
+            for k, (rows, dst) in enumerate(groups):
+                if rows is not None and len(rows) == 0:
+                    continue
+                full = len(groups) == 2 and k == 0  # the misses: full SSSP, arrays into the cache
+                sub = None if rows is None else torch.as_tensor(rows, device=self.device)
+                th = tgt if sub is None else tgt[sub].contiguous()
+                rs_ = sl if rows is None else sl[rows]
+                if full:
+                    o = self.shortest_path_distances(self._slot_rec_xy[rs_], th, slots=rs_, stream=s, _rec=rec)
+                    self._rec_ver[rs_] = self._map_ver[rs_]
+                else:
+                    agents_d, m = self.subset_descriptor(rs_) if (slots is not None or rows is not None) \
+                        else (self.agents_d, self.N)
+                    o = dst if dst is not None else torch.empty((m, Q), dtype=torch.float64, device=self.device)
+                    _lib.check(_lib.lib.simaps_sp_lookup(self.cfg, m, _lib.ptr(agents_d), _lib.ptr(rec), _lib.ptr(th),
+                                                         Q, _lib.ptr(o), _lib.stream_handle(s)))
+                    hold(s, cur, agents_d, th, o)
+                if sub is not None:
+                    out[sub] = o
+        hold(s, cur, rec, tgt, out)
         return out
 
 
@@ -454,7 +535,8 @@ class StateBatch:
         if getattr(self, '_boxes', None) is None or self._boxes.numel() < nbox:
             self._boxes = torch.empty((nbox,), dtype=torch.int32, device=self.device)
         cam = _lib.Camera(spec.height_px, spec.width_px, spec.near, spec.far, spec.cx2, spec.cy2)
-        return {'n': n, 'cam': cam, 'agents': agents_d, 'ids': _to_dev(ids, self.device),
+        return {'n': n, 'slots': np.asarray(idx, dtype=np.int64), 'cam': cam, 'agents': agents_d,
+                'ids': _to_dev(ids, self.device),
                 'params': torch.from_numpy(params).to(self.device), 'depth': dep, 'seg': seg}
 
     def reset_ingest_keys(self, stream=None):
@@ -478,6 +560,7 @@ class StateBatch:
     def launch_ingest(self, prep, stream=None):
         if prep['n'] == 0:
             return
+        self._map_ver[prep['slots']] += 1  # (the receptacle cache of these slots goes stale)
         s, cur = launch_stream(self.device, stream)
         with torch.cuda.stream(s):
             capturing = torch.cuda.is_current_stream_capturing()

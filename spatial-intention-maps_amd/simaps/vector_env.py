@@ -158,17 +158,16 @@ class VectorEnvObservations:
         Qs = [len(p) for pe in positions for p in pe]
         Q = max(Qs) if Qs else 0
         n = self.batch.N
-        src = np.zeros((n, 2))
         tgt = np.zeros((n, max(Q, 1), 2))
         for (e, a), k in self.slot.items():
-            rec = self.batch.scenes[e]['receptacle_position']
-            if rec is None:
+            if self.batch.scenes[e]['receptacle_position'] is None:
                 raise ValueError('distance_to_receptacle needs a receptacle (not a rescue env)')
-            src[k] = rec[:2]
             for q, p in enumerate(positions[e][a]):
                 tgt[k, q] = p[:2]
         if Q:
-            d = self.batch.shortest_path_distances(src, tgt[:, :Q], stream=stream)
+            # from the receptacle arrays get_state left in the cache where the maps are unchanged
+            # (the reference's GridGraph cache), a full SSSP elsewhere (StateBatch.receptacle_distances)
+            d = self.batch.receptacle_distances(tgt[:, :Q], stream=stream)
             if stream is not None:
                 torch.cuda.current_stream(self.batch.device).wait_stream(stream)
             d = d.cpu().numpy()

@@ -22,7 +22,7 @@ def test_header_declares_the_abi():
                                          'simaps_num_channels', 'simaps_sp_distance', 'simaps_shortest_path',
                                          'simaps_ingest', 'simaps_ingest_chunks', 'simaps_path_mode', 'simaps_robot_mask', 'simaps_pack_robots',
                                          'simaps_get_state', 'simaps_sssp_grid',
-                                         'simaps_grid_path'])
+                                         'simaps_grid_path', 'simaps_rec_cache_bytes', 'simaps_sp_lookup'])
 
 
 def test_library_exports_every_declared_symbol():
@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(_lib.lib, name), name
         assert isinstance(getattr(_lib.lib, name), ctypes._CFuncPtr)
     assert set(_lib.EXPORTED) == set(declared_symbols())
-    assert _lib.lib.simaps_abi_version() == 6
+    assert _lib.lib.simaps_abi_version() == 7
 
 
 def test_struct_layouts_match_header():
@@ -40,7 +40,21 @@ def test_struct_layouts_match_header():
     assert _lib.ENV_DTYPE.itemsize == 32
     assert _lib.AGENT_DTYPE.itemsize == 12
     assert ctypes.sizeof(_lib.Config) == 18 * 4 + 4 * 8
-    assert ctypes.sizeof(_lib.Debug) == 4 * 8
+    assert ctypes.sizeof(_lib.Debug) == 5 * 8
+
+
+def test_rec_cache_record_size():
+    """simaps_rec_cache_bytes: a 16-byte header and the room rect's (h + 2) x ((w + 2) | 1) float32
+    distance array, rounded up to 256 bytes; refuses a bad config (host-side only)."""
+    from simaps import _lib, batch, synthetic
+    for name in ('lifting_4-small_divider', 'pushing_4-large_empty'):
+        s = synthetic.make_scene(name, 0)
+        c = batch.make_config(s['flags'], s['room_width'], s['room_length'])
+        want = (16 + (c.room_h + 2) * ((c.room_w + 2) | 1) * 4 + 255) // 256 * 256
+        assert _lib.lib.simaps_rec_cache_bytes(c) == want
+    c.room_h = 0
+    assert _lib.lib.simaps_rec_cache_bytes(c) == _lib.EINVAL
+    assert _lib.lib.simaps_sp_lookup(None, 1, None, None, None, 1, None, None) == _lib.EINVAL
 
 
 def test_host_robot_masks_match_reference():

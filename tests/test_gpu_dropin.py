@@ -187,6 +187,100 @@ def test_sp_distance_many_targets_vs_oracle(V):
         assert got[n].tolist() == [ao.shortest_path_distance(src[n], t) for t in tgt[n]], (e, a)
 
 
+def _sp_golden_items(z):
+    keys = sorted(k[:-len('_dist')] for k in z.files if k.endswith('_dist'))
+    by_cfg = {}
+    for key in keys:
+        cfg, rest = key.rsplit('_e', 1)
+        e, a = (int(x) for x in rest.split('_a'))
+        by_cfg.setdefault(cfg, []).append((e, a, key))
+    return by_cfg
+
+
+def test_receptacle_lookups_from_the_render_cache_reference_goldens(V):
+    """Mapper.distance_to_receptacle answered from the receptacle arrays get_state
+    left in the cache (the reference's GridGraph cache, shortest_paths.pyx:116-119, 156-163) -- after
+    one render every lookup is a cache hit (simaps_sp_lookup, no SSSP) -- equals the reference's own
+    values; so does the cold path (full SSSP, which then fills the cache) and the second, cached call."""
+    synthetic, vector_env = V
+    from simaps import batch
+    z = G.load('sp_distance.npz')
+    for cfg, items in _sp_golden_items(z).items():
+        scenes = [synthetic.make_scene(cfg, 40 + e) for e in range(2)]
+        if scenes[0]['receptacle_position'] is None:
+            continue
+        slots = None
+        want = None
+        for mode in ('render', 'cold'):
+            b = batch.StateBatch(scenes)
+            slots = [b.agents.index((e, a)) for e, a, _ in items]
+            tgt = np.stack([z[k + '_queries'] for _, _, k in items])
+            want = np.stack([z[k + '_dist'] for _, _, k in items])
+            b.enable_receptacle_cache()
+            if mode == 'render':
+                b.render()
+                assert (b._rec_ver == b._map_ver).all()           # every slot cached
+            else:
+                assert not (b._rec_ver[slots] == b._map_ver[slots]).any()
+            got = b.receptacle_distances(tgt, slots=slots).cpu().numpy()
+            assert np.array_equal(got, want), (cfg, mode)
+            assert (b._rec_ver[slots] == b._map_ver[slots]).all()  # (the cold call filled the cache)
+            again = b.receptacle_distances(tgt, slots=slots).cpu().numpy()
+            assert np.array_equal(again, want), (cfg, mode, 'cached')
+
+
+def test_receptacle_cache_follows_map_updates(V):
+    """An ingest (and a set_maps) between the render and the lookups invalidates exactly those slots'
+    cached arrays: their lookups run the SSSP on the new maps, the others stay cache hits, and all of
+    them equal the oracle on the current maps -- also for blocked / outside targets (the EDT slow path
+    rebuilt from the cached array) and in a batch whose render does not fill the cache (no
+    shortest-path-to-receptacle channel: every first lookup is a miss)."""
+    synthetic, vector_env = V
+    from simaps import batch, camera
+    spec = camera.CAMERAS['forward']
+    rs = np.random.RandomState(21)
+    for no_channel in (False, True):
+        scenes = [synthetic.make_scene('lifting_4-small_divider', 660 + e) for e in range(3)]
+        if no_channel:
+            for sc in scenes:
+                sc['flags'] = dict(sc['flags'], use_shortest_path_to_receptacle_map=False)
+        b = batch.StateBatch(scenes)
+        b.enable_receptacle_cache()
+        b.render()
+        Q = 70
+        tgt = np.stack([rs.uniform(-0.3, 0.3, (b.N, Q)), rs.uniform(-0.3, 0.3, (b.N, Q))], -1)
+        tgt[:, ::4, 0] = rs.choice([0.0, -0.5, 0.5, 0.55], (b.N, len(range(0, Q, 4))))  # divider, walls, outside
+
+        def check(tag):
+            got = b.receptacle_distances(tgt).cpu().numpy()
+            for n, (e, a) in enumerate(b.agents):
+                ao = O.AgentOracle(scenes[e], a)
+                rec = scenes[e]['receptacle_position']
+                assert got[n].tolist() == [ao.shortest_path_distance(rec, t) for t in tgt[n]], (tag, e, a)
+        if not no_channel:
+            assert (b._rec_ver == b._map_ver).all()
+        check('after render')
+        moved = [0, 5, 9]
+        f = [synthetic.camera_images(scenes[e], a, 'forward', seed=31 + k) for k, (e, a) in
+             enumerate(b.agents[k] for k in moved)]
+        b.ingest(np.stack([x[0] for x in f]), np.stack([x[1] for x in f]).astype(np.int32), slots=moved)
+        for k, (x, n) in enumerate(zip(f, moved)):
+            e, a = b.agents[n]
+            r = scenes[e]['robots'][a]
+            O.ingest(scenes[e]['overhead'][a], scenes[e]['occupancy'][a], x[0], x[1],
+                     spec.params(r['position'][0], r['position'][1], r['heading']), spec, synthetic.SEG_IDS,
+                     scenes[e]['receptacle_position'] is not None)
+        stale = b._rec_ver != b._map_ver
+        assert sorted(np.nonzero(stale)[0].tolist()) == moved
+        check('after ingest')
+        occ = scenes[1]['occupancy'][2].copy()
+        occ[60:70, 100:110] = 1   # a new obstacle in slot 6's map
+        scenes[1]['occupancy'][2] = occ
+        b.set_maps(occupancy=occ[None], slots=[6])
+        assert (b._rec_ver != b._map_ver).sum() == 1
+        check('after set_maps')
+
+
 def test_distance_to_receptacle_dropin(V):
     synthetic, vector_env = V
     scenes = [synthetic.make_scene('lifting_2_throwing_2-large_empty', 70 + e) for e in range(3)]

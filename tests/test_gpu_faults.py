@@ -213,7 +213,7 @@ def test_path_bad_descriptor_is_reported(S):
     out = torch.empty((b.N, 3), dtype=torch.float64, device=b.device)
     _lib.lib.simaps_fault_status(1)
     assert _lib.lib.simaps_sp_distance(b.cfg, b.N, _lib.ptr(A), _lib.ptr(E), _lib.ptr(R), _lib.ptr(b.occupancy),
-                                       _lib.ptr(src), _lib.ptr(tgt), 3, _lib.ptr(out), _lib.stream_handle()) == 0
+                                       _lib.ptr(src), _lib.ptr(tgt), 3, _lib.ptr(out), None, _lib.stream_handle()) == 0
     torch.cuda.synchronize()
     assert _lib.lib.simaps_fault_status(1) == _lib.FAULT_DESCRIPTOR
     xy = torch.empty((b.N, 64, 2), dtype=torch.float64, device=b.device)

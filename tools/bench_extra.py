@@ -3,6 +3,8 @@
   sp_distance    OccupancyMap.shortest_path_distance (reward lookups): queries/s
   shortest_path  OccupancyMap.shortest_path (movement paths): paths/s
   ingest         Robot.update_map minus the simulator (camera frame -> overhead / occupancy maps): frames/s
+  distance_to_receptacle  the reward lookups from the receptacle, cold and from the render's cache
+  env_step       (--env-step) the device time of one reference VectorEnv.step: paths, ingest, get_state
 
     python tools/bench_extra.py [--config lifting_4-small_divider] [--envs 64] [--queries 8]
 
@@ -73,6 +75,24 @@ def main():
                       'gpu_queries_per_s': N * Q / dt, 'gpu_ms_per_launch': dt * 1e3,
                       'cpu_oracle_queries_per_s': n / el, 'cpu_cores': 1,
                       'cpu_sample': '%d queries incl. each agent\'s cspace / EDT / SPFA' % n}), flush=True)
+    if rec is not None:
+        # reward lookups from the receptacle (Mapper.distance_to_receptacle): cold = the full SSSP per
+        # call (no cache); cached = the arrays the last render left (simaps_sp_lookup), as the
+        # reference's GridGraph cache answers between two map updates
+        cold = timed(lambda: b.receptacle_distances(tgt_d, cache=False), args.steps, 3)
+        b.enable_receptacle_cache()
+        b.render()
+        cached = timed(lambda: b.receptacle_distances(tgt_d), args.steps, 3)
+        assert (b._rec_ver == b._map_ver).all()
+        got_c = b.receptacle_distances(tgt_d).cpu().numpy()
+        got_f = b.receptacle_distances(tgt_d, cache=False).cpu().numpy()
+        print(json.dumps({'row': 'distance_to_receptacle', 'config': args.config, 'agents': N, 'queries_per_agent': Q,
+                          'cold_ms_per_call': cold * 1e3, 'cached_ms_per_call': cached * 1e3,
+                          'cold_queries_per_s': N * Q / cold, 'cached_queries_per_s': N * Q / cached,
+                          'cached_equals_cold': bool(np.array_equal(got_c, got_f)),
+                          'note': 'StateBatch.receptacle_distances per call incl. host side; cached: every slot '
+                                  'rendered since its last map change (simaps_sp_lookup), cold: cache=False '
+                                  '(cspace + snap + SSSP per agent, simaps_sp_distance)'}), flush=True)
 
     # movement paths: robot position -> random target (half across x = 0)
     psrc = np.array([scenes[e]['robots'][a]['position'][:2] for e, a in b.agents])
@@ -133,6 +153,54 @@ def bench_dropin_step(args):
                           'note': 'update(%s) + get_state() + synchronize, host packing and uploads included; '
                                   'median of %d steps' % (mode, len(ts))}),
               flush=True)
+
+
+def bench_env_step(args):
+    """the device work of one reference VectorEnv.step (envs.py:230-320) at
+    BASELINE configs[1] (64 envs x 4 lifting robots), for E awaiting robots (default one per env, the
+    steady state; --all: every robot, the first step): movement paths for the new actions
+    (store_new_action -> Mapper.shortest_path, envs.py:234 -> 875-876; targets in the robot's local
+    map, the action space), the awaiting robots' update_map (envs.py:277-280: a forward camera frame
+    each) and their get_state render (envs.py:304, 322-323).  Each launch's device time by HIP
+    events (K back-to-back launches of that part alone) and the three together, in step order, one
+    stream.  Run it under rocprofv3 --kernel-trace --stats for the per-kernel split."""
+    scenes = [synthetic.make_scene(args.config, e) for e in range(args.envs)]
+    b = batch.StateBatch(scenes)
+    A = len(scenes[0]['robots'])
+    slots = list(range(b.N)) if args.all else [e * A + (e % A) for e in range(args.envs)]
+    n = len(slots)
+    rs = np.random.RandomState(4)
+    psrc = np.array([scenes[e]['robots'][a]['position'][:2] for e, a in (b.agents[k] for k in slots)])
+    ptgt = psrc + rs.uniform(-0.5, 0.5, psrc.shape)   # inside the robot's local map
+    src_d, tgt_d = torch.as_tensor(psrc).cuda(), torch.as_tensor(ptgt).cuda()
+    frames = [synthetic.camera_images(scenes[e], a, 'forward', seed=k) for k, (e, a) in enumerate(b.agents[k] for k in slots)]
+    dep = torch.as_tensor(np.stack([f[0] for f in frames])).cuda()
+    seg = torch.as_tensor(np.stack([f[1] for f in frames]).astype(np.int32)).cuda()
+    prep = b.prepare_ingest(dep, seg, camera='forward', slots=slots)
+    out = b.alloc_state(n)
+    s = torch.cuda.current_stream()
+    parts = {'paths': lambda: b.launch_shortest_paths(src_d, tgt_d, slots=slots),
+             'ingest': lambda: b.launch_ingest(prep),
+             'get_state': lambda: b.render(out, slots=slots)}
+    parts['step'] = lambda: [f() for f in (parts['paths'], parts['ingest'], parts['get_state'])]
+    res = {}
+    K = max(args.steps, 20)
+    for name, f in parts.items():
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(K):
+            f()
+        e1.record(s)
+        torch.cuda.synchronize()
+        res[name + '_us'] = e0.elapsed_time(e1) / K * 1e3
+    print(json.dumps(dict({'row': 'env_step', 'config': args.config, 'awaiting_robots': n,
+                           'note': 'device time per reference step (HIP events, %d launches each): movement paths '
+                                   '(early-exit kernel, local-map targets), forward-camera ingest, get_state of the '
+                                   'awaiting robots; step = the three in order on one stream' % K}, **res)),
+          flush=True)
 
 
 def bench_remap(args):
@@ -226,6 +294,10 @@ def bench_ingest(args):
 
 
 if __name__ == '__main__':
+    if '--env-step' in sys.argv:
+        bench_env_step(argparse.Namespace(config='lifting_4-small_divider', envs=64, steps=50, all=False))
+        bench_env_step(argparse.Namespace(config='lifting_4-small_divider', envs=64, steps=50, all=True))
+        sys.exit(0)
     if '--dropin-only' in sys.argv:
         bench_dropin_step(argparse.Namespace(config='lifting_4-small_divider', envs=64, steps=50))
         bench_remap(argparse.Namespace(config='lifting_4-small_divider', envs=64))
