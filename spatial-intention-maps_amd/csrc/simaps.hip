@@ -2460,32 +2460,28 @@ __global__ void __launch_bounds__(NT) get_state_kernel(
             const int *mc = reinterpret_cast<const int *>(sh.mwin + 120 + 4 * 4);
             const int mt0 = mt[0], mt1 = mt[1], mt2 = mt[2], mt3 = mt[3];
             const int mc0 = mc[0], mc1 = mc[1], mc2 = mc[2], mc3 = mc[3];
-            // one box pixel: its stamp code (0: none) -- the fp64 source index (rot_src), the mask
-            // window bits; pos = crop-relative pixel or -1 outside the crop
-            auto stamp = [&](int rp, int &pos) -> unsigned {
+            // (two box-row pairs per iteration, their fp64 chains interleaved, measured slower: the
+            // stamps phase 3.8 -> 4.4 us, round 4)
+            for (int rp = sub; 2 * rp <= bi1 - bi0; rp += wpr) {
                 const int gi = bi0 + 2 * rp + (ln >> 5), gj = bj0 + (ln & 31);
                 unsigned code = 0;
-                int m0 = 0, m1 = 0;
-                const bool in = gi <= bi1 && gj <= bj1 && rot_src(R, LW, gi - st_i, gj - st_j, m0, m1);
-                const int r = m0 - mt0, cc = m1 - mt1, r2 = m0 - mc0, c2 = m1 - mc1;
-                const bool okm = in && (unsigned)r < (unsigned)mt2 && (unsigned)cc < (unsigned)mt3;
-                const bool okc = in && cube && (unsigned)r2 < (unsigned)mc2 && (unsigned)c2 < (unsigned)mc3;
-                const unsigned wm = sh.mwin[type * 24 + (okm ? r : 0)], wc = sh.mwin[4 * 24 + (okc ? r2 : 0)];
-                if (okm && ((wm >> cc) & 1u)) code = code0;
-                if (okc && ((wc >> c2) & 1u)) code |= 1u << 5;
+                if (gi <= bi1 && gj <= bj1) {
+                    int m0, m1;
+                    const bool in = rot_src(R, LW, gi - st_i, gj - st_j, m0, m1);
+                    if (in) {
+                        const int r = m0 - mt0, cc = m1 - mt1;
+                        if ((unsigned)r < (unsigned)mt2 && (unsigned)cc < (unsigned)mt3 && ((sh.mwin[type * 24 + r] >> cc) & 1u))
+                            code = code0;
+                        const int r2 = m0 - mc0, c2 = m1 - mc1;
+                        if (cube && (unsigned)r2 < (unsigned)mc2 && (unsigned)c2 < (unsigned)mc3 && ((sh.mwin[4 * 24 + r2] >> c2) & 1u))
+                            code |= 1u << 5;
+                    }
+                }
                 const int ca = gi - ci0, cb = gj - cj0;
-                pos = (unsigned)ca < (unsigned)CROP && (unsigned)cb < (unsigned)CROP ? ca * CROP + cb : -1;
-                return code;
-            };
-            // two box-row pairs per iteration: their fp64 chains are independent, so they overlap
-            // (one pair per iteration left each wave's stamps a serial latency chain)
-            const int nrp = (bi1 - bi0) / 2 + 1;
-            for (int rp = sub; rp < nrp; rp += 2 * wpr) {
-                int pa, pb = -1;
-                const unsigned ka = stamp(rp, pa);
-                const unsigned kb = rp + wpr < nrp ? stamp(rp + wpr, pb) : 0u;
-                if (ka && pa >= 0) atomicOr(&cmap32[pa >> 2], ka << (8 * (pa & 3)));
-                if (kb && pb >= 0) atomicOr(&cmap32[pb >> 2], kb << (8 * (pb & 3)));
+                if (code && (unsigned)ca < (unsigned)CROP && (unsigned)cb < (unsigned)CROP) {
+                    const int pos = ca * CROP + cb;
+                    atomicOr(&cmap32[pos >> 2], code << (8 * (pos & 3)));
+                }
             }
         }
         g.sync();

@@ -84,10 +84,11 @@ def _load(path=LIB_PATH):
     L.simaps_get_state.restype = i32
     L.simaps_sp_distance.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.simaps_sp_distance.restype = i32
-    L.simaps_rec_cache_bytes.argtypes = [ctypes.POINTER(Config)]
-    L.simaps_rec_cache_bytes.restype = i32
-    L.simaps_sp_lookup.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, i32, vp, vp]
-    L.simaps_sp_lookup.restype = i32
+    if hasattr(L, 'simaps_sp_lookup'):  # (ABI 7; absent only in an older revision's A/B build)
+        L.simaps_rec_cache_bytes.argtypes = [ctypes.POINTER(Config)]
+        L.simaps_rec_cache_bytes.restype = i32
+        L.simaps_sp_lookup.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, i32, vp, vp]
+        L.simaps_sp_lookup.restype = i32
     L.simaps_shortest_path.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.simaps_shortest_path.restype = i32
     L.simaps_ingest.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(Camera), i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp]
