@@ -43,6 +43,33 @@ def cpu_baseline(config, budget_s=6.0, procs=0):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
+PHASE_PROFILE = os.path.join('profiles', 'phase_binding.json')
+
+
+def binding_note(config, stacks, layout):
+    """How to read roofline.frac: the kernel is latency-bound, not HBM-bound (DESIGN.md section 5,
+    'Second roof').  Each of the 256 workgroups renders one stack on its own CU, so a launch lasts as
+    long as its workgroups' two concurrent dependency chains -- the SSSP sweep track and the render
+    track -- plus the distance phase after their join.  The per-workgroup medians come from the
+    committed s_memrealtime stamp profile of the same config / launch size / layout
+    (tools/phase_profile.py on the stamp build, summarised into profiles/phase_binding.json), or
+    None when there is none."""
+    path = os.path.join(ROOT, PHASE_PROFILE)
+    try:
+        p = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if (p.get('config'), p.get('N'), p.get('layout')) != (config, stacks, layout):
+        return None
+    st, rt = p['sweep_track_us'], p['render_track_us']
+    return {'resource': 'latency: per-workgroup dependency chains (SSSP line-to-line sweep recurrence; '
+                        'render-track fp64 geometry + barrier-separated phases), one stack per CU',
+            'sweep_track_us': st['end'], 'sssp_rounds_us': st['rounds'], 'render_track_us': rt['end'],
+            'join_us': p['join_us'], 'distance_phase_us': p['distance_us']['all'],
+            'workgroup_total_us': p['total_us_median'], 'sssp_rounds': p['rounds']['median'],
+            'source': 'from_profile: %s (%s, stamp build, per-workgroup medians)' % (PHASE_PROFILE, p.get('tag'))}
+
+
 def rank_envs(rank, envs_per_rank, world=1, total_envs=None):
     """Env ids (= scene seeds) of one rank: a contiguous block of whole envs.
     Weak scaling (total_envs None): every rank renders envs_per_rank envs, the job world *
@@ -246,6 +273,7 @@ def main():
                 traffic_src = 'from_profile: profiles/pmc_traffic.json (%s, rocprofv3 PMC passes)' % t.get('tag')
         except (OSError, ValueError):
             traffic = None
+    binding = binding_note(args.config, b.N, args.layout)
     gather = None
     if args.gather and world > 1:
         gather = gather_states(out.cpu() if args.shared_gpu else out, args.gather, world, rank)
@@ -264,7 +292,7 @@ def main():
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'traffic_source': traffic_src,
                          'kernel': 'get_state_kernel', 'kernel_ms': kern_ms,
-                         'algorithmic_bytes_per_stack': B},
+                         'algorithmic_bytes_per_stack': B, 'binding': binding},
         }
         res['config'].update({'total_envs': args.total_envs} if strong else {'envs_per_gpu': args.envs})
         res['distributed'] = ranks

@@ -98,6 +98,20 @@ def test_rank_report_without_process_group():
     assert rep == {'world_size': 1, 'backend': None, 'ranks': [{'rank': 0, 'device': 'cpu'}], 'distinct_devices': 1}
 
 
+def test_binding_note_from_committed_stamps():
+    """The bench line's roofline.binding comes from the committed stamp profile of the BASELINE
+    config (one launch of 64 envs x 4 agents, CHW) and is left out for any other workload."""
+    sys.path.insert(0, ROOT)
+    import bench
+    note = bench.binding_note('lifting_4-small_divider', 256, 'chw')
+    assert note is not None and note['resource'].startswith('latency')
+    for k in ('sweep_track_us', 'sssp_rounds_us', 'render_track_us', 'join_us', 'distance_phase_us', 'workgroup_total_us'):
+        assert 0 < note[k] < 100, k
+    assert note['sssp_rounds_us'] < note['sweep_track_us'] < note['join_us'] < note['workgroup_total_us']
+    assert bench.binding_note('lifting_4-small_divider', 1024, 'chw') is None
+    assert bench.binding_note('pushing_4-large_empty', 256, 'chw') is None
+
+
 def test_rank_envs_partition():
     sys.path.insert(0, ROOT)
     import bench

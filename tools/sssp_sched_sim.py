@@ -36,6 +36,7 @@ S2 = np.float32(np.sqrt(2))
 ONE = np.float32(1)
 INF = np.float32(np.inf)
 DIRS = ('down', 'up', 'right', 'left')
+SKIP = None
 OPP = {'down': 'up', 'up': 'down', 'right': 'left', 'left': 'right'}
 
 
@@ -50,16 +51,19 @@ def relax_line(prev, cur, free_cur):
 class Sweep:
     """One wave's sweep of one direction over lines [first .. ] with the kernel's stop rule."""
 
-    def __init__(self, dist, free, name, lines):
+    def __init__(self, dist, free, name, lines, skip=None):
         self.dist, self.free, self.name = dist, free, name
+        self.skip = skip            # (min gap in steps, restart cycles): jump over clean gaps
+        self.restarts = 0
         H, W = free.shape
         self.vert = name in ('down', 'up')
         n = H if self.vert else W
         fwd = name in ('down', 'right')
         self.order = list(range(n)) if fwd else list(range(n - 1, -1, -1))
         pos = {l: i for i, l in enumerate(self.order)}
-        self.i = min(pos[l] for l in lines)
-        self.last = max(pos[l] for l in lines)
+        self.dirty = sorted(pos[l] for l in lines)
+        self.i = self.dirty[0]
+        self.last = self.dirty[-1]
         self.n = n
         self.quiet = 0
         self.steps = 0
@@ -90,14 +94,155 @@ class Sweep:
             self.quiet += 1
             if self.i - 1 >= self.last and self.quiet >= 4:
                 return False
+            if self.skip and self.quiet >= 4 and (self.steps % 4) == 0:
+                # a quiet group: every line up to the next dirty one is clean and unchanged by this
+                # sweep, so the sweep may restart there (a new prologue of line prefetches)
+                nd = next(p for p in self.dirty if p >= self.i)
+                if nd - self.i >= self.skip[0]:
+                    self.i = nd
+                    self.quiet = 0
+                    self.restarts += 1
+                    return self.skip[1]
         return True
 
 
-def run_round(dist, free, masks, cost, spec=False):
+class RowClose:
+    """Judge's round-3 proposal, modelled: a wave that closes whole rows over their straight
+    horizontal edges (a DPP min-plus scan left-to-right, then right-to-left, per row: the result of
+    the sequential relaxations, which this model applies; diagonals stay with the down / up sweeps).
+    One step = one row; its cost is the scan's issue cost (instructions x cycles), the rows being
+    independent."""
+
+    def __init__(self, dist, free, name, rows):
+        self.dist, self.free, self.name = dist, free, name
+        self.rows = sorted(rows)
+        self.k = 0
+        self.steps = 0
+        self.improved_lines = []
+
+    def step(self):
+        if self.k >= len(self.rows):
+            return False
+        r = self.rows[self.k]
+        self.k += 1
+        row, fr = self.dist[r].copy(), self.free[r]
+        W = len(row)
+        for j in range(1, W):
+            if fr[j] and row[j - 1] + ONE < row[j]:
+                row[j] = row[j - 1] + ONE
+        for j in range(W - 2, -1, -1):
+            if fr[j] and row[j + 1] + ONE < row[j]:
+                row[j] = row[j + 1] + ONE
+        imp = row < self.dist[r]
+        self.dist[r] = row
+        self.steps += 1
+        if imp.any():
+            self.improved_lines.append((r, np.nonzero(imp)[0]))
+        return True
+
+
+def simulate_rowscan(free, src, cost, c_barrier, c_row, waves=2):
+    """down / up sweeps (straight + both diagonals) beside `waves` row-closure waves; marks: a
+    vertical sweep's lowered rows -> the opposite sweep and the row closure; a closed row that
+    improved -> both vertical sweeps.  Ends after a round that improves nothing."""
+    H, W = free.shape
+    dist = np.full((H, W), INF, np.float32)
+    dist[src] = 0
+    vm = {'down': {src[0]}, 'up': {src[0]}}
+    rows = {src[0]}
+    total, rounds, steps = 0.0, 0, {'down': 0, 'up': 0, 'rows': 0}
+    cost = dict(cost)
+    while True:
+        rounds += 1
+        objs = {nm: Sweep(dist, free, nm, m) for nm, m in vm.items() if m}
+        rl = sorted(rows)
+        for q in range(waves):
+            part = rl[q::waves]
+            if part:
+                objs['rows%d' % q] = RowClose(dist, free, 'rows%d' % q, part)
+                cost['rows%d' % q] = c_row
+        heap = [(cost[nm], nm) for nm in objs]
+        heapq.heapify(heap)
+        t_end = 0.0
+        while heap:
+            t, nm = heapq.heappop(heap)
+            if objs[nm].step():
+                heapq.heappush(heap, (t + cost[nm], nm))
+            else:
+                t_end = max(t_end, t)
+        total += t_end + c_barrier
+        vm = {'down': set(), 'up': set()}
+        rows = set()
+        for nm, o in objs.items():
+            key = 'rows' if nm.startswith('rows') else nm
+            steps[key] = max(steps[key], 0) + o.steps if key != 'rows' else steps[key] + o.steps
+            for line, cells in o.improved_lines:
+                if nm.startswith('rows'):
+                    vm['down'].add(line)
+                    vm['up'].add(line)
+                else:
+                    vm[OPP[nm]].add(line)
+                    rows.add(line)
+        if not (vm['down'] or vm['up'] or rows):
+            break
+        if rounds > 400:
+            raise RuntimeError('no convergence')
+    return dist, total, rounds, steps
+
+
+def simulate_async(free, src, cost, c_start, c_poll):
+    """No rounds: each direction's wave sweeps again as soon as its own sweep ends (snapshot of its
+    dirty lines, c_start cycles of prologue), marking the others at the end of every sweep as the
+    round-3 kernel does; an idle wave notices new marks after c_poll cycles.  Done when no sweep
+    runs and every mask is empty (the same fixpoint: any schedule of exact relaxations reaches it)."""
+    H, W = free.shape
+    dist = np.full((H, W), INF, np.float32)
+    dist[src] = 0
+    masks = {'down': {src[0]}, 'up': {src[0]}, 'right': {src[1]}, 'left': {src[1]}}
+    running = {}
+    steps = {k: 0 for k in DIRS}
+    heap = []
+    for nm in DIRS:
+        heapq.heappush(heap, (c_start, nm))
+    idle = set()
+    t_end = 0.0
+    sweeps_run = 0
+    while heap:
+        t, nm = heapq.heappop(heap)
+        sw = running.get(nm)
+        if sw is None:
+            m = masks[nm]
+            if not m:
+                idle.add(nm)
+                continue
+            masks[nm] = set()
+            running[nm] = sw = Sweep(dist, free, nm, m)
+            sweeps_run += 1
+        if sw.step():
+            heapq.heappush(heap, (t + cost[nm], nm))
+            continue
+        # the sweep ended: its marks, then the next sweep of this wave
+        del running[nm]
+        steps[nm] += sw.steps
+        vert = nm in ('down', 'up')
+        pa, pb = ('right', 'left') if vert else ('down', 'up')
+        for line, cells in sw.improved_lines:
+            for tgt, val in ((OPP[nm], [line]), (pa, cells.tolist()), (pb, cells.tolist())):
+                masks[tgt].update(val)
+                if tgt in idle:
+                    idle.discard(tgt)
+                    heapq.heappush(heap, (t + c_poll, tgt))
+        t_end = max(t_end, t)
+        heapq.heappush(heap, (t + c_start, nm))
+    assert not any(masks.values()) and not running
+    return dist, t_end, sweeps_run, steps
+
+
+def run_round(dist, free, masks, cost, spec=False, skip=None):
     """The round's sweeps, interleaved by time: returns ({dir: Sweep}, round time in cycles).
     spec: a wave whose sweep ended while another's still runs sweeps its direction again over every
     line (speculative; it stops at the next group of 4 steps once the last real sweep ends)."""
-    sweeps = {nm: Sweep(dist, free, nm, m) for nm, m in masks.items() if m}
+    sweeps = {nm: Sweep(dist, free, nm, m, skip) for nm, m in masks.items() if m}
     H, W = free.shape
     heap = [(cost[nm], nm) for nm in sweeps]
     heapq.heapify(heap)
@@ -122,8 +267,9 @@ def run_round(dist, free, masks, cost, spec=False):
                 extra[nm] = Sweep(dist, free, nm, range(n))
             heapq.heappush(heap, (t + cost[nm], key))
             continue
-        if sweeps[nm].step():
-            heapq.heappush(heap, (t + cost[nm], nm))
+        r = sweeps[nm].step()
+        if r:
+            heapq.heappush(heap, (t + cost[nm] + (0 if r is True else r), nm))
         else:
             t_end = max(t_end, t)
             live.discard(nm)
@@ -175,12 +321,13 @@ def simulate(free, src, rule, cost, c_barrier, c_check):
     steps = {k: 0 for k in DIRS}
     while True:
         rounds += 1
-        sweeps, t = run_round(dist, free, masks, cost, spec=rule.endswith('spec'))
+        sweeps, t = run_round(dist, free, masks, cost, spec=rule.endswith('spec'),
+                              skip=SKIP if rule == 'marks_skip' else None)
         total += t + c_barrier
         per_round.append({nm: s.steps for nm, s in sweeps.items()})
         for nm, s in sweeps.items():
             steps[nm] += s.steps
-        if rule in ('marks', 'perp_final'):
+        if rule in ('marks', 'marks_skip', 'perp_final'):
             nxt = {k: set() for k in DIRS}
             any_imp = False
             for nm, s in sweeps.items():
@@ -188,7 +335,7 @@ def simulate(free, src, rule, cost, c_barrier, c_check):
                 pa, pb = ('right', 'left') if vert else ('down', 'up')
                 for line, cells in s.improved_lines:
                     any_imp = True
-                    if rule == 'marks':
+                    if rule in ('marks', 'marks_skip'):
                         nxt[OPP[nm]].add(line)
                     nxt[pa].update(cells.tolist())
                     nxt[pb].update(cells.tolist())
@@ -220,10 +367,19 @@ def main():
     ap.add_argument('--cpl1', type=float, default=100.0, help='cycles per 1-cell-per-lane step')
     ap.add_argument('--barrier', type=float, default=300.0, help='cycles per round barrier + masks')
     ap.add_argument('--check', type=float, default=1500.0, help='cycles per check pass + barrier')
+    ap.add_argument('--skip-gap', type=int, default=8, help='marks_skip: min clean gap (steps) to jump')
+    ap.add_argument('--restart', type=float, default=200.0, help='marks_skip: cycles per restart')
+    ap.add_argument('--row-instr', type=float, default=150.0,
+                    help='rowscan: instructions per row closure (both scan directions, fast path only)')
+    ap.add_argument('--poll', type=float, default=150.0, help='async: cycles for an idle wave to see new marks')
+    ap.add_argument('--instr-cycles', type=float, default=6.1, help='issue cycles per instruction')
     args = ap.parse_args()
+    global SKIP
+    SKIP = (args.skip_gap, args.restart)
     import oracle
     from simaps import synthetic
-    res = {r: [] for r in ('marks', 'check', 'check_both', 'check_spec', 'perp_final')}
+    res = {r: [] for r in ('marks', 'marks_skip', 'check', 'check_both', 'check_spec', 'perp_final', 'rowscan',
+                           'async')}
     detail = {r: [] for r in res}
     for e in range(args.envs):
         sc = synthetic.make_scene(args.config, e)
@@ -244,6 +400,21 @@ def main():
             for s in srcs:
                 ref = oracle.spfa_image(ao.cspace, s)[i0:i1, j0:j1]
                 for rule in res:
+                    if rule == 'async':
+                        d, t, r, st = simulate_async(free, (s[0] - i0, s[1] - j0), cost, args.restart, args.poll)
+                        d = np.where(np.isinf(d), np.float32(-1), d)
+                        assert np.array_equal(np.where(free, d, 0), np.where(free, ref, 0)), (e, a, rule)
+                        per_agent[rule] = max(per_agent[rule], t)
+                        detail[rule].append({'rounds': r, 'cycles': t, 'steps': st})
+                        continue
+                    if rule == 'rowscan':
+                        d, t, r, st = simulate_rowscan(free, (s[0] - i0, s[1] - j0), cost, args.barrier,
+                                                       args.row_instr * args.instr_cycles)
+                        d = np.where(np.isinf(d), np.float32(-1), d)
+                        assert np.array_equal(np.where(free, d, 0), np.where(free, ref, 0)), (e, a, rule)
+                        per_agent[rule] = max(per_agent[rule], t)
+                        detail[rule].append({'rounds': r, 'cycles': t, 'steps': st})
+                        continue
                     d, t, r, pr, st = simulate(free, (s[0] - i0, s[1] - j0), rule, cost, args.barrier, args.check)
                     d = np.where(np.isinf(d), np.float32(-1), d)
                     assert np.array_equal(np.where(free, d, 0), np.where(free, ref, 0)), (e, a, rule)
@@ -258,8 +429,9 @@ def main():
         out[rule] = {'cycles_median': float(np.median(v)), 'cycles_max': float(v.max()),
                      'cycles_p90': float(np.percentile(v, 90)),
                      'rounds_median': float(np.median([d['rounds'] for d in detail[rule]])),
-                     'steps_median': {k: float(np.median([d['steps'][k] for d in detail[rule]])) for k in DIRS}}
-    for rule in ('check', 'check_both', 'check_spec', 'perp_final'):
+                     'steps_median': {k: float(np.median([d['steps'][k] for d in detail[rule]]))
+                                      for k in detail[rule][0]['steps']}}
+    for rule in ('marks_skip', 'check', 'check_both', 'check_spec', 'perp_final', 'rowscan', 'async'):
         out[rule + '_vs_marks_median'] = out[rule]['cycles_median'] / out['marks']['cycles_median']
         out[rule + '_vs_marks_max'] = out[rule]['cycles_max'] / out['marks']['cycles_max']
     print(json.dumps(out))
