@@ -2866,6 +2866,9 @@ __device__ __forceinline__ bool line_free(const SH &sh, const SsspScratch &S, in
 #ifndef SIMAPS_POP_CAP  // the diagnostic build (tests/test_gpu_faults.py) lowers it to exercise the fault path
 #define SIMAPS_POP_CAP (1 << 24)
 #endif
+#ifndef SIMAPS_SPFA_PIPE  // the round-4 software-pipelined pop (0: the round-3 pop, for A/B builds)
+#define SIMAPS_SPFA_PIPE 1
+#endif
 #ifndef SIMAPS_SPFA_RING  // > 0: the diagnostic ring build (tests/test_gpu_faults.py) -- a queue ring of at most
 #define SIMAPS_SPFA_RING 0  // this many slots, so that the ring wraps many times per query (the product's
 #endif                      // ring has one slot per cell and rarely wraps); a live queue past it is a fault
@@ -2904,6 +2907,123 @@ __device__ __forceinline__ int dir_off(int k, int pw)
     const int di = k < 2 ? 0 : (k < 5 ? -1 : 1);
     const int dj = k < 2 ? (k == 0 ? -1 : 1) : ((k - 2) % 3) - 1;
     return di * pw + dj;
+}
+
+#ifndef SIMAPS_SPFA_ASM  // the common pops as one inline-asm loop (0: the C++ pop alone, for A/B builds)
+#define SIMAPS_SPFA_ASM 1
+#endif
+// The common SPFA pop (shortest_paths.pyx:89-107) as one inline-asm loop (round 4).  The C++ pop in
+// path_core costs ~85 instructions with the compiler's exec juggling and register copies; this one
+// ~50.  The next pop's LDS reads are issued right after this pop's writes, so their latency overlaps
+// the bookkeeping and the next pop's checks; the improved heads and u's own pin byte go out as one
+// write per array (lane 8 -- doff 0, the popped vertex -- rewrites its unchanged distance), not as a
+// same-address write from every lane.  The loop runs pops while each is "common": the queue keeps
+// >= 3 entries after the pop, no pushed distance is below the front's (no SLF swap, pyx:104-107),
+// the pop does not lower the front's distance, and neither the tail nor the read-ahead slot reaches
+// the ring's end (no slot wraps).  Then the pushes go to the tail in edge order, slot = tail + rank
+// among the pushed edges, and the next front / second are the current second / third.  It returns
+// when `left` reaches 0 or when the pop at hand is not common -- before any of that pop's writes,
+// with its reads (vv / dv / pv / dF0 / pth, issued one pop ahead, as path_core's pf_* values)
+// complete -- so that the C++ pop replays that one exactly.  State as in path_core: u the front, F0
+// the second, qn the slot of F0, qt the tail slot, cnt the live entries including u.  DIST / QUEUE /
+// PIN: the byte offsets of the LDS arrays (checked by the caller).
+// Wait states: a VALU SGPR write is read by a VALU >= 2 instructions later (du); the opening s_nop
+// covers the compiler's last writes of the inputs.  The wave's LDS operations complete in order, so
+// one lgkmcnt(0) before each pop waits for the read-ahead and everything before it.
+template <int DIST, int QUEUE, int PIN>
+__device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt, int &cnt, int &left, int ring,
+                                               int &vv, float &dv, int &pv, float &dF0, int &pth, int doff, float wl,
+                                               int pbits)
+{
+    static_assert(PIN + 255 < 65536 && QUEUE + 4 < 65536, "ds offsets are 16-bit");
+    const uint64_t l8 = 1ull << 8;  // lane 8: the popped vertex itself (doff 0)
+    // Pops the loop may run without a ring wrap: the tail grows by <= 8 per pop and must stay within
+    // ring - 8 (qt + 8 <= ring), the read-ahead slot by 1 and must stay within ring - 3 (qn + 3 <=
+    // ring); and at most `left`.  With no wrap the live entries are cnt = qt - qn + 1, so cnt is not
+    // carried (the loop needs cnt >= 4, i.e. qt - qn >= 3, for the read-ahead slots to be live).
+    int bud = min(left, min((ring - 8 - qt) >> 3, ring - 3 - qn));
+    const int bud0 = bud;
+    uint64_t ex, nq, fm, im, sw;
+    int du, th, t;
+    float nd;
+    int ta, tb, tc, td;
+    if (bud > 0 && cnt >= 4 && qt >= qn) {  // (qt < qn: the live entries wrap the ring; the C++ pop runs)
+        int tq = 2 * qn;  // byte offset of slot qn in the queue (the read-ahead slot is qn + 2)
+        asm volatile(
+            "s_nop 1\n\t"
+            "s_mov_b64 %[ex], exec\n\t"
+            "v_mov_b32_e32 %[tc], %[tq]\n"
+            "1:\n\t"
+            "v_readlane_b32 %[du], %[dv], 8\n\t"
+            "v_readfirstlane_b32 %[th], %[pth]\n\t"
+            "v_cmp_gt_u32_e64 %[nq], 16, %[pv]\n\t"
+            "v_and_b32_e32 %[tb], 15, %[pv]\n\t"
+            "v_add_f32_e32 %[nd], %[du], %[wl]\n\t"
+            "v_cmp_eq_u32_e64 %[fm], %[F0], %[vv]\n\t"
+            "v_cmp_lt_f32_e64 %[im], %[nd], %[dv]\n\t"
+            "v_cmp_lt_f32_e64 %[sw], %[nd], %[dF0]\n\t"
+            // lane 8 writes u's own cells: its distance unchanged, its pin byte without the queued bit (pyx:92)
+            "v_cndmask_b32_e64 %[tb], %[pbits], %[tb], %[l8]\n\t"
+            "v_cndmask_b32_e64 %[td], %[nd], %[dv], %[l8]\n\t"
+            "v_lshlrev_b32_e32 %[ta], 2, %[vv]\n\t"
+            "s_and_b64 %[nq], %[nq], %[im]\n\t"
+            "s_and_b64 %[fm], %[fm], %[im]\n\t"
+            "s_and_b64 %[sw], %[sw], %[nq]\n\t"
+            "s_or_b64 %[sw], %[sw], %[fm]\n\t"
+            "s_cmp_lg_u64 %[sw], 0\n\t"
+            "s_cbranch_scc1 9f\n\t"
+            // commit: the improved heads (pyx:97-99) and u's pin byte, then the pushes (pyx:100-103)
+            "s_or_b64 exec, %[im], %[l8]\n\t"
+            "ds_write_b32 %[ta], %[td] offset:%c[DIST]\n\t"
+            "ds_write_b8 %[vv], %[tb] offset:%c[PIN]\n\t"
+            "s_cmp_eq_u64 %[nq], 0\n\t"
+            "s_cbranch_scc1 2f\n\t"
+            "s_mov_b64 exec, %[nq]\n\t"
+            "s_mov_b64 vcc, %[nq]\n\t"
+            "v_mbcnt_lo_u32_b32 %[td], vcc_lo, 0\n\t"
+            "v_add_u32_e32 %[td], %[qt], %[td]\n\t"
+            "v_lshlrev_b32_e32 %[td], 1, %[td]\n\t"
+            "ds_write_b16 %[td], %[vv] offset:%c[QUEUE]\n"
+            "2:\n\t"
+            "s_mov_b64 exec, %[ex]\n\t"
+            // the next pop's reads: front F0 (its edge heads and itself), second th's distance, the
+            // third entry (slot qn + 2)
+            "v_add_u32_e32 %[vv], %[F0], %[doff]\n\t"
+            "v_lshlrev_b32_e32 %[tb], 2, %[pth]\n\t"
+            "v_lshlrev_b32_e32 %[ta], 2, %[vv]\n\t"
+            "ds_read_b32 %[dF0], %[tb] offset:%c[DIST]\n\t"
+            "ds_read_u16 %[pth], %[tc] offset:%c[QUEUE4]\n\t"
+            "ds_read_b32 %[dv], %[ta] offset:%c[DIST]\n\t"
+            "ds_read_u8 %[pv], %[vv] offset:%c[PIN]\n\t"
+            // bookkeeping and the next pop's checks while the reads are in flight
+            "s_bcnt1_i32_b64 %[t], %[nq]\n\t"
+            "s_add_u32 %[qt], %[qt], %[t]\n\t"
+            "s_add_u32 %[qn], %[qn], 1\n\t"
+            "v_add_u32_e32 %[tc], 2, %[tc]\n\t"
+            "s_mov_b32 %[u], %[F0]\n\t"
+            "s_mov_b32 %[F0], %[th]\n\t"
+            "s_sub_u32 %[bud], %[bud], 1\n\t"
+            "s_cmp_le_i32 %[bud], 0\n\t"
+            "s_cbranch_scc1 8f\n\t"
+            "s_sub_u32 %[t], %[qt], %[qn]\n\t"
+            "s_cmp_lt_i32 %[t], 3\n\t"
+            "s_cbranch_scc1 8f\n\t"
+            "s_waitcnt lgkmcnt(0)\n\t"
+            "s_branch 1b\n"
+            "8:\n\t"
+            "s_waitcnt lgkmcnt(0)\n"
+            "9:\n\t"
+            : [u] "+s"(u), [F0] "+s"(F0), [qn] "+s"(qn), [qt] "+s"(qt), [bud] "+s"(bud),
+              [vv] "+v"(vv), [dv] "+v"(dv), [pv] "+v"(pv), [dF0] "+v"(dF0), [pth] "+v"(pth),
+              [ex] "=&s"(ex), [nq] "=&s"(nq), [fm] "=&s"(fm), [im] "=&s"(im), [sw] "=&s"(sw), [du] "=&s"(du),
+              [th] "=&s"(th), [t] "=&s"(t), [nd] "=&v"(nd), [ta] "=&v"(ta), [tb] "=&v"(tb), [tc] "=&v"(tc),
+              [td] "=&v"(td)
+            : [tq] "s"(tq), [l8] "s"(l8), [doff] "v"(doff), [wl] "v"(wl), [pbits] "v"(pbits), [DIST] "i"(DIST),
+              [QUEUE] "i"(QUEUE), [QUEUE4] "i"(QUEUE + 4), [PIN] "i"(PIN)
+            : "memory", "scc", "vcc");
+        left -= bud0 - bud;
+        cnt = qt - qn + 1;
+    }
 }
 
 // Steps (3)-(6) of the movement path on the LDS-resident free bits (S.freeb) between the cells
@@ -3016,12 +3136,138 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         const float finT = EARLY ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh.finT))) : 0.0f;
         // an unreachable target (fixpoint +inf) never gets a parent: the SPFA cannot change the path
         if (EARLY && finT == INFINITY) count = 0, early = true;
+#if SIMAPS_SPFA_PIPE
+        // the reads of the next pop, issued one pop ahead: its vertex's 8 edge heads and itself
+        // (lane 8), the distance of the entry after it (the SLF front during that pop) and the slot
+        // after that one
+        int pf_v = 0, pf_pv = 0, pf_third = 0;
+        float pf_dv = 0.0f, pf_dF0 = 0.0f;
+        auto pf_issue = [&](int fr, int sc, int slot) {
+            pf_v = fr + doff;
+            pf_dv = Ld[pf_v];
+            pf_pv = Li[pf_v];
+            pf_dF0 = Ld[sc];
+            pf_third = Lq[slot];
+        };
+        pf_issue(front, second, qn + 1 == ring ? 0 : qn + 1);
+        // the asm pop addresses the LDS arrays by their compile-time offsets in the kernel's LDS block
+        const bool asm_ok = (uint32_t)(uintptr_t)Ld == (uint32_t)OFF_PA && (uint32_t)(uintptr_t)Lq == (uint32_t)(OFF_PA + 4 * CELLS) &&
+                            (uint32_t)(uintptr_t)Li == (uint32_t)(OFF_PA + 6 * CELLS);
+#endif
         // pop rounds (inner loop: one exit, so the common pop ends in one compare) up to `lim`, then
         // (EARLY) an early-exit check
         if (count > 0)
             for (;;) {
                 int left = lim - pops;  // pops of this round (the common pop's one exit test: min(count, left))
                 for (;;) {
+#if SIMAPS_SPFA_PIPE && SIMAPS_SPFA_ASM
+                    if (asm_ok) {  // the common pops in one asm loop; it returns at `left` = 0 or an uncommon pop
+                        int fs = __builtin_amdgcn_readfirstlane(front), ss = __builtin_amdgcn_readfirstlane(second);
+                        spfa_fast_pops<OFF_PA, OFF_PA + 4 * CELLS, OFF_PA + 6 * CELLS>(
+                            fs, ss, qn, qt, count, left, ring, pf_v, pf_dv, pf_pv, pf_dF0, pf_third, doff, wl, (int)pbits);
+                        front = fs;
+                        second = ss;
+                        if (left <= 0) break;
+                    }
+#endif
+#if SIMAPS_SPFA_PIPE
+                    {
+                    // The pop, software-pipelined (round 4).  Its LDS reads -- the popped vertex's 8 edge
+                    // heads and itself, the next front's distance, the slot after it -- were issued at the
+                    // end of the previous pop, right after that pop's writes, so their latency overlaps
+                    // that pop's queue bookkeeping.  The common pop (the SLF swap of pyx:104-107 happens in
+                    // ~0.4 % of pops) is lane-parallel: with no pushed distance below the front's, the
+                    // pushes go to the tail in edge order (slot = tail + rank among the pushed edges), so
+                    // the next front is known (second) and its reads can be issued at once.  Every other
+                    // pop -- a possible swap, the front lowered by this pop (its distance changes between
+                    // edges), or a queue of <= 2 entries (the slots read ahead may be written by this
+                    // pop's pushes) -- replays the pushes with an SALU loop over the edge bits in edge
+                    // order, the front's distance in an SGPR.  Distances here are >= 0 or INFR (blocked
+                    // cells hold -inf and are never relaxed or pushed), so float order is unsigned order
+                    // and the SLF test is one s_cmp.  Masks are 32-bit: only lanes 0..7 carry edges.
+                    const int u = __builtin_amdgcn_readfirstlane(front);
+                    qh = qn;
+                    count--;
+                    const int F0 = __builtin_amdgcn_readfirstlane(second);
+                    const int q2 = qh + 1 == ring ? 0 : qh + 1;
+                    qn = q2;
+                    const int v = pf_v;
+                    const float dv = pf_dv, dF0 = pf_dF0;
+                    const int pv = pf_pv;
+                    const float du = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), 8));
+                    const float nd = du + wl;
+                    const bool better = nd < dv;
+                    const uint32_t imp = (uint32_t)__builtin_amdgcn_ballot_w64(better);
+                    const uint32_t push = imp & (uint32_t)__builtin_amdgcn_ballot_w64(pv < 16);
+                    const int pu = __builtin_amdgcn_readlane(pv, 8) & 0xf;  // u leaves the queue (pyx:92)
+                    const int th = __builtin_amdgcn_readfirstlane(pf_third);
+                    const uint32_t odd = ((uint32_t)__builtin_amdgcn_ballot_w64(v == F0) & imp) |
+                                         ((uint32_t)__builtin_amdgcn_ballot_w64(nd < dF0) & push);
+                    if (count >= 3 && odd == 0u) {
+                        Li[u] = (uint8_t)pu;
+                        if (better) { Ld[v] = nd; Li[v] = pbits; }
+                        if (push) {
+                            const int rank = (int)__builtin_amdgcn_mbcnt_lo(push, 0u);
+                            int slot = qt + rank;
+                            slot = slot >= ring ? slot - ring : slot;
+                            if ((push >> lane) & 1u) Lq[slot] = (uint16_t)v;
+                            qt += __builtin_popcount(push);
+                            qt = qt >= ring ? qt - ring : qt;
+                            count += __builtin_popcount(push);
+                        }
+                        front = F0;
+                        second = th;
+                        pf_issue(F0, th, q2 + 1 == ring ? 0 : q2 + 1);
+                    } else {
+                        Li[u] = (uint8_t)pu;
+                        int nf = F0, nsecond = th;
+                        if (imp) {
+                            if (better) { Ld[v] = nd; Li[v] = pbits; }
+                            if (push) {
+                                // F0 (queued, so never pushed) lowered by edge k: later pushes compare with its
+                                // new distance while it is still the front.  With an empty queue F0 is stale.
+                                const uint32_t fm = count > 0 ? (uint32_t)__builtin_amdgcn_ballot_w64(v == F0) & imp : 0u;
+                                uint32_t todo = push | fm;
+                                int fr = count > 0 ? F0 : -1;  // the front after the pop (-1: the queue is empty)
+                                uint32_t dfr = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(dF0));
+                                do {
+                                    const int k = __builtin_ctz(todo);
+                                    todo &= todo - 1;
+                                    const int vk = __builtin_amdgcn_readlane(v, k);
+                                    const uint32_t ndk = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(nd), k);
+                                    if ((fm >> k) & 1u) {
+                                        if (fr == F0) dfr = ndk;
+                                        continue;
+                                    }
+                                    int content = vk;
+                                    if (fr < 0) {  // the first push into an empty queue is the front (qh == qt)
+                                        fr = vk;
+                                        dfr = ndk;
+                                    } else if (ndk < dfr) {  // SLF: swap with the front (pyx:104-107)
+                                        content = fr;
+                                        Lq[qh] = (uint16_t)vk;
+                                        fr = vk;
+                                        dfr = ndk;
+                                    }
+                                    Lq[qt] = (uint16_t)content;
+                                    nsecond = qt == q2 ? content : nsecond;  // the slot after the front was empty
+                                    qt = qt + 1 == ring ? 0 : qt + 1;
+                                    count++;
+                                } while (todo);
+                                nf = fr;
+                            }
+                        }
+                        front = nf;
+                        second = nsecond;
+                        pf_issue(nf, nsecond, q2 + 1 == ring ? 0 : q2 + 1);
+                    }
+                    --left;
+                    if constexpr (SIMAPS_SPFA_RING > 0)
+                        if (count > ring && lane == 0) sh.fault |= SIMAPS_FAULT_ROUNDS;  // (diagnostic ring overflowed)
+                    if (min(count, left) <= 0) break;
+                    continue;
+                    }
+#endif
                     // (front / second are wave-uniform: keep them in SGPRs across the loop)
                     const int u = __builtin_amdgcn_readfirstlane(front);
                     qh = qn;
