@@ -196,6 +196,15 @@ class VectorEnvObservations:
         return paths
 
 
+MAX_WINDOW_CELLS, MAX_WINDOW_W = 9024, 120  # SIMAPS_MAX_ROOM_CELLS / SIMAPS_MAX_ROOM_W (include/simaps.h)
+
+
+def window_fits(h, w):
+    """Whether an h x w window of free cells fits the LDS-resident SSSP / SPFA kernels (the checks of
+    simaps_sssp_grid / simaps_grid_path)."""
+    return h >= 1 and 1 <= w <= MAX_WINDOW_W and (h + 2) * ((w + 2) | 1) <= MAX_WINDOW_CELLS
+
+
 class GridGraph:
     """shortest_paths.pyx GridGraph (pyx:10-167) on the device: 8-connected grid over cells with
     grid != 0, weights 1 / float32(sqrt(2)), float32 distances, unreachable -> -1.
@@ -217,6 +226,11 @@ class GridGraph:
             self.window = (i0, j0, i1 - i0 + 1, j1 - j0 + 1)
         else:
             self.window = (0, 0, 1, 1)
+        if not window_fits(self.window[2], self.window[3]):
+            raise ValueError('GridGraph: the free cells span a %d x %d window; the LDS-resident SSSP / SPFA take '
+                             'windows with (h + 2) * ((w + 2) | 1) <= %d cells and w <= %d (include/simaps.h; every '
+                             'reference call site passes a room cspace, which fits)'
+                             % (self.window[2], self.window[3], MAX_WINDOW_CELLS, MAX_WINDOW_W))
         self._cache = {}
 
     def _check_source(self, source):
@@ -265,4 +279,4 @@ class GridGraph:
         return float(self.shortest_path_images([source])[0][i, j])
 
 
-__all__ = ['VectorEnvObservations', 'GridGraph', 'robot_groups']
+__all__ = ['VectorEnvObservations', 'GridGraph', 'robot_groups', 'window_fits']

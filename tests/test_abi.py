@@ -143,3 +143,19 @@ def test_path_mode_setter():
         assert L.simaps_path_mode(0) == 0  # unchanged by the refused calls
     finally:
         L.simaps_path_mode(prev)
+
+
+def test_gridgraph_window_limits_match_header():
+    """The drop-in GridGraph refuses, up front, a grid whose free cells exceed the LDS window limits of
+    include/simaps.h (SIMAPS_MAX_ROOM_CELLS / SIMAPS_MAX_ROOM_W), with the same rule the ABI applies."""
+    from simaps import vector_env
+    txt = open(HEADER).read()
+    cells = int(re.search(r'#define SIMAPS_MAX_ROOM_CELLS (\d+)', txt).group(1))
+    maxw = int(re.search(r'#define SIMAPS_MAX_ROOM_W (\d+)', txt).group(1))
+    assert (vector_env.MAX_WINDOW_CELLS, vector_env.MAX_WINDOW_W) == (cells, maxw)
+    fits = vector_env.window_fits
+    assert fits(44, 92) and fits(92, 92) and fits(1, 1)            # small / large rooms, one cell
+    assert not fits(93, 93) and not fits(40, 121) and not fits(0, 5)
+    for h in range(1, 200, 7):
+        for w in range(1, 130, 3):
+            assert fits(h, w) == (w <= maxw and (h + 2) * ((w + 2) | 1) <= cells)
