@@ -2931,98 +2931,146 @@ __device__ __forceinline__ int dir_off(int k, int pw)
 // covers the compiler's last writes of the inputs.  The wave's LDS operations complete in order, so
 // one lgkmcnt(0) before each pop waits for the read-ahead and everything before it.
 template <int DIST, int QUEUE, int PIN>
-__device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt, int &cnt, int &left, int ring,
-                                               int &vv, float &dv, int &pv, float &dF0, int &pth, int doff, float wl,
-                                               int pbits)
+__device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt, int &cnt, int &left, int &lim_add,
+                                               int ring, int &vv, float &dv, int &pv, float &dF0, int &pth, int doff,
+                                               float wl, int pbits, int tchk, int tv, float finT)
 {
     static_assert(PIN + 255 < 65536 && QUEUE + 4 < 65536, "ds offsets are 16-bit");
     const uint64_t l8 = 1ull << 8;  // lane 8: the popped vertex itself (doff 0)
-    // Pops the loop may run without a ring wrap: the tail grows by <= 8 per pop and must stay within
-    // ring - 8 (qt + 8 <= ring), the read-ahead slot by 1 and must stay within ring - 3 (qn + 3 <=
-    // ring); and at most `left`.  With no wrap the live entries are cnt = qt - qn + 1, so cnt is not
-    // carried (the loop needs cnt >= 4, i.e. qt - qn >= 3, for the read-ahead slots to be live).
-    int bud = min(left, min((ring - 8 - qt) >> 3, ring - 3 - qn));
-    const int bud0 = bud;
+    // Pops the loop may run with no per-pop test but its budget: no ring wrap (the tail grows by <= 8
+    // per pop and stays within ring - 8, the read-ahead slot by 1 and stays within ring - 3), >= 4
+    // live entries before every pop (the count drops by <= 1 per pop: budget cnt - 3) and at most
+    // `left`.  qn grows by exactly 1 per pop and u is lane 8's edge head of the read-ahead, so
+    // neither is carried; with no wrap the live entries are cnt = qt - qn + 1.
+    // The budget is run in segments of min(left, what remains of it) pops.  When a segment ends at
+    // `left` = 0 and tchk is set (the early-exit mode, target not yet at its fixpoint distance), the
+    // loop itself makes path_core's 32-pop check -- one LDS read of the target's distance -- and
+    // either returns (the target is final: path_core walks its chain) or runs the next 32 pops
+    // (lim_add counts those, so path_core's pop accounting `pops = lim - left` still holds).
+    int gb = __builtin_amdgcn_readfirstlane(min(cnt - 3, min((ring - 8 - qt) >> 3, ring - 3 - qn)));
+    const int gb0 = gb;
+    int seg = __builtin_amdgcn_readfirstlane(min(left, gb)), bud = seg, lft = __builtin_amdgcn_readfirstlane(left), ladd = 0;
+    // the target's byte offset in the distance array, or -1: no target checks in the loop
+    const int tv4 = __builtin_amdgcn_readfirstlane(tchk ? 4 * tv : -1);
+    const uint32_t fin = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(finT));
     uint64_t ex, nq, fm, im, sw;
     int du, th, t;
     float nd;
     int ta, tb, tc, td;
-    if (bud > 0 && cnt >= 4 && qt >= qn) {  // (qt < qn: the live entries wrap the ring; the C++ pop runs)
+    if (seg > 0 && qt >= qn) {  // (qt < qn: the live entries wrap the ring; the C++ pop runs)
         int tq = 2 * qn;  // byte offset of slot qn in the queue (the read-ahead slot is qn + 2)
+        // two pops per iteration with the second's registers swapped (no copy of the next second into
+        // F0, one branch and one read-ahead slot increment per two pops)
+#define FP_POP(A, B, QOFF, L9, L8, LS)                                                              \
+            "v_readlane_b32 %[du], %[dv], 8\n\t"                                                   \
+            "v_readfirstlane_b32 " B ", %[pth]\n\t"                                                \
+            "v_cmp_gt_u32_e64 %[nq], 16, %[pv]\n\t"                                                \
+            "v_and_b32_e32 %[tb], 15, %[pv]\n\t"                                                   \
+            "v_add_f32_e32 %[nd], %[du], %[wl]\n\t"                                                \
+            "v_cmp_eq_u32_e64 %[fm], " A ", %[vv]\n\t"                                             \
+            "v_cmp_lt_f32_e64 %[im], %[nd], %[dv]\n\t"                                             \
+            "v_cmp_lt_f32_e64 %[sw], %[nd], %[dF0]\n\t"                                            \
+            "v_cndmask_b32_e64 %[tb], %[pbits], %[tb], %[l8]\n\t"                                  \
+            "v_cndmask_b32_e64 %[td], %[nd], %[dv], %[l8]\n\t"                                     \
+            "v_lshlrev_b32_e32 %[ta], 2, %[vv]\n\t"                                                \
+            "s_and_b64 %[nq], %[nq], %[im]\n\t"                                                    \
+            "s_and_b64 %[fm], %[fm], %[im]\n\t"                                                    \
+            "s_and_b64 %[sw], %[sw], %[nq]\n\t"                                                    \
+            "s_or_b64 %[sw], %[sw], %[fm]\n\t"                                                     \
+            "s_cmp_lg_u64 %[sw], 0\n\t"                                                            \
+            "s_cbranch_scc1 " L9 "\n\t"                                                            \
+            "s_or_b64 exec, %[im], %[l8]\n\t"                                                      \
+            "ds_write_b32 %[ta], %[td] offset:%c[DIST]\n\t"                                        \
+            "ds_write_b8 %[vv], %[tb] offset:%c[PIN]\n\t"                                          \
+            "s_cmp_eq_u64 %[nq], 0\n\t"                                                            \
+            "s_cbranch_scc1 " LS "f\n\t"                                                                 \
+            "s_mov_b64 exec, %[nq]\n\t"                                                            \
+            "s_mov_b64 vcc, %[nq]\n\t"                                                             \
+            "v_mbcnt_lo_u32_b32 %[td], vcc_lo, 0\n\t"                                              \
+            "v_add_u32_e32 %[td], %[qt], %[td]\n\t"                                                \
+            "v_lshlrev_b32_e32 %[td], 1, %[td]\n\t"                                                \
+            "ds_write_b16 %[td], %[vv] offset:%c[QUEUE]\n"                                         \
+            LS ":\n\t"                                                                             \
+            "s_mov_b64 exec, %[ex]\n\t"                                                            \
+            "v_add_u32_e32 %[vv], " A ", %[doff]\n\t"                                              \
+            "v_lshlrev_b32_e32 %[tb], 2, %[pth]\n\t"                                               \
+            "v_lshlrev_b32_e32 %[ta], 2, %[vv]\n\t"                                                \
+            "ds_read_b32 %[dF0], %[tb] offset:%c[DIST]\n\t"                                        \
+            "ds_read_u16 %[pth], %[tc] offset:%c[" QOFF "]\n\t"                                    \
+            "ds_read_b32 %[dv], %[ta] offset:%c[DIST]\n\t"                                         \
+            "ds_read_u8 %[pv], %[vv] offset:%c[PIN]\n\t"                                           \
+            "s_bcnt1_i32_b64 %[t], %[nq]\n\t"                                                      \
+            "s_add_u32 %[qt], %[qt], %[t]\n\t"                                                     \
+            "s_sub_u32 %[bud], %[bud], 1\n\t"                                                      \
+            "s_cmp_le_i32 %[bud], 0\n\t"                                                           \
+            "s_cbranch_scc1 " L8 "\n\t"                                                            \
+            "s_waitcnt lgkmcnt(0)\n\t"
+        // At a segment's end (its last pop's reads issued): account the segment, wait for the reads, and
+        // leave unless it ended at `left` = 0 with target checks on; then check the target (leave if
+        // it is final) and run the next 32 pops after FIX (the register fix-up for the iteration half).
+#define FP_REFILL(FIX, LEXIT)                                                                      \
+            "s_sub_u32 %[gb], %[gb], %[seg]\n\t"                                                   \
+            "s_sub_u32 %[lft], %[lft], %[seg]\n\t"                                                 \
+            "s_mov_b32 %[seg], 0\n\t"                                                             \
+            "s_waitcnt lgkmcnt(0)\n\t"                                                             \
+            "s_cmp_le_i32 %[gb], 0\n\t"                                                            \
+            "s_cbranch_scc1 " LEXIT "\n\t"                                                         \
+            "s_cmp_eq_u32 %[tv4], -1\n\t"                                                          \
+            "s_cbranch_scc1 " LEXIT "\n\t"                                                         \
+            "s_cmp_gt_i32 %[lft], 0\n\t"                                                           \
+            "s_cbranch_scc1 " LEXIT "\n\t"                                                         \
+            "v_mov_b32_e32 %[ta], %[tv4]\n\t"                                                      \
+            "ds_read_b32 %[td], %[ta] offset:%c[DIST]\n\t"                                         \
+            "s_waitcnt lgkmcnt(0)\n\t"                                                             \
+            "v_readfirstlane_b32 %[t], %[td]\n\t"                                                  \
+            "s_cmp_eq_u32 %[t], %[fin]\n\t"                                                        \
+            "s_cbranch_scc1 " LEXIT "\n\t"                                                         \
+            "s_add_u32 %[ladd], %[ladd], 32\n\t"                                                   \
+            "s_mov_b32 %[lft], 32\n\t"                                                             \
+            "s_min_u32 %[seg], %[gb], 32\n\t"                                                      \
+            "s_mov_b32 %[bud], %[seg]\n\t"                                                         \
+            FIX                                                                                    \
+            "s_branch 1b\n"
         asm volatile(
             "s_nop 1\n\t"
             "s_mov_b64 %[ex], exec\n\t"
             "v_mov_b32_e32 %[tc], %[tq]\n"
             "1:\n\t"
-            "v_readlane_b32 %[du], %[dv], 8\n\t"
-            "v_readfirstlane_b32 %[th], %[pth]\n\t"
-            "v_cmp_gt_u32_e64 %[nq], 16, %[pv]\n\t"
-            "v_and_b32_e32 %[tb], 15, %[pv]\n\t"
-            "v_add_f32_e32 %[nd], %[du], %[wl]\n\t"
-            "v_cmp_eq_u32_e64 %[fm], %[F0], %[vv]\n\t"
-            "v_cmp_lt_f32_e64 %[im], %[nd], %[dv]\n\t"
-            "v_cmp_lt_f32_e64 %[sw], %[nd], %[dF0]\n\t"
-            // lane 8 writes u's own cells: its distance unchanged, its pin byte without the queued bit (pyx:92)
-            "v_cndmask_b32_e64 %[tb], %[pbits], %[tb], %[l8]\n\t"
-            "v_cndmask_b32_e64 %[td], %[nd], %[dv], %[l8]\n\t"
-            "v_lshlrev_b32_e32 %[ta], 2, %[vv]\n\t"
-            "s_and_b64 %[nq], %[nq], %[im]\n\t"
-            "s_and_b64 %[fm], %[fm], %[im]\n\t"
-            "s_and_b64 %[sw], %[sw], %[nq]\n\t"
-            "s_or_b64 %[sw], %[sw], %[fm]\n\t"
-            "s_cmp_lg_u64 %[sw], 0\n\t"
-            "s_cbranch_scc1 9f\n\t"
-            // commit: the improved heads (pyx:97-99) and u's pin byte, then the pushes (pyx:100-103)
-            "s_or_b64 exec, %[im], %[l8]\n\t"
-            "ds_write_b32 %[ta], %[td] offset:%c[DIST]\n\t"
-            "ds_write_b8 %[vv], %[tb] offset:%c[PIN]\n\t"
-            "s_cmp_eq_u64 %[nq], 0\n\t"
-            "s_cbranch_scc1 2f\n\t"
-            "s_mov_b64 exec, %[nq]\n\t"
-            "s_mov_b64 vcc, %[nq]\n\t"
-            "v_mbcnt_lo_u32_b32 %[td], vcc_lo, 0\n\t"
-            "v_add_u32_e32 %[td], %[qt], %[td]\n\t"
-            "v_lshlrev_b32_e32 %[td], 1, %[td]\n\t"
-            "ds_write_b16 %[td], %[vv] offset:%c[QUEUE]\n"
-            "2:\n\t"
-            "s_mov_b64 exec, %[ex]\n\t"
-            // the next pop's reads: front F0 (its edge heads and itself), second th's distance, the
-            // third entry (slot qn + 2)
-            "v_add_u32_e32 %[vv], %[F0], %[doff]\n\t"
-            "v_lshlrev_b32_e32 %[tb], 2, %[pth]\n\t"
-            "v_lshlrev_b32_e32 %[ta], 2, %[vv]\n\t"
-            "ds_read_b32 %[dF0], %[tb] offset:%c[DIST]\n\t"
-            "ds_read_u16 %[pth], %[tc] offset:%c[QUEUE4]\n\t"
-            "ds_read_b32 %[dv], %[ta] offset:%c[DIST]\n\t"
-            "ds_read_u8 %[pv], %[vv] offset:%c[PIN]\n\t"
-            // bookkeeping and the next pop's checks while the reads are in flight
-            "s_bcnt1_i32_b64 %[t], %[nq]\n\t"
-            "s_add_u32 %[qt], %[qt], %[t]\n\t"
-            "s_add_u32 %[qn], %[qn], 1\n\t"
-            "v_add_u32_e32 %[tc], 2, %[tc]\n\t"
-            "s_mov_b32 %[u], %[F0]\n\t"
-            "s_mov_b32 %[F0], %[th]\n\t"
-            "s_sub_u32 %[bud], %[bud], 1\n\t"
-            "s_cmp_le_i32 %[bud], 0\n\t"
-            "s_cbranch_scc1 8f\n\t"
-            "s_sub_u32 %[t], %[qt], %[qn]\n\t"
-            "s_cmp_lt_i32 %[t], 3\n\t"
-            "s_cbranch_scc1 8f\n\t"
-            "s_waitcnt lgkmcnt(0)\n\t"
+            FP_POP("%[F0]", "%[th]", "QUEUE4", "9f", "8f", "31")
+            FP_POP("%[th]", "%[F0]", "QUEUE6", "7f", "6f", "32")
+            "v_add_u32_e32 %[tc], 4, %[tc]\n\t"
             "s_branch 1b\n"
+            // a segment ended in the first pop of an iteration (the next second is in th)
             "8:\n\t"
-            "s_waitcnt lgkmcnt(0)\n"
+            FP_REFILL("s_mov_b32 %[F0], %[th]\n\tv_add_u32_e32 %[tc], 2, %[tc]\n\t", "5f")
+            "5:\n\t"
+            "s_mov_b32 %[F0], %[th]\n\t"
+            "s_branch 9f\n"
+            // an uncommon pop in the second pop of an iteration (its second is in th)
+            "7:\n\t"
+            "s_mov_b32 %[F0], %[th]\n\t"
+            "s_branch 9f\n"
+            // a segment ended in the second pop of an iteration
+            "6:\n\t"
+            FP_REFILL("v_add_u32_e32 %[tc], 4, %[tc]\n\t", "9f")
             "9:\n\t"
-            : [u] "+s"(u), [F0] "+s"(F0), [qn] "+s"(qn), [qt] "+s"(qt), [bud] "+s"(bud),
+            : [F0] "+s"(F0), [qt] "+s"(qt), [bud] "+s"(bud), [seg] "+s"(seg), [gb] "+s"(gb), [lft] "+s"(lft),
+              [ladd] "+s"(ladd),
               [vv] "+v"(vv), [dv] "+v"(dv), [pv] "+v"(pv), [dF0] "+v"(dF0), [pth] "+v"(pth),
               [ex] "=&s"(ex), [nq] "=&s"(nq), [fm] "=&s"(fm), [im] "=&s"(im), [sw] "=&s"(sw), [du] "=&s"(du),
               [th] "=&s"(th), [t] "=&s"(t), [nd] "=&v"(nd), [ta] "=&v"(ta), [tb] "=&v"(tb), [tc] "=&v"(tc),
               [td] "=&v"(td)
-            : [tq] "s"(tq), [l8] "s"(l8), [doff] "v"(doff), [wl] "v"(wl), [pbits] "v"(pbits), [DIST] "i"(DIST),
-              [QUEUE] "i"(QUEUE), [QUEUE4] "i"(QUEUE + 4), [PIN] "i"(PIN)
+            : [tq] "s"(tq), [l8] "s"(l8), [tv4] "s"(tv4), [fin] "s"(fin), [doff] "v"(doff), [wl] "v"(wl), [pbits] "v"(pbits), [DIST] "i"(DIST),
+              [QUEUE] "i"(QUEUE), [QUEUE4] "i"(QUEUE + 4), [QUEUE6] "i"(QUEUE + 6), [PIN] "i"(PIN)
             : "memory", "scc", "vcc");
-        left -= bud0 - bud;
+#undef FP_POP
+#undef FP_REFILL
+        const int done = (gb0 - gb) + (seg - bud);  // pops run (the one at hand, if uncommon, is not among them)
+        left = lft - (seg - bud);
+        lim_add = ladd;
+        qn += done;
         cnt = qt - qn + 1;
+        u = __builtin_amdgcn_readlane(vv, 8);
     }
 }
 
@@ -3131,7 +3179,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         // pop cap (never reached by a correct SPFA) or, in EARLY, the next early-exit check -- so the
         // common pop pays one scalar compare for both
         int pops = 0, gap = 64, lim = EARLY ? 32 : SIMAPS_POP_CAP;
-        bool early = false;
+        bool early = false, tfinal = false;
         // the target's fixpoint distance (uniform: kept in an SGPR)
         const float finT = EARLY ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh.finT))) : 0.0f;
         // an unreachable target (fixpoint +inf) never gets a parent: the SPFA cannot change the path
@@ -3163,8 +3211,12 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
 #if SIMAPS_SPFA_PIPE && SIMAPS_SPFA_ASM
                     if (asm_ok) {  // the common pops in one asm loop; it returns at `left` = 0 or an uncommon pop
                         int fs = __builtin_amdgcn_readfirstlane(front), ss = __builtin_amdgcn_readfirstlane(second);
+                        int ladd = 0;
                         spfa_fast_pops<OFF_PA, OFF_PA + 4 * CELLS, OFF_PA + 6 * CELLS>(
-                            fs, ss, qn, qt, count, left, ring, pf_v, pf_dv, pf_pv, pf_dF0, pf_third, doff, wl, (int)pbits);
+                            fs, ss, qn, qt, count, left, ladd, ring, pf_v, pf_dv, pf_pv, pf_dF0, pf_third, doff, wl,
+                            (int)pbits, __builtin_amdgcn_readfirstlane(EARLY && !tfinal ? 1 : 0),
+                            __builtin_amdgcn_readfirstlane(tv), finT);
+                        lim += ladd;
                         front = fs;
                         second = ss;
                         if (left <= 0) break;
@@ -3392,6 +3444,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                 // fixpoint in one lane-parallel global read.
                 lim = pops + 32;
                 if (EARLY && __builtin_amdgcn_readfirstlane(__float_as_int(Ld[tv])) == __float_as_int(finT)) {
+                    tfinal = true;  // (from now on the asm loop leaves the target checks to this code)
                     int v = tv, pv = Li[tv], st = 0;
                     bool ok = true;
                     while (ok && v != su) {

@@ -27,7 +27,7 @@ DIRS = [(0, -1), (0, 1), (-1, -1), (-1, 0), (-1, 1), (1, -1), (1, 0), (1, 1)]  #
 WTS = [ONE, ONE, S2, ONE, S2, S2, ONE, S2]
 
 
-def spfa_trace(grid, src, tgt, F):
+def spfa_trace(grid, src, tgt, F, interval=32):
     """Replay pyx:69-107; returns (total pops, exact exit pop, scheduled exit pop)."""
     H, W = grid.shape
     INF = np.float32(2 * H * W)
@@ -44,7 +44,7 @@ def spfa_trace(grid, src, tgt, F):
     inq[s] = True
     pops = 0
     exact = sched = None
-    lim, gap = 32, 64
+    lim, gap = interval, 64
 
     def chain_final():
         v = t
@@ -80,7 +80,7 @@ def spfa_trace(grid, src, tgt, F):
         if exact is None and chain_final():
             exact = pops
         if sched is None and pops == lim:
-            lim = pops + 32
+            lim = pops + interval
             if d[t] == F[t]:
                 if chain_final():
                     sched = pops
@@ -93,6 +93,7 @@ def spfa_trace(grid, src, tgt, F):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--envs', type=int, default=8)
+    ap.add_argument('--interval', type=int, default=32, help='pops between target checks (the kernel: 32)')
     args = ap.parse_args()
     import oracle as O
     from simaps import synthetic
@@ -122,7 +123,7 @@ def main():
                     if F[tgt[0] * ao.shape[1] + tgt[1]] < 0:
                         continue
                     F = np.where(F < 0, np.float32(2 * ao.shape[0] * ao.shape[1]), F)
-                    rows.append(spfa_trace(ao.cspace.astype(bool), src, tgt, F))
+                    rows.append(spfa_trace(ao.cspace.astype(bool), src, tgt, F, args.interval))
             r = np.array(rows, dtype=np.float64)
             out['%s/%s' % (cfg, kind)] = {
                 'queries': len(rows), 'pops_median': float(np.median(r[:, 0])), 'pops_max': float(r[:, 0].max()),
