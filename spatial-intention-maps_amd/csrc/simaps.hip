@@ -2914,7 +2914,8 @@ __device__ __forceinline__ int dir_off(int k, int pw)
 #endif
 // The common SPFA pop (shortest_paths.pyx:89-107) as one inline-asm loop (round 4).  The C++ pop in
 // path_core costs ~85 instructions with the compiler's exec juggling and register copies; this one
-// ~50.  The next pop's LDS reads are issued right after this pop's writes, so their latency overlaps
+// ~43 (two pops per iteration, so the next second needs no copy).  The next pop's LDS reads are
+// issued right after this pop's writes, so their latency overlaps
 // the bookkeeping and the next pop's checks; the improved heads and u's own pin byte go out as one
 // write per array (lane 8 -- doff 0, the popped vertex -- rewrites its unchanged distance), not as a
 // same-address write from every lane.  The loop runs pops while each is "common": the queue keeps
@@ -2922,7 +2923,9 @@ __device__ __forceinline__ int dir_off(int k, int pw)
 // the pop does not lower the front's distance, and neither the tail nor the read-ahead slot reaches
 // the ring's end (no slot wraps).  Then the pushes go to the tail in edge order, slot = tail + rank
 // among the pushed edges, and the next front / second are the current second / third.  It returns
-// when `left` reaches 0 or when the pop at hand is not common -- before any of that pop's writes,
+// when its budget runs out (`left`, or the wrap / count limits), when the early-exit mode's 32-pop
+// target check (done in the loop while tchk is set) finds the target final, or when the pop at hand
+// is not common -- before any of that pop's writes,
 // with its reads (vv / dv / pv / dF0 / pth, issued one pop ahead, as path_core's pf_* values)
 // complete -- so that the C++ pop replays that one exactly.  State as in path_core: u the front, F0
 // the second, qn the slot of F0, qt the tail slot, cnt the live entries including u.  DIST / QUEUE /
