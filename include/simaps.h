@@ -251,13 +251,16 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
                          const double *targets, int max_points, double *out_xy, int32_t *out_count, void *stream);
 
 /* Which path kernels simaps_shortest_path / simaps_grid_path launch (host-side, process-wide; returns
- * the previous mode): 0 automatic (= 2), 1 compact (the SPFA runs to an empty queue), 2 early exit
- * (the SSSP fixpoint by directional sweeps first, then the SPFA only until every vertex of the
- * target's parent chain has its final distance -- whose parent then can no longer change; the
- * fixpoint is parked in device scratch taken from the default memory pool in stream order on the
- * launch stream and returned right after the launch -- a launch being captured into a graph takes
- * the compact kernels instead).  Both return the
- * reference's waypoints exactly. */
+ * the previous mode): 1 compact (the SPFA runs to an empty queue); 2 early exit (the SSSP fixpoint
+ * by directional sweeps first, then the SPFA only until every vertex of the target's parent chain
+ * has its final distance -- whose parent then can no longer change; the fixpoint is parked in device
+ * scratch taken from the default memory pool in stream order on the launch stream and returned right
+ * after the launch -- a launch being captured into a graph takes the compact kernels instead);
+ * 3 early exit with the sweeps overlapped (they run beside the SPFA in the same workgroup, the
+ * fixpoint in LDS: no scratch, graph capture keeps it; half the queries per CU of mode 2);
+ * 0 automatic: 3 while the whole launch is resident at once at mode 3's residency (N <= CUs x 2
+ * small-room / x 1 large-room queries), else 2.  Every mode returns the reference's waypoints
+ * exactly. */
 int simaps_path_mode(int mode);
 
 /* Batched observation ingest into the per-agent maps (occupancy / overhead [M, H, W], slot

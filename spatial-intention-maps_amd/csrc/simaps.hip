@@ -2883,19 +2883,29 @@ struct PathHdr {
     int changed[3];        // (EARLY) per-round "a sweep improved a cell" flags
     uint64_t dirty[4][2];  // (EARLY) per sweep direction: lines to relax again
     float finT;            // (EARLY) the target's fixpoint distance
+    unsigned trio[4];      // (OVL) the sweep waves' Group barrier (arrivals, generation, timeout flag)
+    int swept;             // (OVL) 1 once the fixpoint (and finT) is complete: released by the sweep waves
 };
 constexpr int OFF_PS = align16((int)sizeof(PathHdr));
 constexpr int OFF_PA = OFF_PS + align16((int)(offsetof(SsspScratch, dtab) + sizeof(B128) * MAX_WIN_ROWS));
 // (The early-exit variant's SSSP fixpoint runs in the dist array and is then parked in global memory --
-// the per-stream scratch of path_scratch(), CELLS f32 per query -- so both variants have this layout.)
-template <int CELLS>
+// the per-stream scratch of path_scratch(), CELLS f32 per query -- so both variants have this layout.
+// The overlapped variant, OVL, keeps the fixpoint in its own LDS array `fix` [CELLS] f32 after pin:
+// its sweeps run on waves 1-3 while wave 0 already pops, so the two arrays live side by side.)
+template <int CELLS, bool OVL = false>
 constexpr int path_lds_bytes()
 {
-    return align16(OFF_PA + 7 * CELLS > OFF_PS + (int)sizeof(SsspScratch) ? OFF_PA + 7 * CELLS
-                                                                           : OFF_PS + (int)sizeof(SsspScratch));
+    return align16(OFF_PA + align16(7 * CELLS) + (OVL ? 4 * CELLS : 0) > OFF_PS + (int)sizeof(SsspScratch)
+                       ? OFF_PA + align16(7 * CELLS) + (OVL ? 4 * CELLS : 0)
+                       : OFF_PS + (int)sizeof(SsspScratch));
 }
 static_assert(path_lds_bytes<PATH_SMALL_CELLS>() * 4 <= 160 * 1024, "4 small-room queries per CU");
 static_assert(path_lds_bytes<SIMAPS_MAX_ROOM_CELLS>() * 2 <= 160 * 1024, "2 queries per CU at the room limit");
+static_assert(path_lds_bytes<PATH_SMALL_CELLS, true>() * 2 <= 160 * 1024, "OVL: 2 small-room queries per CU");
+static_assert(path_lds_bytes<SIMAPS_MAX_ROOM_CELLS, true>() <= 160 * 1024, "OVL: 1 query per CU at the room limit");
+// per-CU residency of a path kernel (LDS decides it: 4 waves of <= 128 VGPRs fit many times over)
+template <int CELLS, bool OVL>
+constexpr int path_per_cu() { return (160 * 1024) / path_lds_bytes<CELLS, OVL>(); }
 static_assert(MAX_ROWS <= 256 && SIMAPS_MAX_ROOM_W <= 256, "rect cells pack as (row << 8) | col");
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
@@ -3083,7 +3093,15 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
 // approximate_polygon and the line-of-sight pruning on `line_mask`.  Leaves the kept waypoints in
 // outp[0, cnt) (u16 rect cells (row << 8) | col, target first, i.e. before pyx:152's reversal) and
 // returns cnt in wave 0.  All PNT threads call it.
-template <int CELLS, bool EARLY>
+//
+// OVL (round 4, with EARLY): the sweeps and the SPFA overlap.  Waves 1-3 relax the fixpoint in their
+// own LDS array `fix` (directions 0 / 1 / 2 then 3, rounds separated by the LDS barrier of a
+// 3-wave Group) while wave 0 pops from the first cycle; wave 0 starts its target
+// checks at the first 32-pop boundary after the sweep waves released `swept`.  Any schedule of exact
+// relaxations reaches the same unique f32 fixpoint and the SPFA never reads `fix` before `swept`, so
+// the results are those of EARLY; the fixpoint stays in LDS (no global scratch, no copy, chain checks
+// read LDS), so the launch also runs under graph capture.
+template <int CELLS, bool EARLY, bool OVL = false>
 __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr, int H, int W, bool run_spfa,
                                          int line_mask, float *gfin, const uint16_t *&outp_ret)
 {
@@ -3109,24 +3127,57 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
     // either the prefetched next entry or the vertex an SLF swap just put there), so no read waits
     // for the previous pop's writes except the SLF front's distance, read only when a pop pushes.
     const float INFR = (float)(2 * H * W);
+    static_assert(!OVL || EARLY, "OVL is a schedule of the early-exit variant");
+    float *fix = OVL ? reinterpret_cast<float *>(arr + align16(7 * CELLS)) : nullptr;
     if (tid == 0) STAMP_NB(2);
+    const int su = (sh.src_s[0][0] - sh.i0 + 1) * pw + (sh.src_s[0][1] - sh.j0 + 1);
+    const int tv = (sh.src_s[1][0] - sh.i0 + 1) * pw + (sh.src_s[1][1] - sh.j0 + 1);
     for (int k = tid; k < cells; k += PNT) {
         const int rr = k / pw, cc = k - rr * pw;  // (once per cell)
         const bool fr = rr >= 1 && rr <= h && cc >= 1 && cc <= w && b_test(S.freeb[rr - 1], cc - 1);
-        dist[k] = fr ? (EARLY ? INFINITY : INFR) : -INFINITY;  // (EARLY: the sweeps' initial state)
+        if (OVL) {  // the SPFA's initial state in dist, the sweeps' (source at 0) in fix
+            dist[k] = fr ? INFR : -INFINITY;
+            fix[k] = k == su ? 0.0f : (fr ? INFINITY : -INFINITY);
+        } else {
+            dist[k] = fr ? (EARLY ? INFINITY : INFR) : -INFINITY;  // (EARLY: the sweeps' initial state)
+        }
         pin[k] = 0;
         queue[k] = 0;  // (every ring slot holds a cell index: the prefetched `second` needs no clamp)
     }
-    const int su = (sh.src_s[0][0] - sh.i0 + 1) * pw + (sh.src_s[0][1] - sh.j0 + 1);
-    const int tv = (sh.src_s[1][0] - sh.i0 + 1) * pw + (sh.src_s[1][1] - sh.j0 + 1);
     if (EARLY && tid < 8) {  // only the source's row / column is dirty (all else is +-inf)
         const int d2 = tid >> 1, word = tid & 1;
         const int bit = d2 < 2 ? sh.src_s[0][0] - sh.i0 : sh.src_s[0][1] - sh.j0;
         sh.dirty[d2][word] = (bit >> 6) == word ? 1ull << (bit & 63) : 0ull;
         if (tid < 3) sh.changed[tid] = 0;
+        if (tid == 3) sh.trio[0] = sh.trio[1] = sh.trio[2] = 0u, sh.swept = 0;
     }
     lds_barrier();
-    if (EARLY && run_spfa) {
+    if (OVL && run_spfa && tid >= 64) {
+        // waves 1-3: the fixpoint in fix, directions 0 and 1 on waves 1 and 2, 2 then 3 on wave 3 (the
+        // marks make any order exact); the 3-slot round flags as in the EARLY rounds below
+        const int wave = tid >> 6;
+        const Group g3{tid - 64, PNT - 64, sh.trio, PNT / 64 - 1};
+        int steps = 0, round = 0;
+        for (;; round++) {
+            if (tid == 64) sh.changed[(round + 1) % 3] = 0;
+            bool chg = sweep(fix, h, w, pw, wave == 3 ? 2 : wave - 1, sh.dirty, steps);
+            if (wave == 3) chg = sweep(fix, h, w, pw, 3, sh.dirty, steps) || chg;
+            if (chg && lane == 0) sh.changed[round % 3] = 1;
+            g3.sync();
+            if (!sh.changed[round % 3] || round >= h * w + 16) break;
+        }
+        if (tid == 64) {
+            const unsigned f = (round >= h * w + 16 ? SIMAPS_FAULT_ROUNDS : 0u) | (sh.trio[2] ? SIMAPS_FAULT_TIMEOUT : 0u);
+            if (f) __hip_atomic_fetch_or(&sh.fault, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            sh.finT = fix[tv];
+            STAMP_VAL(8, round + 1);
+            STAMP_NB(10);  // (stamp build: the sweeps' end)
+            // (local-only fence, as Group::sync: an acquire / release atomic would also wait for global accesses)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            __hip_atomic_store(&sh.swept, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    if (EARLY && !OVL && run_spfa) {
         // The f32 fixpoint of the graph from the source -- the SPFA's final distances, bitwise (SURVEY
         // a10) -- by the get_state sweeps, one direction per wave, rounds until nothing improves.
         // A vertex whose SPFA distance already equals it can never improve again, so its parent is
@@ -3183,10 +3234,11 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         // common pop pays one scalar compare for both
         int pops = 0, gap = 64, lim = EARLY ? 32 : SIMAPS_POP_CAP;
         bool early = false, tfinal = false;
-        // the target's fixpoint distance (uniform: kept in an SGPR)
-        const float finT = EARLY ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh.finT))) : 0.0f;
+        // the target's fixpoint distance (uniform: kept in an SGPR); OVL: known once `swept` is seen
+        bool have_fin = !OVL;
+        float finT = EARLY && !OVL ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh.finT))) : 0.0f;
         // an unreachable target (fixpoint +inf) never gets a parent: the SPFA cannot change the path
-        if (EARLY && finT == INFINITY) count = 0, early = true;
+        if (EARLY && !OVL && finT == INFINITY) count = 0, early = true;
 #if SIMAPS_SPFA_PIPE
         // the reads of the next pop, issued one pop ahead: its vertex's 8 edge heads and itself
         // (lane 8), the distance of the entry after it (the SLF front during that pop) and the slot
@@ -3217,7 +3269,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                         int ladd = 0;
                         spfa_fast_pops<OFF_PA, OFF_PA + 4 * CELLS, OFF_PA + 6 * CELLS>(
                             fs, ss, qn, qt, count, left, ladd, ring, pf_v, pf_dv, pf_pv, pf_dF0, pf_third, doff, wl,
-                            (int)pbits, __builtin_amdgcn_readfirstlane(EARLY && !tfinal ? 1 : 0),
+                            (int)pbits, __builtin_amdgcn_readfirstlane(EARLY && have_fin && !tfinal ? 1 : 0),
                             __builtin_amdgcn_readfirstlane(tv), finT);
                         lim += ladd;
                         front = fs;
@@ -3446,7 +3498,14 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                 // round per step), 64 vertices to a batch, each batch's distances compared with the
                 // fixpoint in one lane-parallel global read.
                 lim = pops + 32;
-                if (EARLY && __builtin_amdgcn_readfirstlane(__float_as_int(Ld[tv])) == __float_as_int(finT)) {
+                if (OVL && !have_fin &&
+                    __builtin_amdgcn_readfirstlane(__hip_atomic_load(&sh.swept, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                    have_fin = true;
+                    finT = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh.finT)));
+                    if (finT == INFINITY) { early = true; break; }
+                }
+                if (EARLY && have_fin && __builtin_amdgcn_readfirstlane(__float_as_int(Ld[tv])) == __float_as_int(finT)) {
                     tfinal = true;  // (from now on the asm loop leaves the target checks to this code)
                     int v = tv, pv = Li[tv], st = 0;
                     bool ok = true;
@@ -3459,7 +3518,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                             if (lane == k) mine = v;
                             pv = Li[v];
                         }
-                        if (ok && __ballot(mine >= 0 && Ld[mine] != gfin[mine])) ok = false;
+                        if (ok && __ballot(mine >= 0 && Ld[mine] != (OVL ? fix[mine] : gfin[mine]))) ok = false;
                     }
                     // drain the walk's LDS reads here: left pending on any exit of this block, they make
                     // the compiler wait for every LDS access at the loop's back edge on the common
@@ -3577,7 +3636,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
     return 0;
 }
 
-template <int CELLS, bool EARLY>
+template <int CELLS, bool EARLY, bool OVL>
 __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents,
                                                    const simaps_env *__restrict__ envs,
                                                    const simaps_robot *__restrict__ robots,
@@ -3586,7 +3645,7 @@ __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry g
                                                    int max_pts, double *__restrict__ out_xy, int *__restrict__ out_n,
                                                    float *scratch, unsigned *fault)
 {
-    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS>()];
+    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS, OVL>()];
     PathHdr &sh = *reinterpret_cast<PathHdr *>(smem);
     SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_PS);
     const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -3629,8 +3688,8 @@ __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry g
     if (tid == 0) STAMP_NB(1);
     snap_sources(sh, S, 2, g);
     const uint16_t *outp;
-    const int cnt = path_core<CELLS, EARLY>(sh, S, smem + OFF_PA, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE,
-                                            EARLY ? scratch + (size_t)n * CELLS : nullptr, outp);
+    const int cnt = path_core<CELLS, EARLY, OVL>(sh, S, smem + OFF_PA, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE,
+                                                 EARLY && !OVL ? scratch + (size_t)n * CELLS : nullptr, outp);
     if (tid < 64) {
         // (7) positions (envs.py:2494-2503); path[0] / path[-1] replaced by the given positions
         if (cnt < 2) {
@@ -3656,14 +3715,14 @@ __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry g
 // workgroup per (grid, source, target): the same exact SPFA / parent walk / approximate_polygon as
 // path_kernel, without the cspace, snap and straight-line steps of OccupancyMap.shortest_path, the
 // line-of-sight pruning on the grid itself, and the waypoints returned as cells (target last).
-template <int CELLS, bool EARLY>
+template <int CELLS, bool EARLY, bool OVL>
 __global__ void __launch_bounds__(PNT) grid_path_kernel(int H, int W, const uint8_t *__restrict__ grids,
                                                         const int32_t *__restrict__ sources,
                                                         const int32_t *__restrict__ targets, int wi0, int wj0, int wh,
                                                         int ww, int max_pts, int32_t *__restrict__ out_ij,
                                                         int32_t *__restrict__ out_n, float *scratch, unsigned *fault)
 {
-    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS>()];
+    __shared__ __attribute__((aligned(16))) char smem[path_lds_bytes<CELLS, OVL>()];
     PathHdr &sh = *reinterpret_cast<PathHdr *>(smem);
     SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_PS);
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -3697,8 +3756,8 @@ __global__ void __launch_bounds__(PNT) grid_path_kernel(int H, int W, const uint
         return;
     }
     const uint16_t *outp;
-    const int cnt = path_core<CELLS, EARLY>(sh, S, smem + OFF_PA, H, W, true, LINE_GRID_ONE,
-                                            EARLY ? scratch + (size_t)b * CELLS : nullptr, outp);
+    const int cnt = path_core<CELLS, EARLY, OVL>(sh, S, smem + OFF_PA, H, W, true, LINE_GRID_ONE,
+                                                 EARLY && !OVL ? scratch + (size_t)b * CELLS : nullptr, outp);
     if (tid < 64) {
         if (cnt > max_pts) {
             if (lane == 0) out_n[b] = -cnt;  // caller's buffer too small
@@ -4254,15 +4313,38 @@ const Geometry &geometry()
     return g;
 }
 
-// Path kernel choice: the early-exit variant (SSSP fixpoint first, then the SPFA only until the target's
-// parent chain is final) unless simaps_path_mode(1) forces the compact one.  Same LDS footprint and
-// the same pop loop, so it pays only its sweeps (~15 us small rooms, ~26 us large) and chain checks:
-// measured 0.7-1.05x the compact launch time for targets across the room and 0.5-0.95x for targets
-// in the robot's local map (the reference's action space), DESIGN.md section 5.
+// Path kernel choice (simaps_path_mode).  1: compact.  2: early exit (the SSSP fixpoint first, then the
+// SPFA only until the target's parent chain is final; same LDS footprint and pop loop as compact, so it
+// pays its sweeps, ~15 us small rooms / ~26 us large, and chain checks: measured 0.7-1.05x the compact
+// launch time for targets across the room and 0.5-0.95x for targets in the robot's local map, DESIGN.md
+// section 5).  3: early exit with the sweeps overlapped (OVL: on waves 1-3 beside the SPFA, the
+// fixpoint in LDS -- no pool scratch, so graph capture keeps it -- at 2 small-room / 1 large-room
+// queries per CU instead of 4 / 2).  0, automatic: OVL while the launch is resident at once at OVL's
+// residency (N <= CUs x per-CU), else 2 (compact when the launch is being captured).
 std::atomic<int> g_path_mode{0};
-bool path_early(int /*n*/, bool /*small*/)
+enum PathKind { PK_COMPACT, PK_EARLY, PK_OVL };
+int device_cus()
 {
-    return g_path_mode.load() != 1;
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    int v = cache[dev].load(std::memory_order_relaxed);
+    if (v <= 0) {
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cache[dev].store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+PathKind path_kind(int n, bool small)
+{
+    switch (g_path_mode.load()) {
+    case 1: return PK_COMPACT;
+    case 2: return PK_EARLY;
+    case 3: return PK_OVL;
+    default: break;
+    }
+    const int per = small ? path_per_cu<PATH_SMALL_CELLS, true>() : path_per_cu<SIMAPS_MAX_ROOM_CELLS, true>();
+    return (long)n <= (long)device_cus() * per ? PK_OVL : PK_EARLY;
 }
 
 // Device scratch of the early-exit path kernels (the SSSP fixpoint, CELLS f32 per query): stream-
@@ -4510,18 +4592,22 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
     const Geometry &geo = geometry();
     const bool small = (cfg->room_h + 2) * ((cfg->room_w + 2) | 1) <= PATH_SMALL_CELLS;
     const hipStream_t st = (hipStream_t)stream;
+    const PathKind kind = path_kind(N, small);
     PathScratch ps;
-    if (path_early(N, small)) path_scratch(ps, st, (size_t)N * SIMAPS_MAX_ROOM_CELLS * sizeof(float));
+    if (kind == PK_EARLY) path_scratch(ps, st, (size_t)N * SIMAPS_MAX_ROOM_CELLS * sizeof(float));
     float *scratch = ps.p;
-#define SIMAPS_PATH_LAUNCH(C, E)                                                                       \
-    hipLaunchKernelGGL((path_kernel<C, E>), dim3(N), dim3(PNT), 0, st, *cfg, geo, agents, envs, robots, occupancy, sources, \
-                       targets, max_points, out_xy, out_count, scratch, g_fault_dev)
-    if (scratch) {
-        if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, true);
-        else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true);
+#define SIMAPS_PATH_LAUNCH(C, E, O)                                                                    \
+    hipLaunchKernelGGL((path_kernel<C, E, O>), dim3(N), dim3(PNT), 0, st, *cfg, geo, agents, envs, robots, occupancy, \
+                       sources, targets, max_points, out_xy, out_count, scratch, g_fault_dev)
+    if (kind == PK_OVL) {
+        if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, true, true);
+        else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, true);
+    } else if (scratch) {
+        if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, true, false);
+        else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, false);
     } else {
-        if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, false);
-        else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, false);
+        if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, false, false);
+        else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, false, false);
     }
 #undef SIMAPS_PATH_LAUNCH
     const hipError_t e = hipGetLastError();
@@ -4531,7 +4617,7 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
 
 int simaps_path_mode(int mode)
 {
-    if (mode < 0 || mode > 2) return fail(SIMAPS_EINVAL, "path mode %d not in 0..2", mode);
+    if (mode < 0 || mode > 3) return fail(SIMAPS_EINVAL, "path mode %d not in 0..3", mode);
     return g_path_mode.exchange(mode);
 }
 
@@ -4602,18 +4688,22 @@ int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *s
     if (const int rc = pending_faults()) return rc;
     const bool small = (wh + 2) * ((ww + 2) | 1) <= PATH_SMALL_CELLS;
     const hipStream_t st = (hipStream_t)stream;
+    const PathKind kind = path_kind(B, small);
     PathScratch ps;
-    if (path_early(B, small)) path_scratch(ps, st, (size_t)B * SIMAPS_MAX_ROOM_CELLS * sizeof(float));
+    if (kind == PK_EARLY) path_scratch(ps, st, (size_t)B * SIMAPS_MAX_ROOM_CELLS * sizeof(float));
     float *scratch = ps.p;
-#define SIMAPS_GRID_PATH_LAUNCH(C, E)                                                                  \
-    hipLaunchKernelGGL((grid_path_kernel<C, E>), dim3(B), dim3(PNT), 0, st, H, W, grids, sources, targets, wi0, wj0, wh, \
-                       ww, max_points, out_ij, out_count, scratch, g_fault_dev)
-    if (scratch) {
-        if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, true);
-        else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true);
+#define SIMAPS_GRID_PATH_LAUNCH(C, E, O)                                                               \
+    hipLaunchKernelGGL((grid_path_kernel<C, E, O>), dim3(B), dim3(PNT), 0, st, H, W, grids, sources, targets, wi0, wj0, \
+                       wh, ww, max_points, out_ij, out_count, scratch, g_fault_dev)
+    if (kind == PK_OVL) {
+        if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, true, true);
+        else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, true);
+    } else if (scratch) {
+        if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, true, false);
+        else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, false);
     } else {
-        if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, false);
-        else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, false);
+        if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, false, false);
+        else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, false, false);
     }
 #undef SIMAPS_GRID_PATH_LAUNCH
     const hipError_t e = hipGetLastError();

@@ -130,15 +130,17 @@ def test_ingest_chunk_count_and_argument_checks():
 
 
 def test_path_mode_setter():
-    """simaps_path_mode returns the previous mode, accepts 0 (automatic = early exit), 1 (compact)
-    and 2 (early exit) and refuses anything else without changing the mode (host-side only)."""
+    """simaps_path_mode returns the previous mode, accepts 0 (automatic), 1 (compact), 2 (early
+    exit) and 3 (early exit, sweeps overlapped) and refuses anything else without changing the mode
+    (host-side only)."""
     from simaps import _lib
     L = _lib.lib
     prev = L.simaps_path_mode(1)
     try:
         assert L.simaps_path_mode(2) == 1
-        assert L.simaps_path_mode(0) == 2
-        for bad in (-1, 3):
+        assert L.simaps_path_mode(3) == 2
+        assert L.simaps_path_mode(0) == 3
+        for bad in (-1, 4):
             assert L.simaps_path_mode(bad) == _lib.EINVAL
         assert L.simaps_path_mode(0) == 0  # unchanged by the refused calls
     finally:

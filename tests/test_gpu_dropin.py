@@ -295,10 +295,11 @@ def test_distance_to_receptacle_dropin(V):
             assert got[e][a] == [ao.shortest_path_distance(s['receptacle_position'], p) for p in pos[e][a]]
 
 
-@pytest.fixture(params=[1, 2], ids=['compact', 'early_exit'])
+@pytest.fixture(params=[1, 2, 3], ids=['compact', 'early_exit', 'overlap'])
 def path_mode(request):
-    """Both path kernel variants (include/simaps.h simaps_path_mode): 1 the SPFA to an empty queue,
-    2 the SSSP fixpoint first and the SPFA only until the target's parent chain is final."""
+    """Every path kernel variant (include/simaps.h simaps_path_mode): 1 the SPFA to an empty queue,
+    2 the SSSP fixpoint first and the SPFA only until the target's parent chain is final, 3 the same
+    early exit with the fixpoint's sweeps running beside the SPFA (fixpoint in LDS)."""
     from simaps import _lib
     prev = _lib.lib.simaps_path_mode(request.param)
     yield request.param
@@ -847,9 +848,11 @@ def test_periodic_remap_successive_frames(V):
 
 
 def test_path_launch_in_graph_capture(V):
-    """A path launch captured into a graph gets no early-exit scratch (it is taken from the memory
-    pool in stream order per eager launch) and runs the compact kernel: the replay equals the eager
-    launches of both kernels, for targets across the divider (detours: the SPFA runs)."""
+    """Path launches captured into a graph: in mode 2 the early-exit kernel gets no scratch (it is
+    taken from the memory pool in stream order per eager launch) and the capture runs the compact
+    kernel; in the automatic mode a launch this small takes the overlapped kernel, whose fixpoint
+    lives in LDS, so the capture keeps the early exit.  Every replay equals the eager launches of
+    every kernel, for targets across the divider (detours: the SPFA runs)."""
     synthetic, _ = V
     from simaps import _lib, batch
     scenes = [synthetic.make_scene('lifting_4-small_divider', 70 + e) for e in range(8)]
@@ -862,26 +865,30 @@ def test_path_launch_in_graph_capture(V):
     prev = _lib.lib.simaps_path_mode(0)
     try:
         eager = {}
-        for mode in (1, 0):
+        for mode in (1, 2, 3, 0):
             _lib.lib.simaps_path_mode(mode)
             xy, cnt = b.launch_shortest_paths(src, tgt)
             eager[mode] = (xy.cpu().numpy(), cnt.cpu().numpy())
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            gxy, gcnt = b.launch_shortest_paths(src, tgt)
-        gxy.fill_(np.nan)
-        g.replay()
-        torch.cuda.synchronize()
-        _lib.check_faults()
-        got = (gxy.cpu().numpy(), gcnt.cpu().numpy())
+        captured = {}
+        for mode in (0, 2):
+            _lib.lib.simaps_path_mode(mode)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                gxy, gcnt = b.launch_shortest_paths(src, tgt)
+            gxy.fill_(np.nan)
+            g.replay()
+            torch.cuda.synchronize()
+            _lib.check_faults()
+            captured[mode] = (gxy.cpu().numpy(), gcnt.cpu().numpy())
     finally:
         _lib.lib.simaps_path_mode(prev)
-    for xy, cnt in eager.values():
-        assert np.array_equal(cnt, got[1])
-        for n, c in enumerate(cnt):
-            assert c >= 2 and np.array_equal(xy[n, :c], got[0][n, :c]), n
-    assert (got[1] > 2).sum() >= 8  # detours
+    for got in captured.values():
+        for xy, cnt in eager.values():
+            assert np.array_equal(cnt, got[1])
+            for n, c in enumerate(cnt):
+                assert c >= 2 and np.array_equal(xy[n, :c], got[0][n, :c]), n
+        assert (got[1] > 2).sum() >= 8  # detours
 
 
 def test_path_scratch_growth(V):

@@ -147,7 +147,44 @@ def test_path_pop_cap_reaches_the_caller(S):
     assert _lib.lib.simaps_fault_status(0) == 0
 
 
-@pytest.mark.parametrize('mode', [1, 2], ids=['compact', 'early_exit'])
+def test_overlap_sweep_barrier_flag_reaches_the_caller(S):
+    """The overlapped path kernel (simaps_path_mode 3) separates its sweep rounds with a 3-wave
+    Group barrier; the diagnostic build raises the barrier-timeout flag at that spin too, and it
+    surfaces like get_state's.  Straight-line queries run neither sweeps nor SPFA: no flag."""
+    _lib, batch, synthetic = S
+    if not os.path.exists(DIAG_LIB):
+        pytest.fail('build the diagnostic library first: make -C spatial-intention-maps_amd/csrc diag')
+    L = _lib._load(DIAG_LIB)
+    L.simaps_fault_status(1)
+    prev = L.simaps_path_mode(3)
+    try:
+        scene = synthetic.make_scene('lifting_4-small_divider', 5)
+        b = batch.StateBatch([scene])
+        rl, rw = scene['room_length'], scene['room_width']
+
+        def run(src, tgt):
+            s = torch.tensor(src, dtype=torch.float64, device=b.device)
+            t = torch.tensor(tgt, dtype=torch.float64, device=b.device)
+            xy = torch.empty((b.N, 64, 2), dtype=torch.float64, device=b.device)
+            cnt = torch.empty((b.N,), dtype=torch.int32, device=b.device)
+            rc = L.simaps_shortest_path(b.cfg, b.N, _lib.ptr(b.agents_d), _lib.ptr(b.envs_d), _lib.ptr(b.robots_d),
+                                        _lib.ptr(b.occupancy), _lib.ptr(s), _lib.ptr(t), 64, _lib.ptr(xy),
+                                        _lib.ptr(cnt), _lib.stream_handle())
+            torch.cuda.synchronize()
+            return rc
+        src = [[-rl / 4, -rw / 4]] * b.N
+        assert run(src, [[rl / 4, rw / 4 - 0.01 * a] for a in range(b.N)]) == 0
+        assert L.simaps_fault_status(0) & _lib.FAULT_TIMEOUT
+        with pytest.raises(_lib.DeviceFault):
+            _lib.check_faults(L)
+        assert run(src, src) == 0
+        assert L.simaps_fault_status(0) == 0
+    finally:
+        L.simaps_path_mode(prev)
+    assert _lib.lib.simaps_fault_status(0) == 0
+
+
+@pytest.mark.parametrize('mode', [1, 2, 3], ids=['compact', 'early_exit', 'overlap'])
 def test_spfa_ring_wraps_exact(S, monkeypatch, mode):
     """The product SPFA's queue ring has one slot per room cell, and a query pops about once per
     free cell, so its wrap arithmetic rarely runs.  The diagnostic ring build (libsimaps_diagring.so,

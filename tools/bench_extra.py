@@ -198,7 +198,7 @@ def bench_env_step(args):
         res[name + '_us'] = e0.elapsed_time(e1) / K * 1e3
     print(json.dumps(dict({'row': 'env_step', 'config': args.config, 'awaiting_robots': n,
                            'note': 'device time per reference step (HIP events, %d launches each): movement paths '
-                                   '(early-exit kernel, local-map targets), forward-camera ingest, get_state of the '
+                                   '(automatic path mode: the overlapped early-exit kernel at this size, local-map targets), forward-camera ingest, get_state of the '
                                    'awaiting robots; step = the three in order on one stream' % K}, **res)),
           flush=True)
 

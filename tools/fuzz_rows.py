@@ -52,7 +52,7 @@ def _oracle(job):
 def main():
     argv = list(sys.argv[1:])
     mode = 0
-    if '--path-mode' in argv:  # simaps_path_mode: 0 automatic, 1 compact, 2 early exit
+    if '--path-mode' in argv:  # simaps_path_mode: 0 automatic, 1 compact, 2 early exit, 3 overlapped early exit
         k = argv.index('--path-mode')
         mode = int(argv[k + 1])
         del argv[k:k + 2]

@@ -54,7 +54,7 @@ def case(cfg, envs, steps, mode=0, targets='across'):
     _lib.check_faults()
     _lib.lib.simaps_path_mode(prev)
     ms = e0.elapsed_time(e1) / steps
-    out = {'config': cfg, 'targets': targets, 'path_mode': {0: 'auto', 1: 'compact', 2: 'early_exit'}[mode],
+    out = {'config': cfg, 'targets': targets, 'path_mode': {0: 'auto', 1: 'compact', 2: 'early_exit', 3: 'overlap'}[mode],
            'paths_per_launch': N, 'ms_per_launch': ms, 'paths_per_s': N / (ms * 1e-3),
            'detours': int((cnt.cpu().numpy() > 2).sum())}
     if '--stamps' in sys.argv:
@@ -68,8 +68,8 @@ def case(cfg, envs, steps, mode=0, targets='across'):
         pops = st[full, 7]
         out.update({'spfa_queries': int(full.sum()), 'spfa_us_median': float(np.median(spfa_us)),
                     'pops_median': float(np.median(pops)),
-                    'sweep_rounds_median': float(np.median(st[full, 8])) if mode == 2 else None,
-                    'sweeps_us_median': float(np.median((st[full, 10] - st[full, 2]) / 100.0)) if mode == 2 else None,
+                    'sweep_rounds_median': float(np.median(st[full, 8])) if mode in (2, 3) else None,
+                    'sweeps_us_median': float(np.median((st[full, 10] - st[full, 2]) / 100.0)) if mode in (2, 3) else None,
                     'ns_per_pop_median': float(np.median(spfa_us * 1e3 / np.maximum(pops, 1))),
                     'query_us_median': float(np.median((st[full, 6] - st[full, 0]) / 100.0))})
     print(json.dumps(out), flush=True)
@@ -85,5 +85,5 @@ if __name__ == '__main__':
                           ('lifting_4-small_divider', 256), ('lifting_4-small_divider', 512),
                           ('lifting_4-large_doors', 16), ('lifting_4-large_doors', 64), ('lifting_4-large_doors', 256),
                           ('lifting_4-large_doors', 512)):
-            for mode in (1, 2):
+            for mode in (1, 2, 3):
                 case(cfg, envs, steps, mode, targets)
