@@ -19,7 +19,7 @@ import numpy as np  # noqa: E402
 
 CONFIGS = ['lifting_4-small_divider', 'pushing_4-large_empty', 'lifting_2_throwing_2-large_empty', 'rescue_4-small_empty',
            'lifting_4-large_doors', 'lifting_4-large_tunnels', 'lifting_4-large_rooms']
-SEED0 = 6000
+SEED0 = int(os.environ.get('SIMAPS_FUZZ_SEED0', '6000'))  # (--seed0 sets it for the spawned oracle workers too)
 
 
 def queries(scene, e, a, Q):
@@ -55,6 +55,12 @@ def main():
     if '--path-mode' in argv:  # simaps_path_mode: 0 automatic, 1 compact, 2 early exit, 3 overlapped early exit
         k = argv.index('--path-mode')
         mode = int(argv[k + 1])
+        del argv[k:k + 2]
+    if '--seed0' in argv:  # first scene seed (default 6000): fresh seeds for a new fuzz run
+        k = argv.index('--seed0')
+        global SEED0
+        SEED0 = int(argv[k + 1])
+        os.environ['SIMAPS_FUZZ_SEED0'] = str(SEED0)
         del argv[k:k + 2]
     envs = int(argv[0]) if len(argv) > 0 else 16
     Q = int(argv[1]) if len(argv) > 1 else 4
