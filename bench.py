@@ -4,6 +4,10 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N ...
 
+Without a launcher, `--gpus N` (N > 1) starts N rank processes itself (one per GPU, before any GPU
+call in the parent); under a launcher, --gpus must equal its WORLD_SIZE.  More ranks than visible
+GPUs is refused unless --shared-gpu (a 1-GPU rehearsal over gloo).
+
 A step = one launch rendering every agent of E envs (E x A stacks) from HBM-resident per-agent
 maps (inputs uploaded before the timed region).  Multi-GPU: each rank renders its own block of
 envs (distinct seeds) -- E per rank (weak scaling, default) or a contiguous share of
@@ -186,9 +190,99 @@ def gather_states(out, reps, world, rank, return_data=False):
     return (stats, dst) if return_data else stats
 
 
-def main():
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def resolve_world(gpus, env, device_count, shared_gpu=False, standin=False):
+    """How many ranks this invocation runs and who launches them: ('single', 1), ('external', W)
+    when a launcher (torch.distributed.run) already set WORLD_SIZE, or ('spawn', N) when
+    `bench.py --gpus N` has to start its own N ranks -- the reference's data-parallel collector
+    starts its own workers too (train_multiprocess.py:217-228).  Raises SystemExit (non-zero, with
+    a message) on a request that cannot be honoured: --gpus different from the launcher's
+    WORLD_SIZE, or more ranks than visible GPUs (unless --shared-gpu rehearses them on cuda:0)."""
+    if gpus is not None and gpus < 1:
+        raise SystemExit('bench.py: --gpus must be >= 1 (got %d)' % gpus)
+    if 'WORLD_SIZE' in env:
+        world = int(env['WORLD_SIZE'])
+        if gpus is not None and gpus != world:
+            raise SystemExit('bench.py: --gpus %d but the launcher started WORLD_SIZE=%d ranks' % (gpus, world))
+        kind = 'external'
+    else:
+        world = 1 if gpus is None else gpus
+        kind = 'spawn' if world > 1 else 'single'
+    if not (shared_gpu or standin) and world > device_count:
+        raise SystemExit('bench.py: %d ranks requested but %d GPU(s) visible (--shared-gpu rehearses several '
+                         'ranks on cuda:0)' % (world, device_count))
+    return kind, world
+
+
+def spawn_ranks(world, argv, shared_gpu=False):
+    """Start `world` child ranks of this script (same arguments), one process per GPU, each with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run would; the parent never
+    touches the GPU.  Rank 0's stdout is the bench line.  Returns the first non-zero exit status
+    (the other ranks are then terminated) or 0."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK='0' if shared_gpu else str(r), WORLD_SIZE=str(world),
+                   LOCAL_WORLD_SIZE=str(world), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
+                   SIMAPS_BENCH_LAUNCHER='spawn')
+        procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
+class StandinBatch:
+    """Test-only stand-in for StateBatch (bench.py --standin): the same scenes, slot count and
+    output shape, on the CPU, with a render that only fills its output.  It lets the CPU suite run
+    bench.main() end to end -- spawn, process group, timed region, rank report, the line -- without
+    a GPU; a --standin line says so in `data` and is never a measurement."""
+
+    def __init__(self, scenes, layout):
+        from simaps import _lib, batch
+        s0 = scenes[0]
+        self.N = sum(len(s['robots']) for s in scenes)
+        self.H, self.W = s0['H'], s0['W']
+        cfg = batch.make_config(s0['flags'], s0['room_width'], s0['room_length'], layout)
+        self.C = _lib.lib.simaps_num_channels(cfg, len(s0['robots']))
+        self.layout = layout
+
+    def alloc_state(self):
+        import torch
+        shape = (self.N, self.C, 96, 96) if self.layout == 'chw' else (self.N, 96, 96, self.C)
+        return torch.empty(shape, dtype=torch.float32)
+
+    def render(self, out, stream=None):
+        out.fill_(1.0)
+        return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='ranks (one per GPU); without a launcher bench.py starts them itself (default: 1, or '
+                         'the launcher\'s WORLD_SIZE)')
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument('--config', default='lifting_4-small_divider')
@@ -208,20 +302,29 @@ def main():
     ap.add_argument('--shared-gpu', action='store_true',
                     help='rehearsal on a 1-GPU box: every rank renders on cuda:0 and the barriers / reductions go '
                          'over gloo (RCCL refuses two ranks on one device); NOT a scaling measurement')
-    args = ap.parse_args()
+    ap.add_argument('--standin', action='store_true', help=argparse.SUPPRESS)  # CPU tests only (StandinBatch)
+    args = ap.parse_args(argv)
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
+    # Before any GPU call: decide the ranks, and start them ourselves when no launcher did.
+    # (torch.cuda.device_count() does not initialise the GPU on this image.)
+    ndev = 0 if args.standin else torch.cuda.device_count()
+    kind, world = resolve_world(args.gpus, os.environ, ndev, args.shared_gpu, args.standin)
+    if kind == 'spawn':
+        return spawn_ranks(world, argv, args.shared_gpu)
+    launcher = os.environ.get('SIMAPS_BENCH_LAUNCHER', kind)
+
     rank = int(os.environ.get('RANK', '0'))
     local = 0 if args.shared_gpu else int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
-    red = 'cpu' if args.shared_gpu else 'cuda'  # device of the timing / counter reductions
+    cpu = args.standin
+    if not cpu:
+        torch.cuda.set_device(local)
+    red = 'cpu' if (args.shared_gpu or cpu) else 'cuda'  # device of the timing / counter reductions
     dist_on = world > 1 or args.init_dist
     if dist_on:
-        if args.shared_gpu:
+        if args.shared_gpu or cpu:
             dist.init_process_group('gloo')
         else:
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
@@ -232,30 +335,34 @@ def main():
         raise SystemExit('--total-envs must give every rank at least one env')
     env_ids = rank_envs(rank, args.envs, world, args.total_envs)
     scenes = [synthetic.make_scene(args.config, e) for e in env_ids]
-    b = batch.StateBatch(scenes, device='cuda', layout=args.layout)
+    b = StandinBatch(scenes, args.layout) if cpu else batch.StateBatch(scenes, device='cuda', layout=args.layout)
     out = b.alloc_state()
-    stream = torch.cuda.current_stream()
+    stream = None if cpu else torch.cuda.current_stream()
 
     # HIP events on the launch stream bracket the K timed launches (per-launch events would add
     # ~6 us of marker overhead to every step); kernel_ms = their elapsed time / K, i.e. the average
     # launch duration including the launch-to-launch gaps (conservative for the roofline).
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if not cpu:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def step(k):
-        if k == 0:
+        if k == 0 and not cpu:
             ev0.record(stream)
         b.render(out, stream=stream)
-        if k == args.steps - 1:
+        if k == args.steps - 1 and not cpu:
             ev1.record(stream)
 
     own = []
-    elapsed = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, red, own)
-    own_ms = ev0.elapsed_time(ev1) / args.steps
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
+    elapsed = timed_steps(step, args.steps, args.warmup, sync, world, red, own)
+    own_ms = own[0] * 1e3 / args.steps if cpu else ev0.elapsed_time(ev1) / args.steps
     kern_ms = max_over_ranks([own_ms], world, red)[0]
     import socket
-    ranks = rank_report(dict(device_identity(torch.device('cuda', local)), rank=rank, local_rank=local,
+    ident = {'device': 'cpu'} if cpu else device_identity(torch.device('cuda', local))
+    ranks = rank_report(dict(ident, rank=rank, local_rank=local,
                              host=socket.gethostname(), env_range=[env_ids[0], env_ids[-1]],
                              stacks_per_step=b.N, steps=args.steps, seconds=own[0], kernel_ms=own_ms), world)
+    ranks['launcher'] = launcher
 
     stacks_per_step = int(sum_over_ranks([b.N], world, red)[0])
     value = stacks_per_step * args.steps / elapsed
@@ -284,7 +391,9 @@ def main():
             'value': value, 'unit': 'stacks/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True,
             'scaling': 'strong' if strong else 'weak',
-            'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic (seeded scenes, SURVEY 8(d))',
+            'vs_baseline': None, 'dtype': 'f32',
+            'data': 'STANDIN (CPU test of the bench plumbing; not a measurement)' if cpu
+                    else 'synthetic (seeded scenes, SURVEY 8(d))',
             'config': {'workload': args.config, 'agents_per_env': len(scenes[0]['robots']),
                        'stacks_per_step': stacks_per_step, 'grid': '%dx%d' % (b.H, b.W), 'channels': b.C,
                        'layout': args.layout,
@@ -298,12 +407,13 @@ def main():
         res['distributed'] = ranks
         if gather is not None:
             res['gather'] = gather
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not cpu:
             res['cpu_baseline'] = cpu_baseline(args.config, args.cpu_budget, args.cpu_procs)
         print(json.dumps(res), flush=True)
     if dist_on:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

@@ -235,6 +235,12 @@ __device__ __forceinline__ void post_faults(unsigned *fault, unsigned f)
         for (int k = 0; k < SIMAPS_NFAULT; k++)
             if (f & (1u << k)) __hip_atomic_store(fault + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// A workgroup's own LDS fault word: waves that do not meet at a barrier (the overlapped path kernel's
+// SPFA wave beside its sweep waves) may set bits at the same time, so every writer ORs atomically.
+__device__ __forceinline__ void fault_or(unsigned &word, unsigned f)
+{
+    __hip_atomic_fetch_or(&word, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // ------------------------------------------------------------------------------------------------
 // LDS layout
@@ -3168,7 +3174,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         }
         if (tid == 64) {
             const unsigned f = (round >= h * w + 16 ? SIMAPS_FAULT_ROUNDS : 0u) | (sh.trio[2] ? SIMAPS_FAULT_TIMEOUT : 0u);
-            if (f) __hip_atomic_fetch_or(&sh.fault, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (f) fault_or(sh.fault, f);
             sh.finT = fix[tv];
             STAMP_VAL(8, round + 1);
             STAMP_NB(10);  // (stamp build: the sweeps' end)
@@ -3198,7 +3204,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
             }
             if (!sh.changed[round % 3] || round >= h * w + 16) break;
         }
-        if (tid == 0 && round >= h * w + 16) sh.fault |= SIMAPS_FAULT_ROUNDS;
+        if (tid == 0 && round >= h * w + 16) fault_or(sh.fault, SIMAPS_FAULT_ROUNDS);
         if (tid == 0) sh.finT = dist[tv];
         for (int k = tid; k < cells; k += PNT) {
             const float f = dist[k];
@@ -3370,7 +3376,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     }
                     --left;
                     if constexpr (SIMAPS_SPFA_RING > 0)
-                        if (count > ring && lane == 0) sh.fault |= SIMAPS_FAULT_ROUNDS;  // (diagnostic ring overflowed)
+                        if (count > ring && lane == 0) fault_or(sh.fault, SIMAPS_FAULT_ROUNDS);  // (diagnostic ring overflowed)
                     if (min(count, left) <= 0) break;
                     continue;
                     }
@@ -3488,7 +3494,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     second = nsecond;
                     --left;
                     if constexpr (SIMAPS_SPFA_RING > 0)
-                        if (count > ring && lane == 0) sh.fault |= SIMAPS_FAULT_ROUNDS;  // (diagnostic ring overflowed)
+                        if (count > ring && lane == 0) fault_or(sh.fault, SIMAPS_FAULT_ROUNDS);  // (diagnostic ring overflowed)
                     if (min(count, left) <= 0) break;  // (count, left >= 0)
                 }
                 pops = lim - left;
@@ -3532,7 +3538,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
             }
         if (lane == 0) {
             STAMP_VAL(7, pops);  // (stamp build: tools/path_bench.py reports ns per pop)
-            if (count > 0 && !early) sh.fault |= SIMAPS_FAULT_ROUNDS;  // the pop cap stopped a live queue
+            if (count > 0 && !early) fault_or(sh.fault, SIMAPS_FAULT_ROUNDS);  // the pop cap stopped a live queue
         }
     }
     lds_barrier();
@@ -4348,12 +4354,13 @@ PathKind path_kind(int n, bool small)
 }
 
 // Device scratch of the early-exit path kernels (the SSSP fixpoint, CELLS f32 per query): stream-
-// ordered, taken from the device's default memory pool right before the launch (hipMallocAsync on the
-// launch stream) and handed back right after it (hipFreeAsync on the same stream), so no buffer is
-// ever shared between launches, threads or streams, and nothing is synchronised.  The pool keeps what
-// it was given (release threshold raised once per device), so after the first launches this is a
-// pool hit.  A launch being captured into a graph gets none and takes the compact kernels (same
-// results) instead.
+// ordered, taken from a private memory pool of the device right before the launch
+// (hipMallocFromPoolAsync on the launch stream) and handed back right after it (hipFreeAsync on the
+// same stream), so no buffer is ever shared between launches, threads or streams, and nothing is
+// synchronised.  The pool is this library's own (created once per device, release threshold raised so
+// it keeps what it was given: after the first launches this is a pool hit); the device's default pool,
+// which other libraries in the process allocate from, is left as it was.  A launch being captured into
+// a graph gets none and takes the compact kernels (same results) instead.
 struct PathScratch {
     float *p = nullptr;
     hipStream_t st = nullptr;
@@ -4366,24 +4373,36 @@ struct PathScratch {
     }
 };
 std::once_flag g_pool_once[64];
+hipMemPool_t g_pool[64] = {};
 void path_scratch(PathScratch &ps, hipStream_t st, size_t bytes)
 {
     int dev = 0;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipGetDevice(&dev) != hipSuccess || hipStreamIsCapturing(st, &cap) != hipSuccess ||
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || hipStreamIsCapturing(st, &cap) != hipSuccess ||
         cap != hipStreamCaptureStatusNone)
         return;
-    if (dev >= 0 && dev < 64)
-        std::call_once(g_pool_once[dev], [dev] {
-            hipMemPool_t pool;
-            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-                uint64_t keep = UINT64_MAX;
-                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-            }
-        });
+    // An error left pending by the caller stays pending for the launch's own check: no scratch then
+    // (the compact kernels run), and nothing here clears it.
+    if (hipPeekAtLastError() != hipSuccess) return;
+    std::call_once(g_pool_once[dev], [dev] {
+        hipMemPoolProps props = {};
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipMemPool_t pool = nullptr;
+        if (hipMemPoolCreate(&pool, &props) != hipSuccess) {
+            (void)hipGetLastError();  // (only this call's error: none was pending above)
+            return;
+        }
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        g_pool[dev] = pool;
+    });
+    if (!g_pool[dev]) return;
     void *p = nullptr;
-    if (hipMallocAsync(&p, bytes, st) != hipSuccess) {
-        (void)hipGetLastError();  // (no scratch: the compact kernels run instead)
+    if (hipMallocFromPoolAsync(&p, bytes, g_pool[dev], st) != hipSuccess) {
+        (void)hipGetLastError();  // (only this call's error; no scratch: the compact kernels run instead)
         return;
     }
     ps.p = (float *)p;

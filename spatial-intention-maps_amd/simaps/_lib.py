@@ -103,11 +103,30 @@ def _load(path=LIB_PATH):
     L.simaps_grid_path.restype = i32
     L.simaps_fault_status.argtypes = [i32]
     L.simaps_fault_status.restype = i32
-    if L.simaps_abi_version() != ABI_VERSION and os.environ.get('SIMAPS_AB_OLD_ABI') != str(L.simaps_abi_version()):
-        # (SIMAPS_AB_OLD_ABI=<n>: tools/ab_bench.sh timing an older revision's get_state, whose
-        # signature is unchanged; never set by the product path)
-        raise ImportError('libsimaps ABI version mismatch')
+    v = L.simaps_abi_version()
+    if v != ABI_VERSION:
+        if os.environ.get('SIMAPS_AB_OLD_ABI') != str(v):
+            raise ImportError('libsimaps ABI version mismatch: %s has %d, this binding is %d' % (path, v, ABI_VERSION))
+        # SIMAPS_AB_OLD_ABI=<n>: tools/ab_bench.sh timing an older revision's get_state, whose
+        # signature is unchanged.  Only the entry points a bench render needs stay callable; any other
+        # raises instead of being called with this revision's argument list.
+        return _OldAbi(L, v)
     return L
+
+
+class _OldAbi:
+    """An older revision's library bound for an A/B timing only (see _load)."""
+    ALLOWED = ('simaps_abi_version', 'simaps_last_error', 'simaps_fault_status', 'simaps_num_channels',
+               'simaps_get_state')
+
+    def __init__(self, L, version):
+        self._L, self._v = L, version
+
+    def __getattr__(self, name):
+        if name in self.ALLOWED:
+            return getattr(self._L, name)
+        raise SimapsError('%s is not callable on the ABI-%d library loaded for an A/B timing (SIMAPS_AB_OLD_ABI); '
+                          'only %s are' % (name, self._v, ', '.join(self.ALLOWED)))
 
 
 lib = _load()

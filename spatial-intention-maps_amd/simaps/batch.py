@@ -212,6 +212,11 @@ class StateBatch:
         self._rec = None
         self._map_ver = np.zeros(self.N, dtype=np.int64)
         self._rec_ver = np.full(self.N, -1, dtype=np.int64)
+        # slots whose maps a captured ingest graph may change on any replay, unseen by the host
+        # versions above: their cached records are never served (always a miss, full SSSP)
+        self._replayed = np.zeros(self.N, dtype=bool)
+        # the last launch that wrote or read the cache: every next one on another stream waits for it
+        self._rec_ev = None
 
     def set_descriptors(self, scenes):
         """Upload a new per-step scene descriptor (poses, controller state, paths)."""
@@ -362,6 +367,8 @@ class StateBatch:
             dbg = _lib.Debug(*(debug[k].data_ptr() if debug.get(k) is not None else None
                                for k in ('cspace', 'sources', 'dist', 'status')), None if rec is None else rec.data_ptr())
         s, cur = launch_stream(self.device, stream)
+        if rec is not None:
+            self._rec_wait(s)
         _lib.check(_lib.lib.simaps_get_state(
             self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d),
             _lib.ptr(self.paths_d), _lib.ptr(self.occupancy), _lib.ptr(self.overhead), _lib.ptr(out),
@@ -369,6 +376,8 @@ class StateBatch:
             None if dbg is None else dbg, _lib.stream_handle(s)))
         hold(s, cur, out, agents_d, self.envs_d, self.robots_d, self.paths_d, self.occupancy, self.overhead, rec,
              *(debug.values() if debug else ()))
+        if rec is not None:
+            self._rec_record(s)
         if rec is not None:  # every rendered slot's receptacle array is now its current map's
             sl = np.arange(self.N) if slots is None else np.asarray(list(slots), dtype=np.int64)
             self._rec_ver[sl] = self._map_ver[sl]
@@ -389,11 +398,36 @@ class StateBatch:
         if n == 0 or Q == 0:
             return out
         s, cur = launch_stream(self.device, stream)
+        if _rec is not None:
+            self._rec_wait(s)
         _lib.check(_lib.lib.simaps_sp_distance(
             self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d), _lib.ptr(self.occupancy),
             _lib.ptr(src), _lib.ptr(tgt), Q, _lib.ptr(out), _lib.ptr(_rec), _lib.stream_handle(s)))
         hold(s, cur, src, tgt, out, agents_d, self.envs_d, self.robots_d, self.occupancy, _rec)
+        if _rec is not None:
+            self._rec_record(s)
         return out
+
+    def _rec_wait(self, s):
+        """Order a launch on stream `s` that writes or reads the receptacle cache after the previous
+        such launch (on whatever stream it ran): render() and the miss path write records, the lookup
+        reads them, and the caller never sees the buffer to order these itself.  Chained: each user
+        waits for the one before, so all of them are ordered.  (Inside a graph capture the capture's
+        own stream order applies; an event recorded outside it cannot be waited on.)"""
+        if self._rec_ev is None:
+            return
+        with torch.cuda.stream(s):
+            if torch.cuda.is_current_stream_capturing():
+                return
+        s.wait_event(self._rec_ev)
+
+    def _rec_record(self, s):
+        with torch.cuda.stream(s):
+            if torch.cuda.is_current_stream_capturing():
+                return
+        ev = torch.cuda.Event()
+        ev.record(s)
+        self._rec_ev = ev
 
     def enable_receptacle_cache(self):
         """Allocate the receptacle distance cache (one simaps_rec_cache_bytes record per map slot): from
@@ -424,7 +458,7 @@ class StateBatch:
         if not cache:
             return self.shortest_path_distances(self._slot_rec_xy[sl], tgt, slots=slots, stream=stream)
         rec = self.enable_receptacle_cache()
-        hit = self._rec_ver[sl] == self._map_ver[sl]
+        hit = (self._rec_ver[sl] == self._map_ver[sl]) & ~self._replayed[sl]
         Q = tgt.shape[1]
         s, cur = launch_stream(self.device, stream)
         with torch.cuda.stream(s):  # (every launch, copy and allocation below on the launch stream)
@@ -449,9 +483,11 @@ class StateBatch:
                     agents_d, m = self.subset_descriptor(rs_) if (slots is not None or rows is not None) \
                         else (self.agents_d, self.N)
                     o = dst if dst is not None else torch.empty((m, Q), dtype=torch.float64, device=self.device)
+                    self._rec_wait(s)
                     _lib.check(_lib.lib.simaps_sp_lookup(self.cfg, m, _lib.ptr(agents_d), _lib.ptr(rec), _lib.ptr(th),
                                                          Q, _lib.ptr(o), _lib.stream_handle(s)))
                     hold(s, cur, agents_d, th, o)
+                    self._rec_record(s)
                 if sub is not None:
                     out[sub] = o
         hold(s, cur, rec, tgt, out)
@@ -571,6 +607,7 @@ class StateBatch:
         # captured, the eager launches take it too, since a replay may follow any of them.
         if capturing:
             self._zero_mode = True
+            self._replayed[prep['slots']] = True  # (replays change these maps with no host version bump)
         if getattr(self, '_zero_mode', False):
             if getattr(self, '_epoch', 0) != 0:  # keys of earlier eager launches (captured: every replay)
                 self._wait_last_ingest(s)

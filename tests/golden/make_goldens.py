@@ -154,6 +154,9 @@ def run_agent(envs, env, scene, a):
 
 
 def gen_scenes(envs, only=None):
+    # the rotate rounding recorded in each descriptor is THIS host's (the one whose scipy renders the
+    # fixture), not synthetic.make_scene's default; gen_reset / gen_rot_scenes alike
+    host = K.host_rotate_rounding()
     plan = [(c, 2) for c in synthetic.BASELINE_CONFIGS] + \
            [(c, 1) for c in synthetic.CONFIGS if c not in synthetic.BASELINE_CONFIGS and c not in synthetic.MAZE_CONFIGS] + \
            [(c, 2) for c in synthetic.MAZE_CONFIGS]
@@ -162,7 +165,7 @@ def gen_scenes(envs, only=None):
             continue
         arrays = {}
         for e in range(n_envs):
-            scene = synthetic.make_scene(cfg, e)
+            scene = dict(synthetic.make_scene(cfg, e), rotate_rounding=host)
             env = build_env(envs, scene)
             agents = [0, 1] if len(scene['robots']) > 1 else [0]
             arrays['e%d_scene' % e] = np.array(scene_json(scene))

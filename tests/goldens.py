@@ -23,7 +23,8 @@ def scene_cases():
         e = 0
         while 'e%d_scene' % e in z.files:
             scene = json.loads(str(z['e%d_scene' % e]))
-            scene.setdefault('rotate_rounding', 'fma')  # (the round-1/2 fixtures: made on a fused-dgemv host)
+            if 'rotate_rounding' not in scene:  # (make_goldens.py records the rendering host's rounding)
+                raise ValueError('%s e%d: scene descriptor without rotate_rounding' % (os.path.basename(path), e))
             # (robots that have not acted yet carry None paths / target: the reset goldens)
             scene['robots'] = [dict(r, position=tuple(r['position']),
                                     target_ee=None if r['target_ee'] is None else tuple(r['target_ee']),

@@ -281,6 +281,72 @@ def test_receptacle_cache_follows_map_updates(V):
         check('after set_maps')
 
 
+def _rec_check(b, scenes, tgt, tag, **kw):
+    got = b.receptacle_distances(tgt, **kw).cpu().numpy()
+    for n, (e, a) in enumerate(b.agents):
+        ao = O.AgentOracle(scenes[e], a)
+        rec = scenes[e]['receptacle_position']
+        assert got[n].tolist() == [ao.shortest_path_distance(rec, t) for t in tgt[n]], (tag, e, a)
+
+
+def test_receptacle_cache_after_graph_replayed_ingest(V):
+    """an ingest captured into a graph changes the maps on every replay without a
+    host-side version bump.  A render between the capture and a replay must not make the cache serve
+    the pre-replay arrays: slots a captured ingest writes are never cache hits, and the lookups after
+    the replay equal the oracle on the replayed maps."""
+    synthetic, vector_env = V
+    from simaps import batch, camera
+    spec = camera.CAMERAS['forward']
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 680 + e) for e in range(2)]
+    b = batch.StateBatch(scenes)
+    b.enable_receptacle_cache()
+    rs = np.random.RandomState(3)
+    tgt = np.stack([rs.uniform(-0.3, 0.3, (b.N, 40)), rs.uniform(-0.3, 0.3, (b.N, 40))], -1)
+    f = [synthetic.camera_images(scenes[e], a, 'forward', seed=200 + 7 * e + a) for e, a in b.agents]
+    prep = b.prepare_ingest(np.stack([x[0] for x in f]), np.stack([x[1] for x in f]).astype(np.int32))
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        b.launch_ingest(prep)
+    assert b._replayed.all()
+    b.render()                       # fills the cache from the (not yet replayed) maps
+    torch.cuda.synchronize()
+    g.replay()                       # the maps change; no host version moves
+    torch.cuda.synchronize()
+    for n, (e, a) in enumerate(b.agents):
+        r = scenes[e]['robots'][a]
+        O.ingest(scenes[e]['overhead'][a], scenes[e]['occupancy'][a], f[n][0], f[n][1].astype(np.int32),
+                 spec.params(r['position'][0], r['position'][1], r['heading']), spec, synthetic.SEG_IDS,
+                 scenes[e]['receptacle_position'] is not None)
+    _rec_check(b, scenes, tgt, 'after replay')
+    _rec_check(b, scenes, tgt, 'again')  # still a miss: the next replay may change the maps again
+
+
+def test_receptacle_cache_across_streams(V):
+    """the receptacle cache is written by render() and the miss path and read by
+    the lookups; launches on different streams are ordered through the batch's cache event.  A render
+    on a side stream followed at once by lookups on the current stream (and the other way round)
+    equals the oracle."""
+    synthetic, vector_env = V
+    from simaps import batch
+    scenes = [synthetic.make_scene('lifting_4-small_divider', 690 + e) for e in range(16)]
+    b = batch.StateBatch(scenes)
+    b.enable_receptacle_cache()
+    rs = np.random.RandomState(4)
+    tgt = np.stack([rs.uniform(-0.3, 0.3, (b.N, 24)), rs.uniform(-0.3, 0.3, (b.N, 24))], -1)
+    side = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    side_out = b.render(stream=side)
+    assert b._rec_ev is not None and (b._rec_ver == b._map_ver).all()
+    _rec_check(b, scenes, tgt, 'render on side, lookup on current')
+    out = b.receptacle_distances(tgt, stream=side)   # lookups on the side stream ...
+    b.render()                                       # ... then a render on the current one
+    torch.cuda.current_stream().wait_stream(side)
+    _rec_check(b, scenes, tgt, 'after both')
+    torch.cuda.synchronize()
+    assert side_out.shape[0] == b.N and out.shape == (b.N, 24)
+
+
 def test_distance_to_receptacle_dropin(V):
     synthetic, vector_env = V
     scenes = [synthetic.make_scene('lifting_2_throwing_2-large_empty', 70 + e) for e in range(3)]

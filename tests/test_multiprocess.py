@@ -167,3 +167,69 @@ def test_rank_envs_strong_partition():
             assert [e for b in blocks for e in b] == list(range(total))
             sizes = [len(b) for b in blocks]
             assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT')}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, capture_output=True, text=True,
+                       env=env, timeout=timeout)
+    lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
+    return p.returncode, [json.loads(l) for l in lines], p.stderr
+
+
+@pytest.mark.timeout(300)
+def test_bench_main_spawns_its_own_ranks():
+    """`bench.py --gpus 2` without a launcher starts its two ranks itself
+    (the reference's collector spawns its own workers, train_multiprocess.py:217-228) and the line
+    reports both: n_gpus == distributed.world_size == 2, one row per rank, one line in total.  The
+    real main() runs end to end with the CPU stand-in launch (--standin) over gloo."""
+    rc, lines, err = _run_bench(['--gpus', '2', '--standin', '--steps', '3', '--warmup', '1', '--envs', '2'])
+    assert rc == 0, err
+    assert len(lines) == 1, lines
+    res = lines[0]
+    assert res['n_gpus'] == 2 and res['distributed']['world_size'] == 2
+    assert res['distributed']['backend'] == 'gloo' and res['distributed']['launcher'] == 'spawn'
+    assert [r['rank'] for r in res['distributed']['ranks']] == [0, 1]
+    assert [r['env_range'] for r in res['distributed']['ranks']] == [[0, 1], [2, 3]]
+    assert res['config']['stacks_per_step'] == 2 * 2 * 4 and res['steps'] == 3
+    assert res['data'].startswith('STANDIN') and 'cpu_baseline' not in res
+
+
+@pytest.mark.timeout(300)
+def test_bench_main_single_rank_line():
+    """--gpus 1 (and no --gpus) runs in-process: world 1, no process group, launcher 'single'."""
+    for extra in (['--gpus', '1'], []):
+        rc, lines, err = _run_bench(extra + ['--standin', '--steps', '2', '--warmup', '1', '--envs', '1',
+                                             '--no-cpu-baseline'])
+        assert rc == 0, err
+        assert len(lines) == 1
+        res = lines[0]
+        assert res['n_gpus'] == 1 and res['distributed']['world_size'] == 1
+        assert res['distributed']['backend'] is None and res['distributed']['launcher'] == 'single'
+
+
+def test_bench_refuses_mismatched_requests():
+    """--gpus differing from a launcher's WORLD_SIZE, or more ranks than visible GPUs without
+    --shared-gpu, exits non-zero with a message before any timed work."""
+    sys.path.insert(0, ROOT)
+    import bench
+    with pytest.raises(SystemExit, match='WORLD_SIZE=2'):
+        bench.resolve_world(3, {'WORLD_SIZE': '2'}, 8)
+    with pytest.raises(SystemExit, match='2 ranks requested but 1 GPU'):
+        bench.resolve_world(2, {}, 1)
+    with pytest.raises(SystemExit, match='>= 1'):
+        bench.resolve_world(0, {}, 8)
+    assert bench.resolve_world(2, {}, 1, shared_gpu=True) == ('spawn', 2)
+    assert bench.resolve_world(8, {}, 8) == ('spawn', 8)
+    assert bench.resolve_world(None, {'WORLD_SIZE': '4'}, 8) == ('external', 4)
+    assert bench.resolve_world(4, {'WORLD_SIZE': '4'}, 8) == ('external', 4)
+    assert bench.resolve_world(None, {}, 1) == ('single', 1)
+    assert bench.resolve_world(1, {}, 0, standin=True) == ('single', 1)
+    # end to end: this container has no GPU, so two real ranks are refused, non-zero, no line
+    rc, lines, err = _run_bench(['--gpus', '2', '--steps', '1', '--warmup', '0'])
+    assert rc != 0 and not lines and 'GPU(s) visible' in err
+    rc, lines, err = _run_bench(['--gpus', '3', '--standin'], env_extra={'WORLD_SIZE': '2', 'RANK': '0'})
+    assert rc != 0 and not lines and 'WORLD_SIZE=2' in err

@@ -68,6 +68,25 @@ def test_rotate_roundings_differ_on_the_goldens():
         assert 0.02 < diff[:1500].mean() < 0.1, diff[:1500].mean()
 
 
+def test_scene_descriptors_record_their_rounding():
+    """every committed scene descriptor carries the rotate rounding of the host
+    whose reference run rendered it (make_goldens.py records K.host_rotate_rounding(), never
+    synthetic.make_scene's default), so the loader needs no default and a regeneration with new
+    seeds cannot produce fixtures whose label contradicts their content."""
+    import glob
+    import json
+    n = 0
+    for f in sorted(glob.glob(os.path.join(G.GOLDEN, 'scene_*.npz'))):
+        z = np.load(f, allow_pickle=False)
+        for k in z.files:
+            if k.endswith('_scene'):
+                assert json.loads(str(z[k])).get('rotate_rounding') in K.ROTATE_ROUNDINGS, (os.path.basename(f), k)
+                n += 1
+    assert n >= 27 + 14 + 4
+    src = open(os.path.join(G.GOLDEN, 'make_goldens.py')).read()
+    assert "dict(synthetic.make_scene(cfg, e), rotate_rounding=host)" in src
+
+
 def test_host_rotate_rounding_is_a_known_form():
     assert K.host_rotate_rounding() in K.ROTATE_ROUNDINGS
 
