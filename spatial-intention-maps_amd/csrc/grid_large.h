@@ -1,0 +1,414 @@
+// GridGraph on grids whose free cells span more than the LDS-resident window (include/simaps.h
+// SIMAPS_MAX_ROOM_CELLS / SIMAPS_MAX_ROOM_W): the reference's GridGraph(grid) takes any C-contiguous
+// uint8 grid (shortest_paths.pyx:24-38).  Included by simaps.hip inside its device namespace; the
+// C ABI (simaps_sssp_grid / simaps_grid_path) dispatches here when a window does not fit.
+//
+// Same algorithm as the LDS kernels, with the arrays in global memory (L2-resident for grids up to a
+// few Mcells) and one workgroup per query:
+//   gl_sssp_kernel  the float32 fixpoint by directional sweeps (4 waves: down / up / right / left,
+//                   each over 64-cell strips of its lines, 16 lines prefetched ahead); every write is
+//                   an atomic min(cell, fl(d_u + w)) of a real edge, so the unique fixpoint -- the
+//                   reference SPFA's distances (pyx:69-114), bit for bit -- is reached whatever the
+//                   interleaving, and a round in which no sweep finds a candidate below the value it
+//                   read proves it (values only fall; in a round without writes every read is exact).
+//   gl_path_kernel  one wave per query: the exact SPFA replay (edge order, SLF swap, pyx:89-107) with
+//                   the early exit of the LDS kernels (it stops once every vertex of the target's
+//                   parent chain holds its fixpoint distance: no parent on it can change any more),
+//                   the parent walk, approximate_polygon(tolerance=1) and the line-of-sight pruning
+//                   (pyx:121-154).  The SPFA is serial by definition; each pop is one round trip to L2.
+// Padded layout per query: (wh + 2) rows x pitch = ww + 2 columns, border and blocked cells -inf,
+// free cells +inf until reached.
+
+constexpr int GL_NT = 256;  // gl_sssp_kernel: one wave per sweep direction
+constexpr int GL_PF = 16;   // lines prefetched ahead in a sweep strip
+constexpr int GL_INQ = 16;  // pin bit 4: in the queue (bits 0-3: 1 + direction of the parent edge)
+
+struct GlDims {
+    int wh, ww, pitch;
+    long cells;
+};
+
+__device__ __forceinline__ GlDims gl_dims(int wh, int ww) { return GlDims{wh, ww, ww + 2, (long)(wh + 2) * (ww + 2)}; }
+
+// Loads that see what other waves (and lanes) of the workgroup wrote through L2: agent scope (the
+// vector L1 is not coherent with the atomics / stores of other waves).
+__device__ __forceinline__ float gl_ld(const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ int gl_ldi(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void gl_st(float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void gl_sti(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// every store / atomic of this wave has reached L2 before the next load issues
+__device__ __forceinline__ void gl_drain() { __builtin_amdgcn_s_waitcnt(0); }
+
+// One sweep of one wave over every line of the window (DIR 0 down, 1 up: lines = rows; 2 right,
+// 3 left: lines = columns), 64 cells of each line at a time (strip s0).  A cell of line l is relaxed
+// from the 3 cells of line l -1 (in sweep order): straight (weight 1) and the two diagonals (float32
+// sqrt(2)).  Inside a strip the previous line's values pass between lanes by DPP; lane 0 / lane 63
+// read their outer neighbour from memory (the previous strip's value, final for this sweep, or the
+// next strip's, from before it) -- a stale value is still some path's length, so every write remains
+// a valid relaxation.  Returns true if some candidate was below the value read.
+template <int DIR>
+__device__ bool gl_sweep(float *D, const GlDims g)
+{
+    constexpr bool VERT = DIR < 2, FWD = (DIR & 1) == 0;
+    const int lane = threadIdx.x & 63;
+    const int N = VERT ? g.wh : g.ww, L = VERT ? g.ww : g.wh;
+    const long sl = VERT ? g.pitch : 1, sa = VERT ? 1 : g.pitch;
+    bool chg = false;
+    for (int s0 = 0; s0 < L; s0 += 64) {
+        const int c = s0 + lane;
+        const bool act = c < L;
+        const int cc = act ? c : L;  // inactive lanes alias the border cell after the line (-inf)
+        const long own = (1 + cc) * sa;
+        // the outer neighbour a strip edge reads (lane 0: c - 1, lane 63: c + 1); others re-read their own cell
+        const long xo = (1 + (lane == 0 ? c - 1 : (lane == 63 && act) ? c + 1 : cc)) * sa;
+        const float one = act ? 1.0f : INFINITY, s2 = act ? SQRT2F : INFINITY;
+        auto base = [&](int t) { return D + (long)(1 + (FWD ? t : N - 1 - t)) * sl; };
+        float Rr[GL_PF], Xr[GL_PF];
+#pragma unroll
+        for (int j = 0; j < GL_PF; j++)
+            if (j < N) {
+                Rr[j] = gl_ld(base(j) + own);
+                Xr[j] = gl_ld(base(j) + xo);
+            }
+        // the previous line: this lane's value (sign trick: -inf = blocked passes on nothing, as |.|
+        // = +inf) and its outer neighbour's
+        float p = INFINITY, xp = INFINITY;
+        for (int t0 = 0; t0 < N; t0 += GL_PF) {
+#pragma unroll
+            for (int j = 0; j < GL_PF; j++) {
+                const int t = t0 + j;
+                if (t < N) {  // (wave-uniform)
+                    const float R = Rr[j], X = Xr[j];
+                    if (t + GL_PF < N) {
+                        Rr[j] = gl_ld(base(t + GL_PF) + own);
+                        Xr[j] = gl_ld(base(t + GL_PF) + xo);
+                    }
+                    const float pl = lane == 0 ? xp : from_prev_lane(p);
+                    const float pr = lane == 63 ? xp : from_next_lane(p);
+                    const float m = fminf(fminf(fabsf(p) + one, fabsf(pl) + s2), fabsf(pr) + s2);
+                    if (m < R) {  // (blocked / border cells hold -inf: never)
+                        atomicMin(reinterpret_cast<int *>(base(t) + own), __float_as_int(m));  // m >= 0: int order
+                        chg = true;
+                    }
+                    p = act ? fminf(m, R) : -INFINITY;
+                    xp = X;
+                }
+            }
+        }
+    }
+    return __ballot(chg) != 0;
+}
+
+// Batched GridGraph(grid).shortest_path_image(source) for windows of any size.  scratch: one padded
+// array per query (the fixpoint: gl_path_kernel's early-exit reference); out (may be null): the
+// [H, W] image as pyx:110-112 leaves it (-1 unreachable, 0 at the source even when blocked).
+__global__ void __launch_bounds__(GL_NT) gl_sssp_kernel(int H, int W, const uint8_t *__restrict__ grids, long grid_stride,
+                                                       const int32_t *__restrict__ sources, int wi0, int wj0, int wh, int ww,
+                                                       float *scratch, long scratch_stride, float *__restrict__ out,
+                                                       unsigned *fault)
+{
+    __shared__ int changed[3];
+    const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6;
+    const uint8_t *grid = grids + b * grid_stride;
+    const GlDims g = gl_dims(wh, ww);
+    float *D = scratch + b * scratch_stride;
+    const int si = sources[2 * b], sj = sources[2 * b + 1];
+    const bool s_in = si >= wi0 && si < wi0 + wh && sj >= wj0 && sj < wj0 + ww && grid[(long)si * W + sj] != 0;
+    const long sq = s_in ? (long)(si - wi0 + 1) * g.pitch + (sj - wj0 + 1) : -1;
+    for (long k = tid; k < g.cells; k += GL_NT) {
+        const int r = (int)(k / g.pitch), c = (int)(k - (long)r * g.pitch);
+        float v = -INFINITY;
+        if (r >= 1 && r <= wh && c >= 1 && c <= ww && grid[(long)(wi0 + r - 1) * W + wj0 + c - 1] != 0)
+            v = k == sq ? 0.0f : INFINITY;
+        gl_st(D + k, v);
+    }
+    if (tid < 3) changed[tid] = 0;
+    gl_drain();
+    __syncthreads();
+    unsigned f = 0;
+    if (s_in) {
+        const long cap = (long)wh * ww + 16;
+        for (long round = 0;; round++) {
+            const bool c = wave == 0 ? gl_sweep<0>(D, g) : wave == 1 ? gl_sweep<1>(D, g)
+                         : wave == 2 ? gl_sweep<2>(D, g) : gl_sweep<3>(D, g);
+            if (c && (tid & 63) == 0) changed[round % 3] = 1;
+            if (tid == 0) changed[(round + 1) % 3] = 0;  // (last read two barriers ago)
+            gl_drain();  // this round's atomics are in L2 before any wave reads for the next one
+            __syncthreads();
+            if (!changed[round % 3]) break;
+            if (round >= cap) {
+                f = SIMAPS_FAULT_ROUNDS;
+                break;
+            }
+        }
+    }
+    if (tid == 0) post_faults(fault, f);
+    if (!out) return;
+    float *o = out + (long)b * H * W;
+    for (long k = tid; k < (long)H * W; k += GL_NT) {
+        const int i = (int)(k / W), j = (int)(k - (long)i * W);
+        float v = (i == si && j == sj) ? 0.0f : -1.0f;
+        const int r = i - wi0, c = j - wj0;
+        if (r >= 0 && r < wh && c >= 0 && c < ww) {
+            const float d = gl_ld(D + (long)(r + 1) * g.pitch + c + 1);
+            if (d >= 0.0f && d != INFINITY) v = d;
+        }
+        o[k] = v;
+    }
+}
+
+// Per-query scratch of gl_path_kernel, in int32 / float32 units of `cells` (padded cells) and `n`
+// (window cells + 1): fix [cells] (gl_sssp_kernel's fixpoint), dist [cells], pin [cells], queue [n]
+// (ring: live entries <= free cells), dense [n], chain [n], stack [2 n].
+__host__ __device__ inline long gl_path_words(int wh, int ww)
+{
+    const long cells = (long)(wh + 2) * (ww + 2), n = (long)wh * ww + 1;
+    return 3 * cells + 5 * n;
+}
+
+// pyx:30 directions: 1 + k in pin bits 0-3; the edge's cell offset in the padded layout
+__device__ __forceinline__ long gl_dir_off(int k, int pitch)
+{
+    const int di = k < 2 ? 0 : (k < 5 ? -1 : 1);
+    const int dj = k < 2 ? (k == 0 ? -1 : 1) : ((k - 2) % 3) - 1;
+    return (long)di * pitch + dj;
+}
+
+// GridGraph(grid).shortest_path(source, target) (pyx:121-154) on windows of any size, one wave per
+// query, after gl_sssp_kernel left the fixpoint from the same source in `fix`.  Output as
+// grid_path_kernel: waypoint cells source first, count or -needed.
+__global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t *__restrict__ grids, long grid_stride,
+                                                    const int32_t *__restrict__ sources, const int32_t *__restrict__ targets,
+                                                    int wi0, int wj0, int wh, int ww, int *scratch, long scratch_stride,
+                                                    int max_pts, int32_t *__restrict__ out_ij, int32_t *__restrict__ out_n,
+                                                    unsigned *fault)
+{
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const uint8_t *grid = grids + b * grid_stride;
+    const GlDims g = gl_dims(wh, ww);
+    const int P = g.pitch;
+    const long n1 = (long)wh * ww + 1;
+    int *base = scratch + b * scratch_stride;
+    const float *fix = reinterpret_cast<const float *>(base);
+    float *dist = reinterpret_cast<float *>(base + g.cells);
+    int *pin = base + 2 * g.cells;
+    int *queue = base + 3 * g.cells;
+    int *dense = queue + n1;
+    int *chain = dense + n1;
+    int *stack = chain + n1;
+    const int si = sources[2 * b], sj = sources[2 * b + 1], ti = targets[2 * b], tj = targets[2 * b + 1];
+    int32_t *o = out_ij + (long)b * max_pts * 2;
+    const bool s_in = si >= wi0 && si < wi0 + wh && sj >= wj0 && sj < wj0 + ww;
+    const bool t_in = ti >= wi0 && ti < wi0 + wh && tj >= wj0 && tj < wj0 + ww;
+    // a source outside the window or blocked has no edges (pyx:56) and a target outside the window is
+    // never reached: the parent walk stops at once and the path is [target]
+    if (!(s_in && t_in && grid[(long)si * W + sj] != 0)) {
+        if (lane == 0) { o[0] = ti; o[1] = tj; out_n[b] = 1; }
+        return;
+    }
+    const long su = (long)(si - wi0 + 1) * P + (sj - wj0 + 1), tv = (long)(ti - wi0 + 1) * P + (tj - wj0 + 1);
+    // (1) SPFA arrays: distances +inf on free cells (the reference's 2 * V: no path reaches it), -inf
+    // on blocked and border cells (never relaxed), pin 0; the queue holds the source (pyx:79-88)
+    for (long k = lane; k < g.cells; k += 64) {
+        const float fv = gl_ld(fix + k);
+        gl_st(dist + k, k == su ? 0.0f : (fv == -INFINITY ? -INFINITY : INFINITY));
+        gl_sti(pin + k, k == su ? GL_INQ : 0);
+    }
+    if (lane == 0) gl_sti(queue, (int)su);
+    gl_drain();
+    unsigned fault_bits = 0;
+    const float finT = gl_ld(fix + tv);  // the target's fixpoint distance (+inf: unreachable, no early exit)
+    const int k8 = lane < 8 ? lane : 8;
+    const long off = lane < 8 ? gl_dir_off(lane, P) : 0;  // lane 8: the popped vertex itself
+    const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
+    long qh = 0, qt = 0, cnt = 1;  // front slot, last slot, live entries
+    const long QR = n1;
+    long pops = 0, lim = finT != INFINITY ? 32 : SIMAPS_POP_CAP, gap = 64;
+    bool early = false;
+    while (cnt > 0) {
+        // (2) pop u; its edges in pyx order on lanes 0-7 (pyx:89-101)
+        const long u = gl_ldi(queue + qh);
+        const long q2 = qh + 1 == QR ? 0 : qh + 1;
+        const long fr = cnt > 1 ? gl_ldi(queue + q2) : -1;  // the next front (queue[head + 1])
+        qh = q2;
+        cnt--;
+        const long v = u + off;
+        const float dv = lane <= 8 ? gl_ld(dist + v) : 0.0f;
+        const int pv = lane <= 8 ? gl_ldi(pin + v) : 0;
+        const float dfr = fr >= 0 ? gl_ld(dist + fr) : 0.0f;  // its distance before this pop
+        const float du = __shfl(dv, 8);
+        const float nd = du + wl;
+        const bool imp = lane < 8 && nd < dv;
+        if (imp) {
+            gl_st(dist + v, nd);
+            gl_sti(pin + v, GL_INQ | (k8 + 1));
+        }
+        if (lane == 8) gl_sti(pin + u, pv & 15);  // in_queue[u] = 0 (pyx:92)
+        // (3) pushes in edge order with the SLF swap against the front (pyx:102-107); the front's
+        // distance as of each edge: lowered by this pop's own edge to it, if any
+        uint64_t todo = __ballot(imp && ((pv & GL_INQ) == 0 || v == fr));
+        long f = fr;
+        float df = dfr;
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const long vk = __shfl(v, k);
+            const float ndk = __shfl(nd, k);
+            const int pk = __shfl(pv, k);
+            if (vk == f) {  // the front itself improved (already in the queue: no push)
+                df = ndk;
+                continue;
+            }
+            (void)pk;
+            qt = qt + 1 == QR ? 0 : qt + 1;
+            cnt++;
+            if (cnt == 1) {  // (the queue was empty: tail == head + 1)
+                if (lane == 0) gl_sti(queue + qt, (int)vk);
+                f = vk;
+                df = ndk;
+            } else if (ndk < df) {
+                if (lane == 0) {
+                    gl_sti(queue + qh, (int)vk);
+                    gl_sti(queue + qt, (int)f);
+                }
+                f = vk;
+                df = ndk;
+            } else if (lane == 0) {
+                gl_sti(queue + qt, (int)vk);
+            }
+        }
+        gl_drain();
+        if (++pops < lim) continue;
+        if (pops >= SIMAPS_POP_CAP) {
+            if (cnt > 0) fault_bits |= SIMAPS_FAULT_ROUNDS;  // the cap stopped a live queue
+            break;
+        }
+        // (4) early exit: the target at its fixpoint distance and then every vertex of its chain
+        bool ok = gl_ld(dist + tv) == finT;
+        for (long w = tv; ok && w != su;) {
+            const long m = lane == 0 ? w : w;  // (uniform)
+            ok = gl_ld(dist + m) == gl_ld(fix + m);
+            const int p = gl_ldi(pin + m) & 15;
+            if (!p) { ok = false; break; }
+            w = m - gl_dir_off(p - 1, P);
+        }
+        if (ok) { early = true; break; }
+        lim = pops + gap;
+        gap = gap < (1 << 20) ? 2 * gap : gap;
+    }
+    (void)early;
+    // (5) dense path: parents from the target back to the source (pyx:131-138)
+    int nd = 0;
+    if (lane == 0) {
+        long w = tv;
+        dense[nd++] = (int)w;
+        while (w != su) {
+            const int p = gl_ldi(pin + w) & 15;
+            if (!p) break;
+            w -= gl_dir_off(p - 1, P);
+            dense[nd++] = (int)w;
+        }
+    }
+    nd = __shfl(nd, 0);
+    gl_drain();
+    auto rc_of = [&](int q, int &r, int &c) { r = q / P - 1 + wi0; c = q % P - 1 + wj0; };
+    // (6) approximate_polygon(dense, tolerance=1) (skimage 0.18.3 measure/_polygon.py), as path_core
+    for (int k = lane; k < nd; k += 64) chain[k] = (k == 0 || k == nd - 1) ? 1 : 0;
+    gl_drain();
+    {
+        long sp = 1, iters = 0;
+        if (lane == 0) { stack[0] = 0; stack[1] = nd - 1; }
+        gl_drain();
+        while (sp > 0 && ++iters <= 2L * nd) {
+            sp--;
+            const int start = gl_ldi(stack + 2 * sp), end = gl_ldi(stack + 2 * sp + 1);
+            int r0, c0, r1, c1;
+            rc_of(gl_ldi(dense + start), r0, c0);
+            rc_of(gl_ldi(dense + end), r1, c1);
+            const long dr = r1 - r0, dc = c1 - c0;
+            const double ang = -atan2((double)dr, (double)dc);
+            const double sn = sin(ang), cs = cos(ang);
+            const double sdist = (double)c0 * sn + (double)r0 * cs;
+            double best = -1.0;
+            int besti = -1;
+            for (int k = start + 1 + lane; k < end; k += 64) {
+                int rr, cc;
+                rc_of(gl_ldi(dense + k), rr, cc);
+                const long dr0 = rr - r0, dc0 = cc - c0, dr1 = rr - r1, dc1 = cc - c1;
+                const bool perp = dr0 * dr + dc0 * dc > 0 && -dr1 * dr - dc1 * dc > 0;
+                double d;
+                if (perp) d = fabs(((double)rr * cs + (double)cc * sn) - sdist);
+                else d = fmin(sqrt((double)(dc0 * dc0 + dr0 * dr0)), sqrt((double)(dc1 * dc1 + dr1 * dr1)));
+                if (d > best) { best = d; besti = k; }
+            }
+            for (int o2 = 32; o2 > 0; o2 >>= 1) {  // wave argmax, first index on ties (np.argmax)
+                const double ob = __shfl_xor(best, o2);
+                const int oi = __shfl_xor(besti, o2);
+                if (ob > best || (ob == best && oi >= 0 && (besti < 0 || oi < besti))) { best = ob; besti = oi; }
+            }
+            if (best > 1.0) {
+                if (lane == 0) {
+                    gl_sti(stack + 2 * sp, besti);
+                    gl_sti(stack + 2 * sp + 1, end);
+                    gl_sti(stack + 2 * sp + 2, start);
+                    gl_sti(stack + 2 * sp + 3, besti);
+                    gl_sti(chain + besti, 1);
+                }
+                sp += 2;
+            }
+            gl_drain();
+        }
+    }
+    // (7) sparse points (chain-flagged, in order) into `stack`, then the line-of-sight pruning on the
+    // grid (pyx:143-150: a line is blocked by any cell != 1) and the reversal (pyx:152)
+    int *sparse = stack;
+    int m = 0;
+    for (int k0 = 0; k0 < nd; k0 += 64) {
+        const int k = k0 + lane;
+        const bool fl = k < nd && gl_ldi(chain + k);
+        const uint64_t bm = __ballot(fl);
+        if (fl) gl_sti(sparse + m + __popcll(bm & ((1ull << lane) - 1)), gl_ldi(dense + k));
+        m += __popcll(bm);
+    }
+    gl_drain();
+    int *kept = chain;  // (chain flags are no longer read)
+    int cnt_out = 0;
+    if (m > 0) {
+        if (lane == 0) gl_sti(kept, gl_ldi(sparse));
+        cnt_out = 1;
+        for (int k = 1; k < m - 1; k++) {
+            gl_drain();
+            int ra, ca, rb, cb;
+            rc_of(gl_ldi(kept + cnt_out - 1), ra, ca);
+            rc_of(gl_ldi(sparse + k + 1), rb, cb);
+            const int len = max(abs(rb - ra), abs(cb - ca)) + 1;
+            bool blocked = false;
+            for (int t = lane; t < len; t += 64) {
+                int pr, pc;
+                line_pixel(ra, ca, rb, cb, t, pr, pc);
+                blocked |= grid[(long)pr * W + pc] != 1;
+            }
+            if (__ballot(blocked) != 0) {
+                if (lane == 0) gl_sti(kept + cnt_out, gl_ldi(sparse + k));
+                cnt_out++;
+            }
+        }
+        if (m > 1) {
+            if (lane == 0) gl_sti(kept + cnt_out, gl_ldi(sparse + m - 1));
+            cnt_out++;
+        }
+    }
+    gl_drain();
+    if (cnt_out > max_pts) {
+        if (lane == 0) out_n[b] = -cnt_out;
+    } else {
+        for (int k = lane; k < cnt_out; k += 64) {
+            int r, c;
+            rc_of(gl_ldi(kept + cnt_out - 1 - k), r, c);
+            o[2 * k] = r;
+            o[2 * k + 1] = c;
+        }
+        if (lane == 0) out_n[b] = cnt_out;
+    }
+    if (lane == 0) post_faults(fault, fault_bits);
+}

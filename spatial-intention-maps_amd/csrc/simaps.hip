@@ -4199,6 +4199,8 @@ __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
     }
 }
 
+#include "grid_large.h"
+
 }  // namespace
 
 // =================================================================================================
@@ -4374,16 +4376,16 @@ struct PathScratch {
 };
 std::once_flag g_pool_once[64];
 hipMemPool_t g_pool[64] = {};
-void path_scratch(PathScratch &ps, hipStream_t st, size_t bytes)
+bool pool_alloc(PathScratch &ps, hipStream_t st, size_t bytes)
 {
     int dev = 0;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || hipStreamIsCapturing(st, &cap) != hipSuccess ||
         cap != hipStreamCaptureStatusNone)
-        return;
+        return false;
     // An error left pending by the caller stays pending for the launch's own check: no scratch then
     // (the compact kernels run), and nothing here clears it.
-    if (hipPeekAtLastError() != hipSuccess) return;
+    if (hipPeekAtLastError() != hipSuccess) return false;
     std::call_once(g_pool_once[dev], [dev] {
         hipMemPoolProps props = {};
         props.allocType = hipMemAllocationTypePinned;
@@ -4399,15 +4401,38 @@ void path_scratch(PathScratch &ps, hipStream_t st, size_t bytes)
         (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
         g_pool[dev] = pool;
     });
-    if (!g_pool[dev]) return;
+    if (!g_pool[dev]) return false;
     void *p = nullptr;
     if (hipMallocFromPoolAsync(&p, bytes, g_pool[dev], st) != hipSuccess) {
-        (void)hipGetLastError();  // (only this call's error; no scratch: the compact kernels run instead)
-        return;
+        (void)hipGetLastError();  // (only this call's error)
+        return false;
     }
     ps.p = (float *)p;
     ps.st = st;
+    return true;
 }
+// the early-exit path kernels' scratch: none (the compact kernels run instead) when it cannot be had
+void path_scratch(PathScratch &ps, hipStream_t st, size_t bytes) { (void)pool_alloc(ps, st, bytes); }
+
+// the LDS-resident GridGraph kernels' window limit (include/simaps.h); beyond it grid_large.h
+bool window_fits_lds(int wh, int ww)
+{
+    return ww <= SIMAPS_MAX_ROOM_W && wh <= MAX_ROWS && (wh + 2) * ((ww + 2) | 1) <= SIMAPS_MAX_ROOM_CELLS;
+}
+
+// scratch of the large-window GridGraph kernels (stream-ordered, the library's pool); they have no
+// other path, so a launch being captured into a graph is refused instead
+int large_scratch(PathScratch &ps, hipStream_t st, size_t bytes, const char *what)
+{
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) != hipSuccess) return fail(SIMAPS_EHIP, "hipStreamIsCapturing failed");
+    if (cap != hipStreamCaptureStatusNone)
+        return fail(SIMAPS_EUNSUPPORTED, "%s on a window beyond the LDS-resident limit cannot be captured into a graph "
+                    "(its scratch is taken in stream order per launch)", what);
+    if (!pool_alloc(ps, st, bytes)) return fail(SIMAPS_EHIP, "%s: no device scratch of %zu bytes", what, bytes);
+    return 0;
+}
+
 
 int check_cfg(const simaps_config *c)
 {
@@ -4702,11 +4727,22 @@ int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *s
     if (!grids || !sources || !targets || !out_ij || !out_count) return fail(SIMAPS_EINVAL, "NULL buffer");
     if (wh <= 0 || ww <= 0 || wi0 < 0 || wj0 < 0 || wi0 + wh > H || wj0 + ww > W)
         return fail(SIMAPS_EINVAL, "window outside the grid");
-    if (ww > SIMAPS_MAX_ROOM_W || wh > MAX_ROWS || (wh + 2) * ((ww + 2) | 1) > SIMAPS_MAX_ROOM_CELLS)
-        return fail(SIMAPS_EUNSUPPORTED, "window %dx%d exceeds the LDS-resident limit", wh, ww);
+    const hipStream_t st = (hipStream_t)stream;
+    if (!window_fits_lds(wh, ww)) {  // any larger window: the global-memory kernels (grid_large.h)
+        if (const int rc = pending_faults()) return rc;
+        const long words = gl_path_words(wh, ww);
+        PathScratch ps;
+        if (const int rc = large_scratch(ps, st, (size_t)B * words * sizeof(int), "grid_path")) return rc;
+        hipLaunchKernelGGL(gl_sssp_kernel, dim3(B), dim3(GL_NT), 0, st, H, W, grids, (long)H * W, sources, wi0, wj0, wh,
+                           ww, ps.p, words, nullptr, g_fault_dev);
+        hipLaunchKernelGGL(gl_path_kernel, dim3(B), dim3(64), 0, st, H, W, grids, (long)H * W, sources, targets, wi0, wj0,
+                           wh, ww, reinterpret_cast<int *>(ps.p), words, max_points, out_ij, out_count, g_fault_dev);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return fail(SIMAPS_EHIP, "grid_path (large window) launch: %s", hipGetErrorString(e));
+        return 0;
+    }
     if (const int rc = pending_faults()) return rc;
     const bool small = (wh + 2) * ((ww + 2) | 1) <= PATH_SMALL_CELLS;
-    const hipStream_t st = (hipStream_t)stream;
     const PathKind kind = path_kind(B, small);
     PathScratch ps;
     if (kind == PK_EARLY) path_scratch(ps, st, (size_t)B * SIMAPS_MAX_ROOM_CELLS * sizeof(float));
@@ -4738,8 +4774,19 @@ int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *s
     if (!grids || !sources || !dists) return fail(SIMAPS_EINVAL, "NULL buffer");
     if (wh <= 0 || ww <= 0 || wi0 < 0 || wj0 < 0 || wi0 + wh > H || wj0 + ww > W)
         return fail(SIMAPS_EINVAL, "window outside the grid");
-    if (ww > SIMAPS_MAX_ROOM_W || wh > MAX_ROWS || (wh + 2) * ((ww + 2) | 1) > SIMAPS_MAX_ROOM_CELLS)
-        return fail(SIMAPS_EUNSUPPORTED, "window %dx%d exceeds the LDS-resident limit", wh, ww);
+    if (H > 32767 || W > 32767) return fail(SIMAPS_EINVAL, "grid %dx%d too large", H, W);
+    if (!window_fits_lds(wh, ww)) {  // any larger window: the global-memory sweeps (grid_large.h)
+        if (const int rc = pending_faults()) return rc;
+        const hipStream_t st = (hipStream_t)stream;
+        const long cells = (long)(wh + 2) * (ww + 2);
+        PathScratch ps;
+        if (const int rc = large_scratch(ps, st, (size_t)B * cells * sizeof(float), "sssp_grid")) return rc;
+        hipLaunchKernelGGL(gl_sssp_kernel, dim3(B), dim3(GL_NT), 0, st, H, W, grids, (long)H * W, sources, wi0, wj0, wh,
+                           ww, ps.p, cells, dists, g_fault_dev);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return fail(SIMAPS_EHIP, "sssp_grid (large window) launch: %s", hipGetErrorString(e));
+        return 0;
+    }
     if (const int rc = pending_faults()) return rc;
     hipLaunchKernelGGL(sssp_grid_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, H, W, grids, sources, dists, wi0,
                        wj0, wh, ww, g_fault_dev);

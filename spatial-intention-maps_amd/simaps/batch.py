@@ -652,7 +652,8 @@ def sssp_grid(grids, sources, window=None, stream=None):
     """Batched GridGraph(grid).shortest_path_image(source) on device.
 
     grids: uint8 tensor [B, H, W] (device), sources: int32 [B, 2].  window = (i0, j0, h, w) that
-    contains every free cell (defaults to the whole grid, which must then fit the LDS limit)."""
+    contains every free cell (defaults to the whole grid).  Windows beyond the LDS-resident limit
+    run the global-memory kernels (same results)."""
     B, H, W = grids.shape
     if window is None:
         window = (0, 0, H, W)
@@ -666,11 +667,9 @@ def sssp_grid(grids, sources, window=None, stream=None):
     return out
 
 
-def grid_paths(grids, sources, targets, window=None, max_points=256, stream=None):
-    """Batched GridGraph(grid).shortest_path(source, target) (pyx:121-154) on device.
-
-    grids: uint8 tensor [B, H, W] (device), sources / targets: int [B, 2] cells.  Returns B lists of
-    (row, col) waypoints, source first, exactly the reference's (same SPFA parents)."""
+def launch_grid_paths(grids, sources, targets, window=None, max_points=256, stream=None):
+    """The device half of grid_paths(): one call, results left on the device as (ij [B, max_points, 2]
+    int32, count [B] int32; count = -needed if max_points is too small)."""
     B, H, W = grids.shape
     if window is None:
         window = (0, 0, H, W)
@@ -678,19 +677,36 @@ def grid_paths(grids, sources, targets, window=None, max_points=256, stream=None
     tgt = torch.as_tensor(targets).to(device=grids.device, dtype=torch.int32).contiguous()
     if tuple(src.shape) != (B, 2) or tuple(tgt.shape) != (B, 2):
         raise ValueError('sources and targets must be [%d, 2]' % B)
-    if B == 0:
-        return []
     ij = torch.empty((B, max_points, 2), dtype=torch.int32, device=grids.device)
     cnt = torch.empty((B,), dtype=torch.int32, device=grids.device)
+    if B == 0:
+        return ij, cnt
     g = grids.contiguous()
     s, cur = launch_stream(grids.device, stream)
     _lib.check(_lib.lib.simaps_grid_path(B, H, W, _lib.ptr(g), _lib.ptr(src), _lib.ptr(tgt), *[int(x) for x in window],
                                          max_points, _lib.ptr(ij), _lib.ptr(cnt), _lib.stream_handle(s)))
     hold(s, cur, g, src, tgt, ij, cnt)
+    return ij, cnt
+
+
+def grid_paths(grids, sources, targets, window=None, max_points=256, stream=None, grow=False):
+    """Batched GridGraph(grid).shortest_path(source, target) (pyx:121-154) on device.
+
+    grids: uint8 tensor [B, H, W] (device), sources / targets: int [B, 2] cells.  Returns B lists of
+    (row, col) waypoints, source first, exactly the reference's (same SPFA parents).  A path with
+    more than max_points waypoints raises RuntimeError, or with grow=True is run again with room for
+    the longest one (the reference's lists have no limit)."""
+    B = grids.shape[0]
+    if B == 0:
+        return []
+    ij, cnt = launch_grid_paths(grids, sources, targets, window, max_points, stream)
+    s, cur = launch_stream(grids.device, stream)
     if s != cur:
         cur.wait_stream(s)
     ij, cnt = ij.cpu().numpy(), cnt.cpu().numpy()
     _lib.check_faults()
     if (cnt < 0).any():
+        if grow:
+            return grid_paths(grids, sources, targets, window, int(-cnt.min()), stream, grow=False)
         raise RuntimeError('a path has %d waypoints > max_points=%d' % (-cnt.min(), max_points))
     return _point_lists(ij, cnt)

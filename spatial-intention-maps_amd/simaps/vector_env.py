@@ -200,8 +200,9 @@ MAX_WINDOW_CELLS, MAX_WINDOW_W = 9024, 120  # SIMAPS_MAX_ROOM_CELLS / SIMAPS_MAX
 
 
 def window_fits(h, w):
-    """Whether an h x w window of free cells fits the LDS-resident SSSP / SPFA kernels (the checks of
-    simaps_sssp_grid / simaps_grid_path)."""
+    """Whether an h x w window of free cells fits the LDS-resident SSSP / SPFA kernels (the rule of
+    simaps_sssp_grid / simaps_grid_path); larger windows run the global-memory kernels
+    (csrc/grid_large.h): same results, slower."""
     return h >= 1 and 1 <= w <= MAX_WINDOW_W and (h + 2) * ((w + 2) | 1) <= MAX_WINDOW_CELLS
 
 
@@ -211,7 +212,9 @@ class GridGraph:
 
     Results are bit-identical to the reference SPFA (the float32 fixpoint is unique, SURVEY.md
     a10).  Like _spfa_with_cache (pyx:116-119) the images are cached per source for the life of
-    the graph.  The free cells must fit the LDS-resident window limit of include/simaps.h."""
+    the graph.  Any 2-D grid, like the reference's (pyx:24-38): when the free cells span a window
+    beyond the LDS-resident limits of include/simaps.h (every reference call site passes a room
+    cspace, which fits), the C ABI runs the global-memory kernels instead (`large` is then True)."""
 
     def __init__(self, grid, device='cuda'):
         g = torch.as_tensor(np.ascontiguousarray(grid) if isinstance(grid, np.ndarray) else grid)
@@ -226,11 +229,7 @@ class GridGraph:
             self.window = (i0, j0, i1 - i0 + 1, j1 - j0 + 1)
         else:
             self.window = (0, 0, 1, 1)
-        if not window_fits(self.window[2], self.window[3]):
-            raise ValueError('GridGraph: the free cells span a %d x %d window; the LDS-resident SSSP / SPFA take '
-                             'windows with (h + 2) * ((w + 2) | 1) <= %d cells and w <= %d (include/simaps.h; every '
-                             'reference call site passes a room cspace, which fits)'
-                             % (self.window[2], self.window[3], MAX_WINDOW_CELLS, MAX_WINDOW_W))
+        self.large = not window_fits(self.window[2], self.window[3])
         self._cache = {}
 
     def _check_source(self, source):
@@ -271,7 +270,7 @@ class GridGraph:
             return []
         grids = self.grid.unsqueeze(0).expand(len(pairs), *self.shape).contiguous()
         return _batch.grid_paths(grids, [p[0] for p in pairs], [p[1] for p in pairs], window=self.window,
-                                 max_points=max(256, self.shape[0] + self.shape[1]), stream=stream)
+                                 max_points=max(256, self.shape[0] + self.shape[1]), stream=stream, grow=True)
 
     def shortest_path_distance(self, source, target):
         """dists[target] from `source` as a Python float (pyx:156-163); -1 if unreachable."""

@@ -148,8 +148,9 @@ def test_path_mode_setter():
 
 
 def test_gridgraph_window_limits_match_header():
-    """The drop-in GridGraph refuses, up front, a grid whose free cells exceed the LDS window limits of
-    include/simaps.h (SIMAPS_MAX_ROOM_CELLS / SIMAPS_MAX_ROOM_W), with the same rule the ABI applies."""
+    """The drop-in GridGraph's `large` flag (the global-memory kernels of csrc/grid_large.h) follows the
+    LDS window limits of include/simaps.h (SIMAPS_MAX_ROOM_CELLS / SIMAPS_MAX_ROOM_W) with the same
+    rule the ABI applies when it picks the kernels."""
     from simaps import vector_env
     txt = open(HEADER).read()
     cells = int(re.search(r'#define SIMAPS_MAX_ROOM_CELLS (\d+)', txt).group(1))

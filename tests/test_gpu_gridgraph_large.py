@@ -1,0 +1,144 @@
+"""GridGraph on grids beyond the LDS-resident window: the reference's
+GridGraph(grid) accepts any C-contiguous uint8 grid (shortest_paths.pyx:24-38); windows larger than
+include/simaps.h's SIMAPS_MAX_ROOM_CELLS / SIMAPS_MAX_ROOM_W run the global-memory kernels of
+csrc/grid_large.h.  Checked bitwise against the reference's own fixtures (the demo.py sample, run
+with the whole 232 x 232 grid as the window so that the large kernels take it) and against the
+oracle's C restatement of pyx:69-154 on 500 x 500 grids."""
+import numpy as np
+import pytest
+import torch
+
+import goldens as G
+import oracle as O
+from test_gpu_dropin import _bitwise, _dp_tie
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def M():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need a GPU (run with -m gpu on an MI355X)')
+    from simaps import batch, vector_env
+    return batch, vector_env
+
+
+def test_demo_sample_through_the_large_kernels(M):
+    """The demo.py sample with window = the whole 232 x 232 grid (beyond SIMAPS_MAX_ROOM_W): its 12
+    reference images (sha256) and the demo known answer, and its reference paths."""
+    batch, vector_env = M
+    import hashlib
+    g = G.load('sssp.npz')
+    demo = g['demo_cspace']
+    H, W = demo.shape
+    assert not vector_env.window_fits(H, W)
+    srcs = g['demo_sources']
+    grids = torch.from_numpy(demo).cuda().unsqueeze(0).expand(len(srcs), H, W).contiguous()
+    imgs = batch.sssp_grid(grids, torch.from_numpy(srcs.astype(np.int32)), window=(0, 0, H, W)).cpu().numpy()
+    for k in range(len(srcs)):
+        assert hashlib.sha256(imgs[k].astype(np.float32).tobytes()).digest() == g['demo_sha'][k].tobytes(), k
+    one = batch.sssp_grid(grids[:1], torch.tensor([[75, 156]], dtype=torch.int32), window=(0, 0, H, W)).cpu().numpy()[0]
+    assert _bitwise(one, g['demo_image'])
+    assert one[131, 112] == np.float32(g['demo_distance'])
+    z = G.load('grid_paths.npz')
+    keys = sorted(k[:-4] for k in z.files if k.startswith('demo_') and k.endswith('_src'))
+    gr = torch.from_numpy(demo).cuda().unsqueeze(0).expand(len(keys), H, W).contiguous()
+    got = batch.grid_paths(gr, [tuple(z[k + '_src']) for k in keys], [tuple(z[k + '_tgt']) for k in keys],
+                           window=(0, 0, H, W), max_points=512)
+    for k, p in zip(keys, got):
+        assert np.array_equal(np.array(p, dtype=np.int32).reshape(-1, 2), z[k + '_path']), k
+    s0 = G.load('paths.npz')
+    got = batch.grid_paths(gr[:3], [tuple(s0['demo_%d_src' % q]) for q in range(3)],
+                           [tuple(s0['demo_%d_tgt' % q]) for q in range(3)], window=(0, 0, H, W))
+    for q in range(3):
+        assert np.array_equal(np.array(got[q]).reshape(-1, 2), s0['demo_%d_path' % q]), q
+
+
+def _big_grids(rs):
+    n = 500
+    yield 'rand25', (rs.random_sample((n, n)) > 0.25).astype(np.uint8)
+    yield 'rand40', (rs.random_sample((n, n)) > 0.40).astype(np.uint8)      # near percolation: long detours
+    e = np.ones((300, 420), np.uint8)
+    e[3::5, 3::5] = 0                                                        # pillar lattice: all ties
+    yield 'pillars', e
+    m = np.ones((257, 300), np.uint8) * 2                                   # free value 2: line of sight blocked
+    m[::8, 1:] = 0
+    m[4::16, :-1] = 2
+    m[::16, 0] = 2
+    m[8::16, -1] = 2
+    yield 'serpentine', m
+
+
+def test_gridgraph_large_images_and_paths_vs_oracle(M):
+    """500 x 500 random grids (two densities), a pillar lattice and a serpentine maze: the drop-in
+    GridGraph takes them (no ValueError), shortest_path_image equals the oracle SPFA bitwise, and
+    shortest_path equals the oracle's path (a Douglas-Peucker floating-point tie -- host-libm
+    dependent in the reference itself -- may differ, counted and bounded)."""
+    batch, vector_env = M
+    rs = np.random.RandomState(505)
+    n_cases = n_tie = 0
+    for name, grid in _big_grids(rs):
+        gg = vector_env.GridGraph(grid)
+        assert gg.large, name
+        free = np.argwhere(grid != 0)
+        for _ in range(2):
+            src = tuple(int(x) for x in free[rs.randint(len(free))])
+            img = gg.shortest_path_image(src)
+            assert _bitwise(img, O.spfa_image(grid, src)), (name, src)
+            tgts = [tuple(int(x) for x in free[rs.randint(len(free))]) for _ in range(6)]
+            got = gg.shortest_paths([(src, t) for t in tgts])
+            for t, p in zip(tgts, got):
+                want = O.grid_shortest_path(grid, src, t)
+                n_cases += 1
+                if np.array_equal(np.array(p, dtype=np.int64).reshape(-1, 2), np.array(want, dtype=np.int64).reshape(-1, 2)):
+                    continue
+                assert _dp_tie(grid, src, t), (name, src, t, p, want)
+                n_tie += 1
+            assert gg.shortest_path_distance(src, tgts[0]) == float(O.spfa_image(grid, src)[tgts[0]])
+    assert n_cases == 48 and n_tie <= 2, (n_cases, n_tie)
+
+
+def test_gridgraph_large_edge_cases(M):
+    """Blocked source (0 at the source, -1 elsewhere), unreachable target ([target]), source ==
+    target, a free region cut in two, and a 1 x 10,000 corridor (a window far beyond the LDS width)."""
+    batch, vector_env = M
+    rs = np.random.RandomState(7)
+    grid = (rs.random_sample((200, 300)) > 0.3).astype(np.uint8)
+    grid[:, 150] = 0                                                         # two halves
+    gg = vector_env.GridGraph(grid)
+    assert gg.large
+    blocked = tuple(int(x) for x in np.argwhere(grid == 0)[5])
+    assert _bitwise(gg.shortest_path_image(blocked), O.spfa_image(grid, blocked))
+    a = tuple(int(x) for x in np.argwhere(grid[:, :150] != 0)[10])
+    r, c = np.argwhere(grid[:, 151:] != 0)[10]
+    b = (int(r), int(c) + 151)
+    assert _bitwise(gg.shortest_path_image(a), O.spfa_image(grid, a))
+    for s, t in ((a, b), (a, a), (blocked, a)):
+        p = gg.shortest_path(s, t)
+        assert np.array_equal(np.array(p).reshape(-1, 2), np.array(O.grid_shortest_path(grid, s, t)).reshape(-1, 2)), (s, t)
+    corridor = np.ones((1, 10000), np.uint8)
+    gc = vector_env.GridGraph(corridor)
+    assert gc.large
+    assert _bitwise(gc.shortest_path_image((0, 17)), O.spfa_image(corridor, (0, 17)))
+    assert gc.shortest_path((0, 17), (0, 9990)) == [(0, 17), (0, 9990)]
+
+
+def test_gridgraph_large_refuses_graph_capture(M):
+    """The large-window kernels take their scratch in stream order per launch: under graph capture
+    the C ABI refuses (SIMAPS_EUNSUPPORTED) instead of capturing an allocation."""
+    batch, vector_env = M
+    from simaps import _lib
+    grid = torch.ones((1, 130, 130), dtype=torch.uint8, device='cuda')
+    src = torch.tensor([[5, 5]], dtype=torch.int32, device='cuda')
+    out = torch.empty((1, 130, 130), dtype=torch.float32, device='cuda')
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        try:
+            g.capture_begin()
+            rc = _lib.lib.simaps_sssp_grid(1, 130, 130, _lib.ptr(grid), _lib.ptr(src), _lib.ptr(out), 0, 0, 130, 130,
+                                           _lib.stream_handle(s))
+        finally:
+            g.capture_end()
+    assert rc == _lib.EUNSUPPORTED and b'captured' in _lib.lib.simaps_last_error()

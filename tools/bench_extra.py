@@ -5,6 +5,8 @@
   ingest         Robot.update_map minus the simulator (camera frame -> overhead / occupancy maps): frames/s
   distance_to_receptacle  the reward lookups from the receptacle, cold and from the render's cache
   env_step       (--env-step) the device time of one reference VectorEnv.step: paths, ingest, get_state
+  gridgraph_large (--gridgraph-large) GridGraph on a 500 x 500 grid (beyond the LDS window: the
+                 global-memory kernels of csrc/grid_large.h): images and paths, 1 and 64 per call
 
     python tools/bench_extra.py [--config lifting_4-small_divider] [--envs 64] [--queries 8]
 
@@ -293,7 +295,46 @@ def bench_ingest(args):
           flush=True)
 
 
+def bench_gridgraph_large(n=500, density=0.25, seed=505):
+    """GridGraph(grid).shortest_path_image / shortest_path on an n x n random grid (obstacle density
+    `density`), B = 1 and 64 queries per launch, against the oracle's C SPFA (the reference's
+    algorithm, 1 core; the reference's Cython SPFA runs at about the same speed, profiles/r2_cpu_calibration.json)."""
+    import oracle
+    rs = np.random.RandomState(seed)
+    grid = (rs.random_sample((n, n)) > density).astype(np.uint8)
+    free = np.argwhere(grid != 0)
+    pick = lambda k: free[rs.randint(len(free), size=k)].astype(np.int32)  # noqa: E731
+    g1 = torch.from_numpy(grid).cuda()
+    rows = {}
+    for B in (1, 64):
+        grids = g1.unsqueeze(0).expand(B, n, n).contiguous()
+        srcs = torch.from_numpy(pick(B)).cuda()
+        tg = pick(B)
+        img = timed(lambda: batch.sssp_grid(grids, srcs), 3, 1)
+        pth = timed(lambda: batch.launch_grid_paths(grids, srcs, torch.from_numpy(tg).cuda(), max_points=1024), 2, 1)
+        rows[B] = (img, pth)
+    s0, t0 = pick(1)[0], pick(1)[0]
+    c0 = time.perf_counter()
+    oracle.spfa_image(grid, tuple(s0))
+    cpu_img = time.perf_counter() - c0
+    c0 = time.perf_counter()
+    oracle.grid_shortest_path(grid, tuple(s0), tuple(t0))
+    cpu_path = time.perf_counter() - c0
+    print(json.dumps({'row': 'gridgraph_large', 'grid': '%dx%d' % (n, n), 'obstacle_density': density,
+                      'gpu_image_ms': {str(B): v[0] * 1e3 for B, v in rows.items()},
+                      'gpu_images_per_s_at_64': 64 / rows[64][0],
+                      'gpu_path_ms': {str(B): v[1] * 1e3 for B, v in rows.items()},
+                      'gpu_paths_per_s_at_64': 64 / rows[64][1],
+                      'cpu_oracle_image_ms': cpu_img * 1e3, 'cpu_oracle_path_ms': cpu_path * 1e3, 'cpu_cores': 1,
+                      'note': 'image: gl_sssp_kernel (directional sweeps in L2); path: the sweeps + gl_path_kernel '
+                              '(one wave replays the SPFA, early exit at the target chain); the SPFA is serial, '
+                              'one L2 round trip per pop'}), flush=True)
+
+
 if __name__ == '__main__':
+    if '--gridgraph-large' in sys.argv:
+        bench_gridgraph_large()
+        sys.exit(0)
     if '--env-step' in sys.argv:
         bench_env_step(argparse.Namespace(config='lifting_4-small_divider', envs=64, steps=50, all=False))
         bench_env_step(argparse.Namespace(config='lifting_4-small_divider', envs=64, steps=50, all=True))
