@@ -15,7 +15,7 @@
 //                   the early exit of the LDS kernels (it stops once every vertex of the target's
 //                   parent chain holds its fixpoint distance: no parent on it can change any more),
 //                   the parent walk, approximate_polygon(tolerance=1) and the line-of-sight pruning
-//                   (pyx:121-154).  The SPFA is serial by definition; each pop is one round trip to L2.
+//                   (pyx:121-154).  The SPFA is serial by definition: one round of loads per pop.
 // Padded layout per query: (wh + 2) rows x pitch = ww + 2 columns, border and blocked cells -inf,
 // free cells +inf until reached.
 
@@ -38,6 +38,17 @@ __device__ __forceinline__ void gl_st(float *p, float v) { __hip_atomic_store(p,
 __device__ __forceinline__ void gl_sti(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 // every store / atomic of this wave has reached L2 before the next load issues
 __device__ __forceinline__ void gl_drain() { __builtin_amdgcn_s_waitcnt(0); }
+
+// lane i <- lane i - 1 (lane 0 <- edge) / lane i <- lane i + 1 (lane 63 <- edge): DPP wave_shr:1 /
+// wave_shl:1 with bound_ctrl off, so the lane without a source keeps the `old` operand
+__device__ __forceinline__ float gl_from_prev_lane(float v, float edge)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float gl_from_next_lane(float v, float edge)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
 
 // One sweep of one wave over every line of the window (DIR 0 down, 1 up: lines = rows; 2 right,
 // 3 left: lines = columns), 64 cells of each line at a time (strip s0).  A cell of line l is relaxed
@@ -83,8 +94,11 @@ __device__ bool gl_sweep(float *D, const GlDims g)
                         Rr[j] = gl_ld(base(t + GL_PF) + own);
                         Xr[j] = gl_ld(base(t + GL_PF) + xo);
                     }
-                    const float pl = lane == 0 ? xp : from_prev_lane(p);
-                    const float pr = lane == 63 ? xp : from_next_lane(p);
+                    // wave shifts with the strip edge's own neighbour as the `old` value of lane 0 /
+                    // lane 63 (no select: a select became a branch around the DPP move, and a DPP read
+                    // from a lane that branch had disabled returns 0 -- a fake neighbour at distance 0)
+                    const float pl = gl_from_prev_lane(p, xp);
+                    const float pr = gl_from_next_lane(p, xp);
                     const float m = fminf(fminf(fabsf(p) + one, fabsf(pl) + s2), fabsf(pr) + s2);
                     if (m < R) {  // (blocked / border cells hold -inf: never)
                         atomicMin(reinterpret_cast<int *>(base(t) + own), __float_as_int(m));  // m >= 0: int order
@@ -208,75 +222,82 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
     }
     const long su = (long)(si - wi0 + 1) * P + (sj - wj0 + 1), tv = (long)(ti - wi0 + 1) * P + (tj - wj0 + 1);
     // (1) SPFA arrays: distances +inf on free cells (the reference's 2 * V: no path reaches it), -inf
-    // on blocked and border cells (never relaxed), pin 0; the queue holds the source (pyx:79-88)
+    // on blocked and border cells (never relaxed), pin 0; the queue holds the source (pyx:79-88).
+    // This wave is the only user of its arrays, so they are read through the L1 (plain loads); every
+    // pop's stores are drained (gl_drain) before the next pop's loads issue.
     for (long k = lane; k < g.cells; k += 64) {
-        const float fv = gl_ld(fix + k);
-        gl_st(dist + k, k == su ? 0.0f : (fv == -INFINITY ? -INFINITY : INFINITY));
-        gl_sti(pin + k, k == su ? GL_INQ : 0);
+        const float fv = fix[k];
+        dist[k] = k == su ? 0.0f : (fv == -INFINITY ? -INFINITY : INFINITY);
+        pin[k] = k == su ? GL_INQ : 0;
     }
-    if (lane == 0) gl_sti(queue, (int)su);
+    if (lane == 0) queue[0] = (int)su;
     gl_drain();
     unsigned fault_bits = 0;
-    const float finT = gl_ld(fix + tv);  // the target's fixpoint distance (+inf: unreachable, no early exit)
+    const float finT = fix[tv];  // the target's fixpoint distance (+inf: unreachable, no early exit)
     const int k8 = lane < 8 ? lane : 8;
     const long off = lane < 8 ? gl_dir_off(lane, P) : 0;  // lane 8: the popped vertex itself
     const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
-    long qh = 0, qt = 0, cnt = 1;  // front slot, last slot, live entries
+    // the queue: live slots qh .. qt (mod QR), cnt entries; its front u and (cnt >= 2) second s2 are
+    // kept in registers, so a pop's reads -- u's edge heads, the entry after s2, s2's distance -- go
+    // out together in one round
     const long QR = n1;
+    long qh = 0, qt = 0, cnt = 1, u = su, s2 = -1;
     long pops = 0, lim = finT != INFINITY ? 32 : SIMAPS_POP_CAP, gap = 64;
     bool early = false;
     while (cnt > 0) {
-        // (2) pop u; its edges in pyx order on lanes 0-7 (pyx:89-101)
-        const long u = gl_ldi(queue + qh);
-        const long q2 = qh + 1 == QR ? 0 : qh + 1;
-        const long fr = cnt > 1 ? gl_ldi(queue + q2) : -1;  // the next front (queue[head + 1])
+        // (2) pop u; its edges in pyx order on lanes 0-7 (pyx:89-101), lane 8 u itself
+        const long q2 = qh + 1 == QR ? 0 : qh + 1, q3 = q2 + 1 == QR ? 0 : q2 + 1;
+        const long v = u + off;
+        const float dv = lane <= 8 ? dist[v] : 0.0f;
+        const int pv = lane <= 8 ? pin[v] : 0;
+        const int third_l = (lane == 9 && cnt >= 3) ? queue[q3] : -1;
+        const float dfr_l = (lane == 10 && cnt >= 2) ? dist[s2] : 0.0f;
+        const long fr = cnt >= 2 ? s2 : -1;  // the front after this pop (queue[head + 1])
+        const long third = __shfl(third_l, 9);
+        const float dfr = __shfl(dfr_l, 10);  // its distance before this pop
         qh = q2;
         cnt--;
-        const long v = u + off;
-        const float dv = lane <= 8 ? gl_ld(dist + v) : 0.0f;
-        const int pv = lane <= 8 ? gl_ldi(pin + v) : 0;
-        const float dfr = fr >= 0 ? gl_ld(dist + fr) : 0.0f;  // its distance before this pop
         const float du = __shfl(dv, 8);
         const float nd = du + wl;
         const bool imp = lane < 8 && nd < dv;
         if (imp) {
-            gl_st(dist + v, nd);
-            gl_sti(pin + v, GL_INQ | (k8 + 1));
+            dist[v] = nd;
+            pin[v] = GL_INQ | (k8 + 1);
         }
-        if (lane == 8) gl_sti(pin + u, pv & 15);  // in_queue[u] = 0 (pyx:92)
+        if (lane == 8) pin[u] = pv & 15;  // in_queue[u] = 0 (pyx:92)
         // (3) pushes in edge order with the SLF swap against the front (pyx:102-107); the front's
-        // distance as of each edge: lowered by this pop's own edge to it, if any
+        // distance as of each edge: lowered by this pop's own edge to it, if any.  Queued heads are
+        // never pushed (the original front too, also after a swap moved it to the tail).
         uint64_t todo = __ballot(imp && ((pv & GL_INQ) == 0 || v == fr));
-        long f = fr;
+        long f = fr, nsec = cnt >= 2 ? third : -1;
+        const long q2n = qh + 1 == QR ? 0 : qh + 1;  // the slot after the front
         float df = dfr;
         while (todo) {
             const int k = __builtin_ctzll(todo);
             todo &= todo - 1;
             const long vk = __shfl(v, k);
             const float ndk = __shfl(nd, k);
-            const int pk = __shfl(pv, k);
-            if (vk == f) {  // the front itself improved (already in the queue: no push)
-                df = ndk;
+            if (__shfl(pv, k) & GL_INQ) {  // the front itself improved (queued: no push)
+                if (vk == f) df = ndk;
                 continue;
             }
-            (void)pk;
             qt = qt + 1 == QR ? 0 : qt + 1;
             cnt++;
-            if (cnt == 1) {  // (the queue was empty: tail == head + 1)
-                if (lane == 0) gl_sti(queue + qt, (int)vk);
+            long content = vk;
+            if (cnt == 1) {  // (the queue was empty: tail == head + 1 == this slot)
                 f = vk;
                 df = ndk;
             } else if (ndk < df) {
-                if (lane == 0) {
-                    gl_sti(queue + qh, (int)vk);
-                    gl_sti(queue + qt, (int)f);
-                }
+                if (lane == 0) queue[qh] = (int)vk;
+                content = f;
                 f = vk;
                 df = ndk;
-            } else if (lane == 0) {
-                gl_sti(queue + qt, (int)vk);
             }
+            if (lane == 0) queue[qt] = (int)content;
+            if (qt == q2n) nsec = content;
         }
+        u = f;
+        s2 = nsec;
         gl_drain();
         if (++pops < lim) continue;
         if (pops >= SIMAPS_POP_CAP) {
@@ -284,13 +305,11 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
             break;
         }
         // (4) early exit: the target at its fixpoint distance and then every vertex of its chain
-        bool ok = gl_ld(dist + tv) == finT;
-        for (long w = tv; ok && w != su;) {
-            const long m = lane == 0 ? w : w;  // (uniform)
-            ok = gl_ld(dist + m) == gl_ld(fix + m);
-            const int p = gl_ldi(pin + m) & 15;
-            if (!p) { ok = false; break; }
-            w = m - gl_dir_off(p - 1, P);
+        bool ok = dist[tv] == finT;
+        for (long w = tv, steps = 0; ok && w != su; steps++) {
+            const int p = pin[w] & 15;
+            if (!p || dist[w] != fix[w] || steps > n1) { ok = false; break; }
+            w -= gl_dir_off(p - 1, P);
         }
         if (ok) { early = true; break; }
         lim = pops + gap;

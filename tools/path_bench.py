@@ -66,8 +66,19 @@ def case(cfg, envs, steps, mode=0, targets='across'):
         full = st[:, 3] > st[:, 0]  # ran the SPFA in this launch (stale stamps of earlier cases are older)
         spfa_us = (st[full, 3] - st[full, 2]) / 100.0  # s_memrealtime: 100 MHz
         pops = st[full, 7]
+        qus = (st[full, 6] - st[full, 0]) / 100.0
+        # every query of the launch whose end stamp is from this launch (straight lines end before it)
+        allq = np.where(st[:N, 6] > st[:N, 0], st[:N, 6] - st[:N, 0], 0) / 100.0
+        t0 = st[:N, 0]
         out.update({'spfa_queries': int(full.sum()), 'spfa_us_median': float(np.median(spfa_us)),
-                    'pops_median': float(np.median(pops)),
+                    'pops_median': float(np.median(pops)), 'pops_max': int(pops.max()) if len(pops) else 0,
+                    'query_us_max': float(allq.max()),
+                    # latency accounting: the launch lasts as long as its slowest query
+                    # plus the dispatch of the workgroups and the kernel's launch / completion overhead
+                    'launch_over_slowest_query': ms * 1e3 / float(allq.max()),
+                    'slowest_over_median_query': float(allq.max() / np.median(qus)) if len(qus) else None,
+                    'entry_skew_us': float((t0.max() - t0.min()) / 100.0),
+                    'slowest_query_pops': int(st[:N, 7][np.argmax(allq)]),
                     'sweep_rounds_median': float(np.median(st[full, 8])) if mode in (2, 3) else None,
                     'sweeps_us_median': float(np.median((st[full, 10] - st[full, 2]) / 100.0)) if mode in (2, 3) else None,
                     'ns_per_pop_median': float(np.median(spfa_us * 1e3 / np.maximum(pops, 1))),
@@ -76,6 +87,11 @@ def case(cfg, envs, steps, mode=0, targets='across'):
 
 
 if __name__ == '__main__':
+    if '--latency' in sys.argv:  # the bench_extra latency row: 64 / 256 paths, local and across, auto mode
+        for targets in ('local', 'across'):
+            for envs in (16, 64):
+                case('lifting_4-small_divider', envs, 5, 0, targets)
+        sys.exit(0)
     # (pushing_4-large_empty has no obstacles: nearly all its paths are straight lines, and a launch
     # lasts as long as its slowest query -- a snapped end's full-room SPFA; lifting_4-large_doors:
     # large rooms with detours)
