@@ -5,8 +5,8 @@
 //
 // Same algorithm as the LDS kernels, with the arrays in global memory (L2-resident for grids up to a
 // few Mcells) and one workgroup per query:
-//   gl_sssp_kernel  the float32 fixpoint by directional sweeps (4 waves: down / up / right / left,
-//                   each over 64-cell strips of its lines, 16 lines prefetched ahead); every write is
+//   gl_sssp_kernel  the float32 fixpoint by directional sweeps (down / up / right / left, GL_WPD waves
+//                   each over 64-cell strips of their lines, lines prefetched ahead); every write is
 //                   an atomic min(cell, fl(d_u + w)) of a real edge, so the unique fixpoint -- the
 //                   reference SPFA's distances (pyx:69-114), bit for bit -- is reached whatever the
 //                   interleaving, and a round in which no sweep finds a candidate below the value it
@@ -19,8 +19,18 @@
 // Padded layout per query: (wh + 2) rows x pitch = ww + 2 columns, border and blocked cells -inf,
 // free cells +inf until reached.
 
-constexpr int GL_NT = 256;  // gl_sssp_kernel: one wave per sweep direction
-constexpr int GL_PF = 16;   // lines prefetched ahead in a sweep strip
+#ifndef SIMAPS_GL_WPD
+#define SIMAPS_GL_WPD 1
+#endif
+constexpr int GL_WPD = SIMAPS_GL_WPD;  // gl_sssp_kernel: waves per sweep direction (each takes every
+constexpr int GL_NT = 4 * 64 * GL_WPD;  //  GL_WPD-th 64-cell strip of its direction's lines)
+#ifndef SIMAPS_GL_POP_NODRAIN
+#define SIMAPS_GL_POP_NODRAIN 0
+#endif
+#ifndef SIMAPS_GL_PF
+#define SIMAPS_GL_PF 32
+#endif
+constexpr int GL_PF = SIMAPS_GL_PF;  // lines prefetched ahead in a sweep strip
 constexpr int GL_INQ = 16;  // pin bit 4: in the queue (bits 0-3: 1 + direction of the parent edge)
 
 struct GlDims {
@@ -54,32 +64,37 @@ __device__ __forceinline__ float gl_from_next_lane(float v, float edge)
 // 3 left: lines = columns), 64 cells of each line at a time (strip s0).  A cell of line l is relaxed
 // from the 3 cells of line l -1 (in sweep order): straight (weight 1) and the two diagonals (float32
 // sqrt(2)).  Inside a strip the previous line's values pass between lanes by DPP; lane 0 / lane 63
-// read their outer neighbour from memory (the previous strip's value, final for this sweep, or the
-// next strip's, from before it) -- a stale value is still some path's length, so every write remains
+// read their outer neighbour from memory (the neighbouring strip's value, as far as its wave got in
+// this sweep or from before it) -- a stale value is still some path's length, so every write remains
 // a valid relaxation.  Returns true if some candidate was below the value read.
 template <int DIR>
-__device__ bool gl_sweep(float *D, const GlDims g)
+__device__ bool gl_sweep(float *D, const GlDims g, int part)
 {
     constexpr bool VERT = DIR < 2, FWD = (DIR & 1) == 0;
     const int lane = threadIdx.x & 63;
     const int N = VERT ? g.wh : g.ww, L = VERT ? g.ww : g.wh;
-    const long sl = VERT ? g.pitch : 1, sa = VERT ? 1 : g.pitch;
+    const int sl = VERT ? g.pitch : 1, sa = VERT ? 1 : g.pitch;
     bool chg = false;
-    for (int s0 = 0; s0 < L; s0 += 64) {
+    // Plain loads through the L1, addressed as a wave-uniform line pointer (SGPRs) plus a 32-bit
+    // per-lane offset: a line the L1 still holds from before another wave's atomics is stale, which
+    // is allowed (see above); gl_sssp_kernel invalidates the L1 at every round's barrier, so in a
+    // round without writes every read is current.
+    auto line = [&](int t) { return D + (long)((FWD ? 1 + t : N - t) * sl); };
+    for (int s0 = 64 * part; s0 < L; s0 += 64 * GL_WPD) {
         const int c = s0 + lane;
         const bool act = c < L;
         const int cc = act ? c : L;  // inactive lanes alias the border cell after the line (-inf)
-        const long own = (1 + cc) * sa;
+        const int own = (1 + cc) * sa;
         // the outer neighbour a strip edge reads (lane 0: c - 1, lane 63: c + 1); others re-read their own cell
-        const long xo = (1 + (lane == 0 ? c - 1 : (lane == 63 && act) ? c + 1 : cc)) * sa;
+        const int xo = (1 + (lane == 0 ? c - 1 : (lane == 63 && act) ? c + 1 : cc)) * sa;
         const float one = act ? 1.0f : INFINITY, s2 = act ? SQRT2F : INFINITY;
-        auto base = [&](int t) { return D + (long)(1 + (FWD ? t : N - 1 - t)) * sl; };
         float Rr[GL_PF], Xr[GL_PF];
 #pragma unroll
         for (int j = 0; j < GL_PF; j++)
             if (j < N) {
-                Rr[j] = gl_ld(base(j) + own);
-                Xr[j] = gl_ld(base(j) + xo);
+                const float *ln = line(j);
+                Rr[j] = ln[own];
+                Xr[j] = ln[xo];
             }
         // the previous line: this lane's value (sign trick: -inf = blocked passes on nothing, as |.|
         // = +inf) and its outer neighbour's
@@ -91,8 +106,9 @@ __device__ bool gl_sweep(float *D, const GlDims g)
                 if (t < N) {  // (wave-uniform)
                     const float R = Rr[j], X = Xr[j];
                     if (t + GL_PF < N) {
-                        Rr[j] = gl_ld(base(t + GL_PF) + own);
-                        Xr[j] = gl_ld(base(t + GL_PF) + xo);
+                        const float *ln = line(t + GL_PF);
+                        Rr[j] = ln[own];
+                        Xr[j] = ln[xo];
                     }
                     // wave shifts with the strip edge's own neighbour as the `old` value of lane 0 /
                     // lane 63 (no select: a select became a branch around the DPP move, and a DPP read
@@ -101,7 +117,7 @@ __device__ bool gl_sweep(float *D, const GlDims g)
                     const float pr = gl_from_next_lane(p, xp);
                     const float m = fminf(fminf(fabsf(p) + one, fabsf(pl) + s2), fabsf(pr) + s2);
                     if (m < R) {  // (blocked / border cells hold -inf: never)
-                        atomicMin(reinterpret_cast<int *>(base(t) + own), __float_as_int(m));  // m >= 0: int order
+                        atomicMin(reinterpret_cast<int *>(line(t)) + own, __float_as_int(m));  // m >= 0: int order
                         chg = true;
                     }
                     p = act ? fminf(m, R) : -INFINITY;
@@ -139,16 +155,19 @@ __global__ void __launch_bounds__(GL_NT) gl_sssp_kernel(int H, int W, const uint
     if (tid < 3) changed[tid] = 0;
     gl_drain();
     __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     unsigned f = 0;
     if (s_in) {
         const long cap = (long)wh * ww + 16;
         for (long round = 0;; round++) {
-            const bool c = wave == 0 ? gl_sweep<0>(D, g) : wave == 1 ? gl_sweep<1>(D, g)
-                         : wave == 2 ? gl_sweep<2>(D, g) : gl_sweep<3>(D, g);
+            const int dir = wave & 3, part = wave >> 2;  // (strips of one direction run side by side)
+            const bool c = dir == 0 ? gl_sweep<0>(D, g, part) : dir == 1 ? gl_sweep<1>(D, g, part)
+                         : dir == 2 ? gl_sweep<2>(D, g, part) : gl_sweep<3>(D, g, part);
             if (c && (tid & 63) == 0) changed[round % 3] = 1;
             if (tid == 0) changed[(round + 1) % 3] = 0;  // (last read two barriers ago)
             gl_drain();  // this round's atomics are in L2 before any wave reads for the next one
             __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (invalidates the L1: the next round reads L2)
             if (!changed[round % 3]) break;
             if (round >= cap) {
                 f = SIMAPS_FAULT_ROUNDS;
@@ -298,7 +317,9 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
         }
         u = f;
         s2 = nsec;
+#if !SIMAPS_GL_POP_NODRAIN  // (timing variant: no wait for the pop's stores before the next pop's loads)
         gl_drain();
+#endif
         if (++pops < lim) continue;
         if (pops >= SIMAPS_POP_CAP) {
             if (cnt > 0) fault_bits |= SIMAPS_FAULT_ROUNDS;  // the cap stopped a live queue
