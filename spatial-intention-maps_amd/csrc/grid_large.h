@@ -24,9 +24,6 @@
 #endif
 constexpr int GL_WPD = SIMAPS_GL_WPD;  // gl_sssp_kernel: waves per sweep direction (each takes every
 constexpr int GL_NT = 4 * 64 * GL_WPD;  //  GL_WPD-th 64-cell strip of its direction's lines)
-#ifndef SIMAPS_GL_POP_NODRAIN
-#define SIMAPS_GL_POP_NODRAIN 0
-#endif
 #ifndef SIMAPS_GL_PF
 #define SIMAPS_GL_PF 32
 #endif
@@ -317,9 +314,7 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
         }
         u = f;
         s2 = nsec;
-#if !SIMAPS_GL_POP_NODRAIN  // (timing variant: no wait for the pop's stores before the next pop's loads)
-        gl_drain();
-#endif
+        gl_drain();  // (a timing variant without this wait was only 4 % faster: profiles/r5h_*)
         if (++pops < lim) continue;
         if (pops >= SIMAPS_POP_CAP) {
             if (cnt > 0) fault_bits |= SIMAPS_FAULT_ROUNDS;  // the cap stopped a live queue
