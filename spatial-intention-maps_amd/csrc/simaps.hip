@@ -2925,9 +2925,6 @@ __device__ __forceinline__ int dir_off(int k, int pw)
     return di * pw + dj;
 }
 
-#ifndef SIMAPS_SPFA_EARLYREAD_EXPERIMENT  // timing experiment only (results invalid): the next pop's reads
-#define SIMAPS_SPFA_EARLYREAD_EXPERIMENT 0   // issued before this pop's writes, with no forwarding
-#endif
 #ifndef SIMAPS_SPFA_ASM  // the common pops as one inline-asm loop (0: the C++ pop alone, for A/B builds)
 #define SIMAPS_SPFA_ASM 1
 #endif
@@ -2948,7 +2945,10 @@ __device__ __forceinline__ int dir_off(int k, int pw)
 // with its reads (vv / dv / pv / dF0 / pth, issued one pop ahead, as path_core's pf_* values)
 // complete -- so that the C++ pop replays that one exactly.  State as in path_core: u the front, F0
 // the second, qn the slot of F0, qt the tail slot, cnt the live entries including u.  DIST / QUEUE /
-// PIN: the byte offsets of the LDS arrays (checked by the caller).
+// PIN: the byte offsets of the LDS arrays (checked by the caller).  Lane 8's write values need no
+// select (round 5, two VALU fewer per pop): its edge weight wl is 0, so its candidate is its own
+// unchanged distance (never an improvement), and its pin byte is (pv & 15) | 0 where the edge lanes
+// write (pv & 0) | pbits -- one v_and_or with per-lane constants m15 / pb8.
 // Wait states: a VALU SGPR write is read by a VALU >= 2 instructions later (du); the opening s_nop
 // covers the compiler's last writes of the inputs.  The wave's LDS operations complete in order, so
 // one lgkmcnt(0) before each pop waits for the read-ahead and everything before it.
@@ -2959,6 +2959,8 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
 {
     static_assert(PIN + 255 < 65536 && QUEUE + 4 < 65536, "ds offsets are 16-bit");
     const uint64_t l8 = 1ull << 8;  // lane 8: the popped vertex itself (doff 0)
+    const int lane = threadIdx.x & 63;
+    const int pb8 = lane < 8 ? pbits : 0, m15 = lane == 8 ? 15 : 0;
     // Pops the loop may run with no per-pop test but its budget: no ring wrap (the tail grows by <= 8
     // per pop and stays within ring - 8, the read-ahead slot by 1 and stays within ring - 3), >= 4
     // live entries before every pop (the count drops by <= 1 per pop: budget cnt - 3) and at most
@@ -2979,33 +2981,19 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
     int du, th, t;
     float nd;
     int ta, tb, tc, td;
-#if SIMAPS_SPFA_EARLYREAD_EXPERIMENT
-    int xv, xa, xb, xq, xp;
-    float xf, xd;
-#endif
     if (seg > 0 && qt >= qn) {  // (qt < qn: the live entries wrap the ring; the C++ pop runs)
         int tq = 2 * qn;  // byte offset of slot qn in the queue (the read-ahead slot is qn + 2)
         // two pops per iteration with the second's registers swapped (no copy of the next second into
         // F0, one branch and one read-ahead slot increment per two pops)
-#if SIMAPS_SPFA_EARLYREAD_EXPERIMENT
 #define FP_POP(A, B, QOFF, L9, L8, LS)                                                              \
-            "v_add_u32_e32 %[xv], " A ", %[doff]\n\t"                                              \
-            "v_lshlrev_b32_e32 %[xb], 2, %[pth]\n\t"                                               \
-            "v_lshlrev_b32_e32 %[xa], 2, %[xv]\n\t"                                                \
-            "ds_read_b32 %[xf], %[xb] offset:%c[DIST]\n\t"                                         \
-            "ds_read_u16 %[xq], %[tc] offset:%c[" QOFF "]\n\t"                                     \
-            "ds_read_b32 %[xd], %[xa] offset:%c[DIST]\n\t"                                         \
-            "ds_read_u8 %[xp], %[xv] offset:%c[PIN]\n\t"                                           \
             "v_readlane_b32 %[du], %[dv], 8\n\t"                                                   \
             "v_readfirstlane_b32 " B ", %[pth]\n\t"                                                \
             "v_cmp_gt_u32_e64 %[nq], 16, %[pv]\n\t"                                                \
-            "v_and_b32_e32 %[tb], 15, %[pv]\n\t"                                                   \
+            "v_and_or_b32 %[tb], %[pv], %[m15], %[pb8]\n\t"                                         \
             "v_add_f32_e32 %[nd], %[du], %[wl]\n\t"                                                \
             "v_cmp_eq_u32_e64 %[fm], " A ", %[vv]\n\t"                                             \
             "v_cmp_lt_f32_e64 %[im], %[nd], %[dv]\n\t"                                             \
             "v_cmp_lt_f32_e64 %[sw], %[nd], %[dF0]\n\t"                                            \
-            "v_cndmask_b32_e64 %[tb], %[pbits], %[tb], %[l8]\n\t"                                  \
-            "v_cndmask_b32_e64 %[td], %[nd], %[dv], %[l8]\n\t"                                     \
             "v_lshlrev_b32_e32 %[ta], 2, %[vv]\n\t"                                                \
             "s_and_b64 %[nq], %[nq], %[im]\n\t"                                                    \
             "s_and_b64 %[fm], %[fm], %[im]\n\t"                                                    \
@@ -3014,50 +3002,7 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
             "s_cmp_lg_u64 %[sw], 0\n\t"                                                            \
             "s_cbranch_scc1 " L9 "\n\t"                                                            \
             "s_or_b64 exec, %[im], %[l8]\n\t"                                                      \
-            "ds_write_b32 %[ta], %[td] offset:%c[DIST]\n\t"                                        \
-            "ds_write_b8 %[vv], %[tb] offset:%c[PIN]\n\t"                                          \
-            "s_cmp_eq_u64 %[nq], 0\n\t"                                                            \
-            "s_cbranch_scc1 " LS "f\n\t"                                                                 \
-            "s_mov_b64 exec, %[nq]\n\t"                                                            \
-            "s_mov_b64 vcc, %[nq]\n\t"                                                             \
-            "v_mbcnt_lo_u32_b32 %[td], vcc_lo, 0\n\t"                                              \
-            "v_add_u32_e32 %[td], %[qt], %[td]\n\t"                                                \
-            "v_lshlrev_b32_e32 %[td], 1, %[td]\n\t"                                                \
-            "ds_write_b16 %[td], %[vv] offset:%c[QUEUE]\n"                                         \
-            LS ":\n\t"                                                                             \
-            "s_mov_b64 exec, %[ex]\n\t"                                                            \
-            "s_bcnt1_i32_b64 %[t], %[nq]\n\t"                                                      \
-            "s_add_u32 %[qt], %[qt], %[t]\n\t"                                                     \
-            "s_sub_u32 %[bud], %[bud], 1\n\t"                                                      \
-            "s_waitcnt lgkmcnt(0)\n\t"                                                             \
-            "v_mov_b32_e32 %[vv], %[xv]\n\t"                                                       \
-            "v_mov_b32_e32 %[dF0], %[xf]\n\t"                                                      \
-            "v_mov_b32_e32 %[pth], %[xq]\n\t"                                                      \
-            "v_mov_b32_e32 %[dv], %[xd]\n\t"                                                       \
-            "v_mov_b32_e32 %[pv], %[xp]\n\t"                                                       \
-            "s_cmp_le_i32 %[bud], 0\n\t"                                                           \
-            "s_cbranch_scc1 " L8 "\n\t"
-#else
-#define FP_POP(A, B, QOFF, L9, L8, LS)                                                              \
-            "v_readlane_b32 %[du], %[dv], 8\n\t"                                                   \
-            "v_readfirstlane_b32 " B ", %[pth]\n\t"                                                \
-            "v_cmp_gt_u32_e64 %[nq], 16, %[pv]\n\t"                                                \
-            "v_and_b32_e32 %[tb], 15, %[pv]\n\t"                                                   \
-            "v_add_f32_e32 %[nd], %[du], %[wl]\n\t"                                                \
-            "v_cmp_eq_u32_e64 %[fm], " A ", %[vv]\n\t"                                             \
-            "v_cmp_lt_f32_e64 %[im], %[nd], %[dv]\n\t"                                             \
-            "v_cmp_lt_f32_e64 %[sw], %[nd], %[dF0]\n\t"                                            \
-            "v_cndmask_b32_e64 %[tb], %[pbits], %[tb], %[l8]\n\t"                                  \
-            "v_cndmask_b32_e64 %[td], %[nd], %[dv], %[l8]\n\t"                                     \
-            "v_lshlrev_b32_e32 %[ta], 2, %[vv]\n\t"                                                \
-            "s_and_b64 %[nq], %[nq], %[im]\n\t"                                                    \
-            "s_and_b64 %[fm], %[fm], %[im]\n\t"                                                    \
-            "s_and_b64 %[sw], %[sw], %[nq]\n\t"                                                    \
-            "s_or_b64 %[sw], %[sw], %[fm]\n\t"                                                     \
-            "s_cmp_lg_u64 %[sw], 0\n\t"                                                            \
-            "s_cbranch_scc1 " L9 "\n\t"                                                            \
-            "s_or_b64 exec, %[im], %[l8]\n\t"                                                      \
-            "ds_write_b32 %[ta], %[td] offset:%c[DIST]\n\t"                                        \
+            "ds_write_b32 %[ta], %[nd] offset:%c[DIST]\n\t"                                        \
             "ds_write_b8 %[vv], %[tb] offset:%c[PIN]\n\t"                                          \
             "s_cmp_eq_u64 %[nq], 0\n\t"                                                            \
             "s_cbranch_scc1 " LS "f\n\t"                                                                 \
@@ -3082,7 +3027,6 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
             "s_cmp_le_i32 %[bud], 0\n\t"                                                           \
             "s_cbranch_scc1 " L8 "\n\t"                                                            \
             "s_waitcnt lgkmcnt(0)\n\t"
-#endif
         // At a segment's end (its last pop's reads issued): account the segment, wait for the reads, and
         // leave unless it ended at `left` = 0 with target checks on; then check the target (leave if
         // it is final) and run the next 32 pops after FIX (the register fix-up for the iteration half).
@@ -3132,19 +3076,13 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
             "6:\n\t"
             FP_REFILL("v_add_u32_e32 %[tc], 4, %[tc]\n\t", "9f")
             "9:\n\t"
-#if SIMAPS_SPFA_EARLYREAD_EXPERIMENT
-            "s_waitcnt lgkmcnt(0)\n\t"
-#endif
             : [F0] "+s"(F0), [qt] "+s"(qt), [bud] "+s"(bud), [seg] "+s"(seg), [gb] "+s"(gb), [lft] "+s"(lft),
               [ladd] "+s"(ladd),
               [vv] "+v"(vv), [dv] "+v"(dv), [pv] "+v"(pv), [dF0] "+v"(dF0), [pth] "+v"(pth),
               [ex] "=&s"(ex), [nq] "=&s"(nq), [fm] "=&s"(fm), [im] "=&s"(im), [sw] "=&s"(sw), [du] "=&s"(du),
               [th] "=&s"(th), [t] "=&s"(t), [nd] "=&v"(nd), [ta] "=&v"(ta), [tb] "=&v"(tb), [tc] "=&v"(tc),
               [td] "=&v"(td)
-#if SIMAPS_SPFA_EARLYREAD_EXPERIMENT
-              , [xv] "=&v"(xv), [xa] "=&v"(xa), [xb] "=&v"(xb), [xf] "=&v"(xf), [xq] "=&v"(xq), [xd] "=&v"(xd), [xp] "=&v"(xp)
-#endif
-            : [tq] "s"(tq), [l8] "s"(l8), [tv4] "s"(tv4), [fin] "s"(fin), [doff] "v"(doff), [wl] "v"(wl), [pbits] "v"(pbits), [DIST] "i"(DIST),
+            : [tq] "s"(tq), [l8] "s"(l8), [tv4] "s"(tv4), [fin] "s"(fin), [doff] "v"(doff), [wl] "v"(wl), [pb8] "v"(pb8), [m15] "v"(m15), [DIST] "i"(DIST),
               [QUEUE] "i"(QUEUE), [QUEUE4] "i"(QUEUE + 4), [QUEUE6] "i"(QUEUE + 6), [PIN] "i"(PIN)
             : "memory", "scc", "vcc");
 #undef FP_POP
@@ -3282,7 +3220,8 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
     }
     if (tid < 64 && run_spfa) {
         const int doff = lane < 8 ? dir_off(lane, pw) : 0;
-        const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
+        // lane 8 (the popped vertex): weight 0, so its candidate is its own distance -- never `better`
+        const float wl = lane == 8 ? 0.0f : (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
         const uint8_t pbits = (uint8_t)((lane + 1) | 0x10);  // a relaxed head: parent edge `lane`, queued
         if (lane == 0) { dist[su] = 0.0f; queue[0] = (uint16_t)su; pin[su] = 0x10; }
         __builtin_amdgcn_wave_barrier();
@@ -3465,7 +3404,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     const float dF0 = Ld[F0];
                     const int third = Lq[q2];          // queue[qh + 1]: the next pop's second (if count >= 2)
                     const float nd = du + wl;
-                    // (lanes >= 8: v = u, so nd = du + 1 > dv: never `better`; no lane test needed)
+                    // (lanes >= 8: v = u, so nd = du + wl >= dv, wl = 0 on lane 8, 1 above: never `better`)
                     const bool better = nd < dv;
                     const uint64_t imp = __builtin_amdgcn_ballot_w64(better);
                     // not queued: bit 4 clear, i.e. pv < 16 (a pin byte is at most 0x18: one compare)
