@@ -2945,10 +2945,9 @@ __device__ __forceinline__ int dir_off(int k, int pw)
 // with its reads (vv / dv / pv / dF0 / pth, issued one pop ahead, as path_core's pf_* values)
 // complete -- so that the C++ pop replays that one exactly.  State as in path_core: u the front, F0
 // the second, qn the slot of F0, qt the tail slot, cnt the live entries including u.  DIST / QUEUE /
-// PIN: the byte offsets of the LDS arrays (checked by the caller).  Lane 8's write values need no
-// select (round 5, two VALU fewer per pop): its edge weight wl is 0, so its candidate is its own
-// unchanged distance (never an improvement), and its pin byte is (pv & 15) | 0 where the edge lanes
-// write (pv & 0) | pbits -- one v_and_or with per-lane constants m15 / pb8.
+// PIN: the byte offsets of the LDS arrays (checked by the caller).  (Round 5 tried lane 8's write
+// values without the two selects -- weight 0 on lane 8 and one v_and_or -- and measured it 3 %
+// slower per pop: profiles/r5i_*.)
 // Wait states: a VALU SGPR write is read by a VALU >= 2 instructions later (du); the opening s_nop
 // covers the compiler's last writes of the inputs.  The wave's LDS operations complete in order, so
 // one lgkmcnt(0) before each pop waits for the read-ahead and everything before it.
@@ -2959,8 +2958,6 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
 {
     static_assert(PIN + 255 < 65536 && QUEUE + 4 < 65536, "ds offsets are 16-bit");
     const uint64_t l8 = 1ull << 8;  // lane 8: the popped vertex itself (doff 0)
-    const int lane = threadIdx.x & 63;
-    const int pb8 = lane < 8 ? pbits : 0, m15 = lane == 8 ? 15 : 0;
     // Pops the loop may run with no per-pop test but its budget: no ring wrap (the tail grows by <= 8
     // per pop and stays within ring - 8, the read-ahead slot by 1 and stays within ring - 3), >= 4
     // live entries before every pop (the count drops by <= 1 per pop: budget cnt - 3) and at most
@@ -2989,11 +2986,13 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
             "v_readlane_b32 %[du], %[dv], 8\n\t"                                                   \
             "v_readfirstlane_b32 " B ", %[pth]\n\t"                                                \
             "v_cmp_gt_u32_e64 %[nq], 16, %[pv]\n\t"                                                \
-            "v_and_or_b32 %[tb], %[pv], %[m15], %[pb8]\n\t"                                         \
+            "v_and_b32_e32 %[tb], 15, %[pv]\n\t"                                                   \
             "v_add_f32_e32 %[nd], %[du], %[wl]\n\t"                                                \
             "v_cmp_eq_u32_e64 %[fm], " A ", %[vv]\n\t"                                             \
             "v_cmp_lt_f32_e64 %[im], %[nd], %[dv]\n\t"                                             \
             "v_cmp_lt_f32_e64 %[sw], %[nd], %[dF0]\n\t"                                            \
+            "v_cndmask_b32_e64 %[tb], %[pbits], %[tb], %[l8]\n\t"                                  \
+            "v_cndmask_b32_e64 %[td], %[nd], %[dv], %[l8]\n\t"                                     \
             "v_lshlrev_b32_e32 %[ta], 2, %[vv]\n\t"                                                \
             "s_and_b64 %[nq], %[nq], %[im]\n\t"                                                    \
             "s_and_b64 %[fm], %[fm], %[im]\n\t"                                                    \
@@ -3002,7 +3001,7 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
             "s_cmp_lg_u64 %[sw], 0\n\t"                                                            \
             "s_cbranch_scc1 " L9 "\n\t"                                                            \
             "s_or_b64 exec, %[im], %[l8]\n\t"                                                      \
-            "ds_write_b32 %[ta], %[nd] offset:%c[DIST]\n\t"                                        \
+            "ds_write_b32 %[ta], %[td] offset:%c[DIST]\n\t"                                        \
             "ds_write_b8 %[vv], %[tb] offset:%c[PIN]\n\t"                                          \
             "s_cmp_eq_u64 %[nq], 0\n\t"                                                            \
             "s_cbranch_scc1 " LS "f\n\t"                                                                 \
@@ -3082,7 +3081,7 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
               [ex] "=&s"(ex), [nq] "=&s"(nq), [fm] "=&s"(fm), [im] "=&s"(im), [sw] "=&s"(sw), [du] "=&s"(du),
               [th] "=&s"(th), [t] "=&s"(t), [nd] "=&v"(nd), [ta] "=&v"(ta), [tb] "=&v"(tb), [tc] "=&v"(tc),
               [td] "=&v"(td)
-            : [tq] "s"(tq), [l8] "s"(l8), [tv4] "s"(tv4), [fin] "s"(fin), [doff] "v"(doff), [wl] "v"(wl), [pb8] "v"(pb8), [m15] "v"(m15), [DIST] "i"(DIST),
+            : [tq] "s"(tq), [l8] "s"(l8), [tv4] "s"(tv4), [fin] "s"(fin), [doff] "v"(doff), [wl] "v"(wl), [pbits] "v"(pbits), [DIST] "i"(DIST),
               [QUEUE] "i"(QUEUE), [QUEUE4] "i"(QUEUE + 4), [QUEUE6] "i"(QUEUE + 6), [PIN] "i"(PIN)
             : "memory", "scc", "vcc");
 #undef FP_POP
@@ -3220,8 +3219,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
     }
     if (tid < 64 && run_spfa) {
         const int doff = lane < 8 ? dir_off(lane, pw) : 0;
-        // lane 8 (the popped vertex): weight 0, so its candidate is its own distance -- never `better`
-        const float wl = lane == 8 ? 0.0f : (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
+        const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
         const uint8_t pbits = (uint8_t)((lane + 1) | 0x10);  // a relaxed head: parent edge `lane`, queued
         if (lane == 0) { dist[su] = 0.0f; queue[0] = (uint16_t)su; pin[su] = 0x10; }
         __builtin_amdgcn_wave_barrier();
@@ -3404,7 +3402,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
                     const float dF0 = Ld[F0];
                     const int third = Lq[q2];          // queue[qh + 1]: the next pop's second (if count >= 2)
                     const float nd = du + wl;
-                    // (lanes >= 8: v = u, so nd = du + wl >= dv, wl = 0 on lane 8, 1 above: never `better`)
+                    // (lanes >= 8: v = u, so nd = du + 1 > dv: never `better`; no lane test needed)
                     const bool better = nd < dv;
                     const uint64_t imp = __builtin_amdgcn_ballot_w64(better);
                     // not queued: bit 4 clear, i.e. pv < 16 (a pin byte is at most 0x18: one compare)
