@@ -28,6 +28,7 @@
  *                          obstacle scatter of OccupancyMap.update (2447-2450), in place, batched.
  *   simaps_robot_mask   <- Mapper._create_robot_mask (envs.py:2218-2242) (host helper).
  *   simaps_num_channels <- the channel list of Mapper.get_state (envs.py:2071-2113).
+ *   simaps_get_state_mixed <- simaps_get_state over agents of several configurations, one launch.
  */
 #ifndef SIMAPS_H
 #define SIMAPS_H
@@ -38,7 +39,7 @@
 extern "C" {
 #endif
 
-#define SIMAPS_ABI_VERSION 7
+#define SIMAPS_ABI_VERSION 8
 
 /* error codes */
 #define SIMAPS_OK 0
@@ -55,8 +56,10 @@ extern "C" {
 #define SIMAPS_FAULT_TIMEOUT 1u    /* a wave-group barrier or scratch hand-over gave up waiting (~0.1 s) */
 #define SIMAPS_FAULT_ROUNDS 2u     /* the SSSP round cap was hit (no convergence) */
 #define SIMAPS_FAULT_DESCRIPTOR 4u /* a descriptor field outside this build's limits was clamped: num_robots
-                                      > SIMAPS_MAX_ROBOTS, robot index >= num_robots, or a used intention /
-                                      history path longer than SIMAPS_MAX_PATH points */
+                                      > SIMAPS_MAX_ROBOTS, robot index >= num_robots, an env's num_robots
+                                      other than num_robots_per_env with intention channels on, a used
+                                      intention / history path longer than SIMAPS_MAX_PATH points, or (mixed
+                                      launch) a configuration index >= n_cfgs */
 
 /* robot classes (envs.py: LiftingRobot 1169, PushingRobot 1059, ThrowingRobot 1279, RescueRobot 1346) */
 #define SIMAPS_LIFTING 0
@@ -212,6 +215,26 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
                      const simaps_robot *robots, const double *paths, const uint8_t *occupancy,
                      const float *overhead, float *state, int num_robots_per_env, const simaps_debug *dbg,
                      void *stream);
+
+/* simaps_get_state over agents of up to SIMAPS_MAX_MIXED configurations in ONE launch (the
+ * reference's multiprocess collector runs one configuration per worker, train_multiprocess.py:159-166;
+ * several workers' envs then share a launch).  cfgs[n_cfgs] and num_robots_per_env[n_cfgs] are HOST
+ * arrays (copied into the launch); everything else is DEVICE:
+ *   agent_cfg [N] int32   the configuration of agent n (index into cfgs)
+ *   map_off   [M] int64   element offset of map slot m in occupancy / overhead (its maps are
+ *                         H x W of its agents' configuration; slots of one configuration may be packed
+ *                         back to back after those of another)
+ *   out_off   [N] int64   float offset of agent n's stack in state (96 * 96 * C of its configuration,
+ *                         in its configuration's layout)
+ * agents / envs / robots / paths as for simaps_get_state (one combined descriptor for all envs).
+ * Bit-identical to one simaps_get_state launch per configuration.  No debug outputs or receptacle cache.
+ * SIMAPS_EINVAL for n_cfgs outside [1, SIMAPS_MAX_MIXED] or a bad configuration. */
+#define SIMAPS_MAX_MIXED 8
+int simaps_get_state_mixed(const simaps_config *cfgs, const int32_t *num_robots_per_env, int n_cfgs, int N,
+                           const simaps_agent *agents, const int32_t *agent_cfg, const simaps_env *envs,
+                           const simaps_robot *robots, const double *paths, const uint8_t *occupancy,
+                           const int64_t *map_off, const float *overhead, float *state, const int64_t *out_off,
+                           void *stream);
 
 /* Batched OccupancyMap.shortest_path_distance(source_position, target_position) / 96 (Python float
  * semantics: the float32 SPFA distance converted to double, divided by 96.0; unreachable -> -1 / 96):

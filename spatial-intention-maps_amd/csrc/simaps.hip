@@ -45,6 +45,7 @@
 #include <type_traits>
 
 #include "geom.h"
+#include "mixed.h"
 #include "simaps.h"
 
 using namespace simaps;
@@ -2301,237 +2302,17 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
     if (t == 0) STAMP_NB(50);
 }
 
+#ifndef SIMAPS_DEVICE_ONLY  // (simaps_mixed.hip includes this file for its device helpers only)
 __global__ void __launch_bounds__(NT) get_state_kernel(
     simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents, const simaps_env *__restrict__ envs,
     const simaps_robot *__restrict__ robots, const double *__restrict__ paths, const uint8_t *__restrict__ occupancy,
     const float *__restrict__ overhead, float *__restrict__ state, int C, simaps_debug dbg, unsigned *fault)
 {
-    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-    Shared &sh = *reinterpret_cast<Shared *>(smem);
-    float *dist = reinterpret_cast<float *>(smem + OFF_DIST);
-    SsspScratch &S = *reinterpret_cast<SsspScratch *>(smem + OFF_UNION);
-    float *tile = reinterpret_cast<float *>(smem + OFF_UNION);
-
-    const int n = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int H = cfg.H, W = cfg.W;
-    if (tid == 0) STAMP_NB(77);  // kernel entry (dispatch skew)
-    simaps_agent ag = agents[n];
-    // Sources of the shortest-path maps (envs.py:2071-2113 order): receptacle, then the robot.
-    const int nsrc = (cfg.use_shortest_path_to_receptacle_map ? 1 : 0) + (cfg.use_shortest_path_map ? 1 : 0);
-    // Two tracks run concurrently from the start: waves [0, cs_waves) build the cspace, snap the
-    // sources and sweep the distance arrays (4 waves per source); the other waves compute the robot
-    // parameters and stamp tiles and render every channel that does not need distances.
-    const int cs_waves = nsrc > 0 ? 4 * nsrc : (dbg.cspace ? 4 : 0);
-    // Small rooms (every small_* BASELINE config): the crop's robot-code map fits in the tail of
-    // distance array 1, outside the raster tile, and the sweep track zeroes the tile when it
-    // releases its scratch (early_tile).  Otherwise the code map lies in the union after the sweep
-    // scratch and the render track zeroes the tile after a barrier.
-    const bool early_tile =
-        nsrc > 0 && (cfg.room_h + 2) * sssp_pitch(cfg.room_w) * 4 <= DIST_FLOATS * 4 - CMAP_BYTES;
-    uint8_t *cmap = reinterpret_cast<uint8_t *>(smem) + (early_tile ? OFF_UNION - CMAP_BYTES : OFF_CMAP);
-    const bool tail_cells = early_tile && !cfg.use_distance_to_receptacle_map &&
-                            tail_cells_off(cfg.room_h, cfg.room_w) + LW * LW * 2 <= DIST_FLOATS * 4;
-    if (tid < 16) (&sh.bar[0][0])[tid] = 0u;
-    if (tid == 16) sh.scratch_free = cs_waves == 0;
-    simaps_env ev = envs[ag.env];
-    // descriptors come through the C ABI unchecked: clamp what would index past the LDS tables
-    // (robot records, segment slots) and report it (SIMAPS_FAULT_DESCRIPTOR)
-    const bool bad_desc = (unsigned)(ev.num_robots - 1) >= (unsigned)SIMAPS_MAX_ROBOTS ||
-                          (unsigned)ag.robot >= (unsigned)ev.num_robots;
-    ev.num_robots = min(max(ev.num_robots, 1), SIMAPS_MAX_ROBOTS);
-    if ((unsigned)ag.robot >= (unsigned)ev.num_robots) ag.robot = 0;
-    lds_barrier();  // the group barriers are zeroed
-    if (tid == 0 && bad_desc) sh.bar[0][3] = 1u;
-    if (tid == 0) STAMP_NB(0);
-    float *out = state + (size_t)n * LW * LW * C;
-    const RenderCtx rc{cfg, sh, out, C, n};
-    if ((tid >> 6) < cs_waves) {
-        const Group g{tid, 64 * cs_waves, sh.bar[0], cs_waves};
-        if (cs_waves == 8) sweep_track<512>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g, early_tile);
-        else sweep_track<256>(sh, S, dist, cfg, geo, ag, ev, robots, occupancy, nsrc, dbg, n, g, early_tile);
-        STAMP_NB(7);
-    } else {
-        const int nw = NT / 64 - cs_waves;
-        const Group g{tid - 64 * cs_waves, 64 * nw, cs_waves ? sh.bar[1] : nullptr, nw};
-        const int t = g.t;
-        const simaps_robot *rb = robots + ev.robot_off;
-        // ---- parameters (one lane per robot; the agent's own local rotation on another wave)
-        if (t == 0) {
-            sh.nr = ev.num_robots;
-            sh.me = ag.robot;
-            sh.env = ag.env;
-            sh.has_rec = ev.has_receptacle;
-        }
-        if (t == 64) {
-            const simaps_robot &me = rb[ag.robot];
-            sh.rot = rot_params(CROP, 90.0 - me.heading * RAD_TO_DEG, cfg.rotate_rounding == SIMAPS_ROT_PLAIN);
-            pos_to_pix(me.x, me.y, H, W, sh.pi, sh.pj);
-            STAMP_NB(72);
-        }
-        if (t >= 128 && t < 128 + ev.num_robots) {
-            const int k = t - 128;
-            const simaps_robot &r = rb[k];
-            RobotP &P = sh.rob[k];
-            if ((cfg.use_intention_map && r.intention_len > SIMAPS_MAX_PATH) ||
-                (cfg.use_history_map && r.history_len > SIMAPS_MAX_PATH))  // cut to SIMAPS_MAX_PATH points
-                __hip_atomic_store(&sh.bar[0][3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const Rot R = rot_params(LW, r.heading * RAD_TO_DEG - 90.0, cfg.rotate_rounding == SIMAPS_ROT_PLAIN);
-            P.c = R.c; P.s = R.s; P.f0 = R.f0; P.f1 = R.f1; P.S0 = R.S0; P.S1 = R.S1;
-            int pi, pj;
-            pos_to_pix(r.x, r.y, H, W, pi, pj);
-            P.st_i = pi - R.S0 / 2;
-            P.st_j = pj - R.S1 / 2;
-            P.type = r.type; P.lifting = r.lifting; P.idle = r.idle; P.group = r.group_index;
-            P.x = r.x; P.y = r.y; P.tx = r.target_x; P.ty = r.target_y;
-            pos_to_pix(r.target_x, r.target_y, H, W, P.tpi, P.tpj);
-            {   // conservative prefilter box: inverse-rotate the mask's nonzero window (+-2 px)
-                const int st = geo.mask_start[r.type], wd = geo.mask_width[r.type];
-                const double lo0 = st - (r.type == SIMAPS_LIFTING ? geo.cube_w : 0) - 1.0, hi0 = st + wd + 1.0;
-                const double lo1 = st - 1.0, hi1 = st + wd + 1.0;
-                double mn0 = 1e30, mx0 = -1e30, mn1 = 1e30, mx1 = -1e30;
-                for (int q = 0; q < 4; q++) {
-                    const double a = ((q & 1) ? hi0 : lo0) - R.f0, b = ((q & 2) ? hi1 : lo1) - R.f1;
-                    const double o0 = R.c * a - R.s * b, o1 = R.s * a + R.c * b;
-                    mn0 = fmin(mn0, o0); mx0 = fmax(mx0, o0); mn1 = fmin(mn1, o1); mx1 = fmax(mx1, o1);
-                }
-                P.bi0 = max(P.st_i, P.st_i + (int)floor(mn0) - 2);
-                P.bi1 = min(P.st_i + R.S0 - 1, P.st_i + (int)ceil(mx0) + 2);
-                P.bj0 = max(P.st_j, P.st_j + (int)floor(mn1) - 2);
-                P.bj1 = min(P.st_j + R.S1 - 1, P.st_j + (int)ceil(mx1) + 2);
-                P.bi1 = min(P.bi1, P.bi0 + 31);  // the window is <= 17 x 13 px: its rotated box fits 32 x 32
-                P.bj1 = min(P.bj1, P.bj0 + 31);
-            }
-            P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
-            P.code0 = (1u << r.group_index) | (r.type != SIMAPS_LIFTING ? 1u << 5 : (!r.lifting ? 1u << 4 : 0u));
-            if (k == 0) STAMP_NB(73);
-        }
-        {   // the crop's robot-code map starts empty; with 8 render waves the zeroing goes to the
-            // waves without parameter work (3, 4, 6, 7), so the robot and segment waves reach the
-            // barrier sooner
-            const int w8 = t >> 6;
-            const bool z8 = g.n == 512;
-            const int zt = z8 ? (w8 == 3 || w8 == 4 ? t - 192 : (w8 >= 6 ? t - 256 : -1)) : t;
-            const int zn = z8 ? 256 : g.n;
-            if (zt >= 0) {
-                uint4 *cz = reinterpret_cast<uint4 *>(cmap);
-                for (int k = zt; k < CMAP_BYTES / 16; k += zn) cz[k] = uint4{0u, 0u, 0u, 0u};
-                if (early_tile) {  // the raster tile beyond the cspace scratch (the sweep track zeroes the rest)
-                    uint4 *tz = reinterpret_cast<uint4 *>(tile);
-                    for (int k = SCRATCH_Q + zt; k < TILE * TILE / 4; k += zn) tz[k] = uint4{0u, 0u, 0u, 0u};
-                }
-            }
-        }
-        // the first history / intention pass's segment table, one lane per robot (raster_lines)
-        const bool segs = (cfg.use_history_map || cfg.use_intention_map) && t >= 320 &&
-                          t < 320 + ev.num_robots * SEG_PER_ROBOT;
-        if (segs) {
-            seg_geom(sh, cfg, rb, paths, cfg.use_history_map ? 4 : cfg.intention_map_encoding, t - 320, ag.robot);
-            if (t == 320) STAMP_NB(74);
-        }
-        // the 5 host-computed robot mask windows (stamp tiles below)
-        if (t < 5 * 24) sh.mwin[t] = geo.mbits[t / 24][t % 24];
-        if (t >= 192 && t < 192 + 20) {
-            const int q = t - 192, m = q >> 2, f = q & 3;
-            sh.mwin[120 + q] = f == 0 ? geo.mrow0[m] : f == 1 ? geo.mcol0[m] : f == 2 ? geo.mnrows[m] : geo.mncols[m];
-        }
-        if (t == 0) STAMP_NB(75);
-        g.sync();
-        if (t == 0) STAMP_NB(9);
-        if (segs) seg_ramp(sh, t - 320);  // (the segment table is read at raster time, many barriers later)
-        if (cfg.use_intention_channels && t == 256) intention_channel_order(sh, cfg, rb);
-
-        if (t == 0) STAMP_NB(51);
-        // ---- rotated robot stamps (Mapper._create_global_robot_map, envs.py:2251-2276): each robot's
-        // scipy-rotated mask, evaluated once per workgroup over its <= 32 x 32 global box; the set
-        // pixels inside the crop OR their code into the crop's robot-code map (bit g = seg value
-        // (g + 5) / 8 of SEG_VALUES robot_group_{g+1}, bit 4 = 0.5, bit 5 = 1.0 lifted-cube mask)
-        uint32_t *cmap32 = reinterpret_cast<uint32_t *>(cmap);
-        const int ci0 = sh.pi - HALF_CROP, cj0 = sh.pj - HALF_CROP;
-        // Waves own robots (nw / nr waves per robot, interleaved over its box rows); per wave-item 2
-        // box rows (lane -> row 2 rp + lane / 32, column lane % 32).  The robot's parameters and mask
-        // window bounds are loaded once per wave; source positions exactly in fp64 (rot_src).
-        const int ln = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
-        const int nrb = ev.num_robots, wpr = nrb <= nw ? nw / nrb : 1;
-        for (int kk = wv; kk < nrb * wpr; kk += nw) {
-            const int k = kk % nrb, sub = kk / nrb;
-            const RobotP &P = sh.rob[k];
-            const int bi0 = __builtin_amdgcn_readfirstlane(P.bi0), bi1 = __builtin_amdgcn_readfirstlane(P.bi1);
-            const int bj0 = P.bj0, bj1 = P.bj1, st_i = P.st_i, st_j = P.st_j;
-            const int type = P.type;
-            const bool cube = type == SIMAPS_LIFTING && P.lifting;
-            const unsigned code0 = P.code0;
-            const Rot R{P.c, P.s, P.f0, P.f1, P.S0, P.S1};
-            const int *mt = reinterpret_cast<const int *>(sh.mwin + 120 + 4 * type);
-            const int *mc = reinterpret_cast<const int *>(sh.mwin + 120 + 4 * 4);
-            const int mt0 = mt[0], mt1 = mt[1], mt2 = mt[2], mt3 = mt[3];
-            const int mc0 = mc[0], mc1 = mc[1], mc2 = mc[2], mc3 = mc[3];
-            // (two box-row pairs per iteration, their fp64 chains interleaved, measured slower: the
-            // stamps phase 3.8 -> 4.4 us, round 4)
-            for (int rp = sub; 2 * rp <= bi1 - bi0; rp += wpr) {
-                const int gi = bi0 + 2 * rp + (ln >> 5), gj = bj0 + (ln & 31);
-                unsigned code = 0;
-                if (gi <= bi1 && gj <= bj1) {
-                    int m0, m1;
-                    const bool in = rot_src(R, LW, gi - st_i, gj - st_j, m0, m1);
-                    if (in) {
-                        const int r = m0 - mt0, cc = m1 - mt1;
-                        if ((unsigned)r < (unsigned)mt2 && (unsigned)cc < (unsigned)mt3 && ((sh.mwin[type * 24 + r] >> cc) & 1u))
-                            code = code0;
-                        const int r2 = m0 - mc0, c2 = m1 - mc1;
-                        if (cube && (unsigned)r2 < (unsigned)mc2 && (unsigned)c2 < (unsigned)mc3 && ((sh.mwin[4 * 24 + r2] >> c2) & 1u))
-                            code |= 1u << 5;
-                    }
-                }
-                const int ca = gi - ci0, cb = gj - cj0;
-                if (code && (unsigned)ca < (unsigned)CROP && (unsigned)cb < (unsigned)CROP) {
-                    const int pos = ca * CROP + cb;
-                    atomicOr(&cmap32[pos >> 2], code << (8 * (pos & 3)));
-                }
-            }
-        }
-        g.sync();
-        if (t == 0) STAMP_NB(1);
-        const float *ovh = overhead + (size_t)ag.map_slot * H * W;
-        if (nw == 8) render_maps<18>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile, tail_cells, dist);
-        else if (nw == 12) render_maps<12>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile, tail_cells, dist);
-        else render_maps<9>(rc, g, geo, ovh, rb, paths, tile, cmap, early_tile, tail_cells, dist);
-        if (t == 0) STAMP_NB(8);
-    }
-    lds_barrier();
-    STAMP(4);
-
-    // ---- all waves: distance channels (need the converged sweeps)
-    STAMP(5);
-    render_distance_channels(rc, ev, dist, nsrc, reinterpret_cast<const uint16_t *>(tile),
-                             tail_cells ? reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(dist) +
-                                                                          tail_cells_off(cfg.room_h, cfg.room_w))
-                                        : reinterpret_cast<const uint16_t *>(tile) + LW * LW);
-    STAMP(6);
-
-    // ---- debug outputs
-    if (nsrc > 0) {
-        if (dbg.sources && tid < 2) {
-            int32_t *o = dbg.sources + ((size_t)n * 2 + tid) * 4;
-            const int s = sh.sp_slot[tid];
-            if (s >= 0) { o[0] = sh.src_q[s][0]; o[1] = sh.src_q[s][1]; o[2] = sh.src_s[s][0]; o[3] = sh.src_s[s][1]; }
-            else { o[0] = o[1] = o[2] = o[3] = -1; }
-        }
-    }
-    if (tid == 0) {
-        const unsigned f = group_faults(sh.bar, sh.rounds, nsrc);
-        post_faults(fault, f);
-        if (dbg.status) {
-            int st = (f & SIMAPS_FAULT_ROUNDS ? 2 : 0) | (f & SIMAPS_FAULT_TIMEOUT ? 4 : 0) |
-                     (f & SIMAPS_FAULT_DESCRIPTOR ? 8 : 0);
-            for (int s = 0; s < nsrc; s++) st |= sh.src_ok[s] ? 0 : 1;
-            dbg.status[n] = st | ((nsrc > 0 ? sh.rounds & 0xfffff : 0) << 8);
-        }
-    }
-#ifdef SIMAPS_PHASE_STAMPS
-    if (tid == 0 && blockIdx.x < MAX_STAMP_WG) g_stamps[blockIdx.x * NSTAMP + 10] = (unsigned long long)sh.rounds;
-#endif
+#define GS_MIXED 0
+#include "get_state_body.inc"
+#undef GS_MIXED
 }
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // Reward lookups from the receptacle distance cache (simaps_sp_lookup)
@@ -2551,6 +2332,7 @@ struct LookupScratch {
     B128 freeb[MAX_ROWS];
 };
 constexpr int LNT = 128;  // two waves: snap_sources' two slots
+#ifndef SIMAPS_DEVICE_ONLY
 __global__ void __launch_bounds__(LNT) sp_lookup_kernel(simaps_config cfg, const simaps_agent *__restrict__ agents,
                                                         const char *__restrict__ rec_cache, int rec_bytes,
                                                         const double *__restrict__ targets, int Q,
@@ -2630,10 +2412,12 @@ __global__ void __launch_bounds__(LNT) sp_lookup_kernel(simaps_config cfg, const
         if (c0 + 64 < Q) lds_barrier();  // every wave has read slow_mask before the next chunk rewrites it
     }
 }
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // GridGraph.shortest_path_image for arbitrary grids (one workgroup per grid)
 // ------------------------------------------------------------------------------------------------
+#ifndef SIMAPS_DEVICE_ONLY
 __global__ void __launch_bounds__(NT) sssp_grid_kernel(int H, int W, const uint8_t *__restrict__ grids,
                                                       const int32_t *__restrict__ sources, float *__restrict__ out,
                                                       int wi0, int wj0, int wh, int ww, unsigned *fault)
@@ -2672,6 +2456,7 @@ __global__ void __launch_bounds__(NT) sssp_grid_kernel(int H, int W, const uint8
         out[(size_t)b * H * W + k] = v;
     }
 }
+#endif
 
 // The robot class of agent ag with get_state_kernel's descriptor clamps (num_robots in [1,
 // SIMAPS_MAX_ROBOTS], robot index < num_robots, class < 4); `bad` = something was clamped
@@ -2692,6 +2477,7 @@ __device__ __forceinline__ int agent_robot_type(const simaps_agent &ag, const si
 // Reward lookups: OccupancyMap.shortest_path_distance (envs.py:2507-2512) from one source position to
 // Q target positions on each agent's own map (Mapper.distance_to_receptacle, envs.py:2190-2194)
 // ------------------------------------------------------------------------------------------------
+#ifndef SIMAPS_DEVICE_ONLY
 __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geometry geo,
                                                          const simaps_agent *__restrict__ agents,
                                                          const simaps_env *__restrict__ envs,
@@ -2781,6 +2567,7 @@ __global__ void __launch_bounds__(NT) sp_distance_kernel(simaps_config cfg, Geom
         if (c0 + 64 < Q) lds_barrier();  // every wave has read slow_mask before the next chunk rewrites it
     }
 }
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // Movement paths: OccupancyMap.shortest_path (envs.py:2478-2505) = straight-line test on cspace_thin,
@@ -4201,10 +3988,13 @@ __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
     }
 }
 
+#ifndef SIMAPS_DEVICE_ONLY
 #include "grid_large.h"
+#endif
 
 }  // namespace
 
+#ifndef SIMAPS_DEVICE_ONLY
 // =================================================================================================
 // C ABI
 // =================================================================================================
@@ -4582,6 +4372,44 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
     return 0;
 }
 
+int simaps_get_state_mixed(const simaps_config *cfgs, const int32_t *num_robots_per_env, int n_cfgs, int N,
+                           const simaps_agent *agents, const int32_t *agent_cfg, const simaps_env *envs,
+                           const simaps_robot *robots, const double *paths, const uint8_t *occupancy,
+                           const int64_t *map_off, const float *overhead, float *state, const int64_t *out_off,
+                           void *stream)
+{
+    if (!cfgs || n_cfgs < 1 || n_cfgs > SIMAPS_MAX_MIXED)
+        return fail(SIMAPS_EINVAL, "n_cfgs %d not in [1, %d]", n_cfgs, SIMAPS_MAX_MIXED);
+    const Geometry &geo = geometry();
+    for (int t = 0; t < 4; t++)
+        if (geo.cspace_r[t] > RMAX) return fail(SIMAPS_EUNSUPPORTED, "cspace radius %d > %d", geo.cspace_r[t], RMAX);
+    simaps_mixed::MixedCfgs mx;
+    memset(&mx, 0, sizeof(mx));
+    bool any_paths = false;
+    for (int k = 0; k < n_cfgs; k++) {
+        if (const int rc = check_cfg(&cfgs[k])) return rc;
+        const int nr = num_robots_per_env ? num_robots_per_env[k] : 0;
+        if (cfgs[k].use_intention_channels && (nr < 1 || nr > SIMAPS_MAX_ROBOTS))
+            return fail(SIMAPS_EINVAL, "configuration %d: intention channels need num_robots_per_env in [1, %d]", k,
+                        SIMAPS_MAX_ROBOTS);
+        mx.cfg[k] = cfgs[k];
+        mx.C[k] = simaps_num_channels(&cfgs[k], nr > 0 ? nr : 1);
+        any_paths = any_paths || cfgs[k].use_intention_map || cfgs[k].use_history_map;
+    }
+    mx.n = n_cfgs;
+    if (N < 0) return fail(SIMAPS_EINVAL, "N < 0");
+    if (N == 0) return 0;
+    if (!agents || !agent_cfg || !envs || !robots || !occupancy || !map_off || !overhead || !state || !out_off)
+        return fail(SIMAPS_EINVAL, "NULL buffer");
+    if (any_paths && !paths) return fail(SIMAPS_EINVAL, "paths is NULL");
+    if (const int rc = pending_faults()) return rc;
+    simaps_mixed::launch_get_state_mixed(mx, geo, N, agents, agent_cfg, envs, robots, paths, occupancy, map_off, overhead,
+                                         state, out_off, g_fault_dev, (hipStream_t)stream);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "get_state_mixed launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
 int simaps_rec_cache_bytes(const simaps_config *cfg)
 {
     const int rc = check_cfg(cfg);
@@ -4798,3 +4626,4 @@ int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *s
 }
 
 }  // extern "C"
+#endif  // SIMAPS_DEVICE_ONLY

@@ -28,7 +28,8 @@ ROBOT_DTYPE = np.dtype([('x', '<f8'), ('y', '<f8'), ('heading', '<f8'), ('target
                         ('history_len', '<i4')], align=True)
 ENV_DTYPE = np.dtype([('receptacle_x', '<f8'), ('receptacle_y', '<f8'), ('has_receptacle', '<i4'),
                       ('robot_off', '<i4'), ('num_robots', '<i4'), ('reserved', '<i4')], align=True)
-ABI_VERSION = 7  # include/simaps.h SIMAPS_ABI_VERSION
+ABI_VERSION = 8  # include/simaps.h SIMAPS_ABI_VERSION
+MAX_MIXED = 8  # SIMAPS_MAX_MIXED
 AGENT_DTYPE = np.dtype([('env', '<i4'), ('robot', '<i4'), ('map_slot', '<i4')], align=True)
 assert ROBOT_DTYPE.itemsize == 72 and ENV_DTYPE.itemsize == 32 and AGENT_DTYPE.itemsize == 12
 
@@ -82,6 +83,10 @@ def _load(path=LIB_PATH):
     L.simaps_get_state.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, vp, i32,
                                    ctypes.POINTER(Debug), vp]
     L.simaps_get_state.restype = i32
+    if hasattr(L, 'simaps_get_state_mixed'):  # (ABI 8; absent only in an older revision's A/B build)
+        L.simaps_get_state_mixed.argtypes = [ctypes.POINTER(Config), vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                             vp, vp]
+        L.simaps_get_state_mixed.restype = i32
     L.simaps_sp_distance.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.simaps_sp_distance.restype = i32
     if hasattr(L, 'simaps_sp_lookup'):  # (ABI 7; absent only in an older revision's A/B build)
@@ -133,7 +138,8 @@ lib = _load()
 
 EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_fault_status', 'simaps_num_channels',
             'simaps_robot_mask', 'simaps_pack_robots', 'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest', 'simaps_ingest_chunks', 'simaps_path_mode',
-            'simaps_sssp_grid', 'simaps_grid_path', 'simaps_rec_cache_bytes', 'simaps_sp_lookup')
+            'simaps_sssp_grid', 'simaps_grid_path', 'simaps_rec_cache_bytes', 'simaps_sp_lookup',
+            'simaps_get_state_mixed')
 
 # error codes and device fault bits (include/simaps.h)
 EINVAL, EUNSUPPORTED, EHIP, EDEVICE = -1, -2, -3, -4

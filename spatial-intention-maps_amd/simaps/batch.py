@@ -710,3 +710,116 @@ def grid_paths(grids, sources, targets, window=None, max_points=256, stream=None
             return grid_paths(grids, sources, targets, window, int(-cnt.min()), stream, grow=False)
         raise RuntimeError('a path has %d waypoints > max_points=%d' % (-cnt.min(), max_points))
     return _point_lists(ij, cnt)
+
+
+def config_key(scene):
+    """What one launch of simaps_get_state shares: grid, room, flags and the rotate rounding."""
+    return (scene['H'], scene['W'], scene['room_width'], scene['room_length'],
+            tuple(sorted(scene['flags'].items())), K.scene_rotate_rounding(scene))
+
+
+def plan_mixed(scenes, layout='chw'):
+    """Host plan of a mixed-configuration launch (simaps_get_state_mixed): the distinct
+    configurations in order of first appearance (at most _lib.MAX_MIXED), each env's configuration,
+    and for agent n = (env e, robot a) in scene order: its configuration, its map slot's element
+    offset (slot n; maps of H x W of its configuration, back to back) and its stack's float offset
+    (96 * 96 * C of its configuration, back to back)."""
+    keys, cfg_of_env = [], []
+    for s in scenes:
+        k = config_key(s)
+        if k not in keys:
+            keys.append(k)
+        cfg_of_env.append(keys.index(k))
+    if len(keys) > _lib.MAX_MIXED:
+        raise ValueError('at most %d configurations per mixed launch (got %d)' % (_lib.MAX_MIXED, len(keys)))
+    first = [cfg_of_env.index(k) for k in range(len(keys))]
+    cfgs, nrs, chans = [], [], []
+    for k, e0 in enumerate(first):
+        s0 = scenes[e0]
+        nr = len(s0['robots'])
+        if s0['flags']['use_intention_channels'] and any(len(scenes[e]['robots']) != nr
+                                                          for e in range(len(scenes)) if cfg_of_env[e] == k):
+            raise ValueError('intention channels need the same robot count in every env of a configuration')
+        c = make_config(s0['flags'], s0['room_width'], s0['room_length'], layout, K.scene_rotate_rounding(s0))
+        cfgs.append(c)
+        nrs.append(nr if s0['flags']['use_intention_channels'] else 0)
+        chans.append(_lib.lib.simaps_num_channels(c, nr))
+    agents = [(e, a) for e, s in enumerate(scenes) for a in range(len(s['robots']))]
+    agent_cfg = np.array([cfg_of_env[e] for e, _ in agents], dtype=np.int32)
+    hw = np.array([scenes[e]['H'] * scenes[e]['W'] for e, _ in agents], dtype=np.int64)
+    per = np.array([K.LOCAL_MAP_PIXEL_WIDTH ** 2 * chans[k] for k in agent_cfg], dtype=np.int64)
+    map_off = np.concatenate([[0], np.cumsum(hw)[:-1]]).astype(np.int64) if len(hw) else hw
+    out_off = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.int64) if len(per) else per
+    return {'cfgs': cfgs, 'num_robots': nrs, 'channels': chans, 'cfg_of_env': cfg_of_env, 'agents': agents,
+            'agent_cfg': agent_cfg, 'map_off': map_off, 'map_numel': int(hw.sum()), 'out_off': out_off,
+            'out_numel': int(per.sum())}
+
+
+class MixedStateBatch:
+    """Envs of several configurations (grid, room, flags, rotate rounding; at most _lib.MAX_MIXED)
+    rendered in ONE launch (simaps_get_state_mixed) -- e.g. the envs of several reference workers,
+    each of which runs one configuration (train_multiprocess.py:159-166).  Every agent of every scene
+    is a map slot, in scene order.  render() returns one flat float32 tensor; states() gives each
+    agent's (C, 96, 96) (layout 'chw') or (96, 96, C) ('hwc') view of it, C that of its own
+    configuration.  The results equal one StateBatch.render per configuration, bit for bit."""
+
+    def __init__(self, scenes, device='cuda', layout='chw'):
+        if not scenes:
+            raise ValueError('a MixedStateBatch needs at least one scene')
+        if layout not in ('chw', 'hwc'):
+            raise ValueError('layout must be chw or hwc')
+        self.device = resolve_device(device)
+        if self.device.type != 'cuda':
+            raise ValueError('MixedStateBatch renders on a GPU device (got %s); there is no CPU path' % self.device)
+        self.layout = layout
+        self.plan = plan_mixed(scenes, layout)
+        self.scenes, self.agents, self.N = scenes, self.plan['agents'], len(self.plan['agents'])
+        occ = np.concatenate([np.asarray(scenes[e]['occupancy'][a], dtype=np.uint8).ravel() for e, a in self.agents])
+        ovh = np.concatenate([np.asarray(scenes[e]['overhead'][a], dtype=np.float32).ravel() for e, a in self.agents])
+        self.occupancy = torch.from_numpy(occ).to(self.device)
+        self.overhead = torch.from_numpy(ovh).to(self.device)
+        self._cfgs = (_lib.Config * len(self.plan['cfgs']))(*self.plan['cfgs'])
+        self._nrs = np.asarray(self.plan['num_robots'], dtype=np.int32)
+        self.agent_cfg_d = torch.from_numpy(self.plan['agent_cfg']).to(self.device)
+        self.map_off_d = torch.from_numpy(self.plan['map_off']).to(self.device)
+        self.out_off_d = torch.from_numpy(self.plan['out_off']).to(self.device)
+        self.set_descriptors(scenes)
+
+    def set_descriptors(self, scenes):
+        """Upload a new per-step scene descriptor (poses, controller state, paths) of the same envs."""
+        if [config_key(s) for s in scenes] != [config_key(s) for s in self.scenes]:
+            raise ValueError('set_descriptors: the envs and their configurations are fixed at construction')
+        robots, envs, ag, paths = pack_descriptors(scenes, self.agents)
+        self.scenes = scenes
+        self.robots_d, self.envs_d, self.agents_d, self.paths_d = (_to_dev(x, self.device) for x in (robots, envs, ag, paths))
+
+    def alloc_state(self):
+        return torch.empty((self.plan['out_numel'],), dtype=torch.float32, device=self.device)
+
+    def render(self, out=None, stream=None):
+        """One launch for every agent; asynchronous on `stream` (default: the current stream)."""
+        if out is None:
+            out = self.alloc_state()
+        if not (out.is_contiguous() and out.dtype == torch.float32 and out.numel() == self.plan['out_numel']
+                and out.device == self.device):
+            raise ValueError('out must be a contiguous float32 tensor of %d elements on %s' % (self.plan['out_numel'], self.device))
+        s, cur = launch_stream(self.device, stream)
+        _lib.check(_lib.lib.simaps_get_state_mixed(
+            self._cfgs, self._nrs.ctypes.data, len(self.plan['cfgs']), self.N, _lib.ptr(self.agents_d),
+            _lib.ptr(self.agent_cfg_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d), _lib.ptr(self.paths_d),
+            _lib.ptr(self.occupancy), _lib.ptr(self.map_off_d), _lib.ptr(self.overhead), _lib.ptr(out),
+            _lib.ptr(self.out_off_d), _lib.stream_handle(s)))
+        hold(s, cur, out, self.agents_d, self.agent_cfg_d, self.envs_d, self.robots_d, self.paths_d, self.occupancy,
+             self.map_off_d, self.overhead, self.out_off_d)
+        return out
+
+    def states(self, out):
+        """Per-agent views of a rendered flat tensor, in agent order."""
+        L = K.LOCAL_MAP_PIXEL_WIDTH
+        views = []
+        for n in range(self.N):
+            C = self.plan['channels'][self.plan['agent_cfg'][n]]
+            o = int(self.plan['out_off'][n])
+            v = out[o:o + L * L * C]
+            views.append(v.view(C, L, L) if self.layout == 'chw' else v.view(L, L, C))
+        return views

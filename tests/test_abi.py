@@ -22,7 +22,8 @@ def test_header_declares_the_abi():
                                          'simaps_num_channels', 'simaps_sp_distance', 'simaps_shortest_path',
                                          'simaps_ingest', 'simaps_ingest_chunks', 'simaps_path_mode', 'simaps_robot_mask', 'simaps_pack_robots',
                                          'simaps_get_state', 'simaps_sssp_grid',
-                                         'simaps_grid_path', 'simaps_rec_cache_bytes', 'simaps_sp_lookup'])
+                                         'simaps_grid_path', 'simaps_rec_cache_bytes', 'simaps_sp_lookup',
+                                         'simaps_get_state_mixed'])
 
 
 def test_library_exports_every_declared_symbol():
@@ -31,7 +32,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(_lib.lib, name), name
         assert isinstance(getattr(_lib.lib, name), ctypes._CFuncPtr)
     assert set(_lib.EXPORTED) == set(declared_symbols())
-    assert _lib.lib.simaps_abi_version() == 7
+    assert _lib.lib.simaps_abi_version() == 8
 
 
 def test_struct_layouts_match_header():
