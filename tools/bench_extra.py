@@ -5,6 +5,8 @@
   ingest         Robot.update_map minus the simulator (camera frame -> overhead / occupancy maps): frames/s
   distance_to_receptacle  the reward lookups from the receptacle, cold and from the render's cache
   env_step       (--env-step) the device time of one reference VectorEnv.step: paths, ingest, get_state
+  mixed          (--mixed) one launch over envs of the BASELINE configurations together
+                 (simaps_get_state_mixed) vs one launch per configuration back to back
   gridgraph_large (--gridgraph-large) GridGraph on a 500 x 500 grid (beyond the LDS window: the
                  global-memory kernels of csrc/grid_large.h): images and paths, 1 and 64 per call
 
@@ -295,6 +297,48 @@ def bench_ingest(args):
           flush=True)
 
 
+def bench_mixed(envs=64, steps=50):
+    """`envs` envs of each BASELINE configuration (configs[0..4]; pushing_4-large_empty and
+    lifting_2_throwing_2-large_empty share one), interleaved env by env, rendered by ONE
+    MixedStateBatch launch vs one StateBatch launch per configuration back to back on the same
+    stream.  Device time by HIP events over `steps` launches (sequences) after warm-up."""
+    cfgs = ['lifting_1-small_empty', 'lifting_4-small_divider', 'pushing_4-large_empty',
+            'lifting_2_throwing_2-large_empty', 'rescue_4-small_empty']
+    scenes = [synthetic.make_scene(c, 1000 * k + e) for e in range(envs) for k, c in enumerate(cfgs)]
+    mb = batch.MixedStateBatch(scenes)
+    out = mb.alloc_state()
+    groups = {}
+    for s in scenes:
+        groups.setdefault(batch.config_key(s), []).append(s)
+    sbs = [batch.StateBatch(g) for g in groups.values()]
+    outs = [b.alloc_state() for b in sbs]
+    s = torch.cuda.current_stream()
+    res = {}
+    for name, f in (('mixed', lambda: mb.render(out)), ('per_config', lambda: [b.render(o) for b, o in zip(sbs, outs)])):
+        for _ in range(5):
+            f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(steps):
+            f()
+        e1.record(s)
+        torch.cuda.synchronize()
+        res[name] = e0.elapsed_time(e1) / steps
+    got = mb.states(out)
+    env_of = {id(sc): i for i, sc in enumerate(scenes)}
+    slot = {ea: k for k, ea in enumerate(mb.agents)}
+    ok = all(torch.equal(got[slot[(env_of[id(b.scenes[e])], a)]], o[n])
+             for b, o in zip(sbs, outs) for n, (e, a) in enumerate(b.agents))
+    print(json.dumps({'row': 'mixed', 'configs': cfgs, 'envs_per_config': envs, 'stacks': mb.N,
+                      'configurations_in_launch': len(mb.plan['cfgs']),
+                      'mixed_ms': res['mixed'], 'per_config_ms': res['per_config'],
+                      'mixed_stacks_per_s': mb.N / (res['mixed'] * 1e-3),
+                      'per_config_stacks_per_s': mb.N / (res['per_config'] * 1e-3),
+                      'per_config_launches': len(sbs), 'mixed_equals_per_config': bool(ok),
+                      'note': 'HIP events over %d launches (sequences); inputs resident' % steps}), flush=True)
+
+
 def bench_gridgraph_large(n=500, density=0.25, seed=505):
     """GridGraph(grid).shortest_path_image / shortest_path on an n x n random grid (obstacle density
     `density`), B = 1 and 64 queries per launch, against the oracle's C SPFA (the reference's
@@ -332,6 +376,9 @@ def bench_gridgraph_large(n=500, density=0.25, seed=505):
 
 
 if __name__ == '__main__':
+    if '--mixed' in sys.argv:
+        bench_mixed()
+        sys.exit(0)
     if '--gridgraph-large' in sys.argv:
         bench_gridgraph_large()
         sys.exit(0)
