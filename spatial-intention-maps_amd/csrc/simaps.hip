@@ -1146,7 +1146,7 @@ __device__ __forceinline__ void mark_range(uint64_t *m, int a, int b)  // bits a
 
 // SSSP_CHECK: the rounds end with the fixpoint check below (sssp_check) instead of inline marks.
 #ifdef SIMAPS_SSSP_CHECK
-constexpr bool SSSP_CHECK = true;   // (A/B build: measured slower)
+constexpr bool SSSP_CHECK = true;   // (A/B build: measured slower, HISTORY.md Appendix C)
 #else
 constexpr bool SSSP_CHECK = false;  // the product: inline marks + a confirming round
 #endif
@@ -1248,7 +1248,7 @@ __device__ __forceinline__ bool sweep(float *Dg, int h, int w, int pw, int dir_i
 // at an assumed ~1,500-cycle check) and built: bitwise, 3 rounds instead of 4 and -35 % line steps
 // on the BASELINE config, but the check itself costs ~2.2 us per round in the kernel (~25 VALU
 // per row on SIMDs shared with the render waves) plus a second barrier, so every config measured
-// slower.  Kept as the SIMAPS_SSSP_CHECK A/B build, not the product.
+// slower (HISTORY.md Appendix C).  Kept as the SIMAPS_SSSP_CHECK A/B build, not the product.
 // Threads t of n (n = 64 * waves, this source's group): lane l owns columns 2l + 1, 2l + 2
 // (w <= 126), wave q a block of rows; returns true (uniform per wave) if this wave found a violation.
 __device__ __forceinline__ uint64_t spread_even(uint32_t x)  // bit i -> bit 2i

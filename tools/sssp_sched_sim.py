@@ -14,7 +14,7 @@ and two ways to decide what the next round sweeps are compared:
 Both reach the oracle's SPFA fixpoint (asserted).  The output is the critical path of the sweep
 waves per source in cycles: per round the slowest wave (its line steps x the step cost of its
 cells-per-lane layout), plus a barrier per round, plus the check passes.  The step costs are
-DESIGN.md section 9's in-kernel measurements (tools/micro/sweep_mb.hip at 8 waves: 148 cycles for
+HISTORY.md Appendix C's in-kernel measurements (tools/micro/sweep_mb.hip at 8 waves: 148 cycles for
 the 2-cells-per-lane step; the 1-cell step runs 9 of its 17 instructions).
 
     python tools/sssp_sched_sim.py [--config lifting_4-small_divider] [--envs 32]
