@@ -813,6 +813,34 @@ class MixedStateBatch:
              self.map_off_d, self.overhead, self.out_off_d)
         return out
 
+    def set_maps(self, occupancy=None, overhead=None, slots=None):
+        """Replace the global maps (Mapper.update / OccupancyMap.update, envs.py:2056-2062, 2447-2450)
+        of every map slot, or of `slots` only: one [H, W] map per slot, of its own configuration's
+        grid (uint8 occupancy, float32 overhead-without-robots), arrays or tensors.  One upload per
+        argument; the copies are ordered on the current stream like StateBatch.set_maps."""
+        slots = list(range(self.N)) if slots is None else [int(k) for k in slots]
+        if any(k < 0 or k >= self.N for k in slots):
+            raise ValueError('slots must lie in [0, %d)' % self.N)
+        shapes = [(self.scenes[self.agents[k][0]]['H'], self.scenes[self.agents[k][0]]['W']) for k in slots]
+        for name, src, dst, dt in (('occupancy', occupancy, self.occupancy, torch.uint8),
+                                   ('overhead', overhead, self.overhead, torch.float32)):
+            if src is None:
+                continue
+            if len(src) != len(slots):
+                raise ValueError('%s: one map per slot (%d), got %d' % (name, len(slots), len(src)))
+            parts = [torch.as_tensor(m) for m in src]
+            for k, m, hw in zip(slots, parts, shapes):
+                if tuple(m.shape) != hw:
+                    raise ValueError('%s of slot %d must have shape %s, got %s' % (name, k, hw, tuple(m.shape)))
+            flat = torch.cat([m.reshape(-1).to(dt) for m in parts]).to(self.device)
+            if slots == list(range(self.N)):
+                dst.copy_(flat)
+            else:
+                off = self.plan['map_off']
+                idx = torch.from_numpy(np.concatenate([np.arange(off[k], off[k] + h * w) for k, (h, w) in
+                                                       zip(slots, shapes)])).to(self.device)
+                dst[idx] = flat
+
     def states(self, out):
         """Per-agent views of a rendered flat tensor, in agent order."""
         L = K.LOCAL_MAP_PIXEL_WIDTH

@@ -172,3 +172,38 @@ def test_intention_channel_robot_count_mismatch_is_contained(S, count):
         with pytest.raises(_lib.DeviceFault, match='descriptor-clamped'):
             _lib.check_faults()
         assert _bitwise(got[4:], clean[4:])
+
+
+def test_mixed_set_maps(S):
+    """set_maps on a subset of slots and on all of them: the render equals one StateBatch per
+    configuration over scenes holding the new maps."""
+    _lib, batch, synthetic = S
+    scenes = _mixed_scenes(synthetic, seed=1100)
+    other = _mixed_scenes(synthetic, seed=1200)  # same configurations and robot counts, other maps
+    mb = batch.MixedStateBatch(scenes)
+    want = [dict(s, occupancy=np.array(s['occupancy']), overhead=np.array(s['overhead'])) for s in scenes]
+    slots = [0, 3, 7, 12, mb.N - 1]
+    pairs = [mb.agents[k] for k in slots]
+    mb.set_maps(occupancy=[other[e]['occupancy'][a] for e, a in pairs],
+                overhead=[torch.as_tensor(other[e]['overhead'][a]).cuda() for e, a in pairs], slots=slots)
+    for e, a in pairs:
+        want[e]['occupancy'][a] = other[e]['occupancy'][a]
+        want[e]['overhead'][a] = other[e]['overhead'][a]
+    got = [v.cpu().numpy() for v in mb.states(mb.render())]
+    ref = _per_config_stacks(batch, want, 'chw')
+    for n, (e, a) in enumerate(mb.agents):
+        assert _bitwise(got[n], ref[(e, a)]), n
+    mb.set_maps(occupancy=[other[e]['occupancy'][a] for e, a in mb.agents],
+                overhead=[other[e]['overhead'][a] for e, a in mb.agents])
+    got = [v.cpu().numpy() for v in mb.states(mb.render())]
+    ref = _per_config_stacks(batch, [dict(s, occupancy=o['occupancy'], overhead=o['overhead'])
+                                     for s, o in zip(scenes, other)], 'chw')
+    for n, (e, a) in enumerate(mb.agents):
+        assert _bitwise(got[n], ref[(e, a)]), n
+    _lib.check_faults()
+    e, a = mb.agents[0]
+    small = np.zeros((3, 3), np.uint8)
+    with pytest.raises(ValueError, match='must have shape'):
+        mb.set_maps(occupancy=[small], slots=[0])
+    with pytest.raises(ValueError, match='one map per slot'):
+        mb.set_maps(occupancy=[small, small], slots=[0])

@@ -3,11 +3,13 @@ through the C ABI in one launch per configuration and compared bitwise with the 
 workers in a process pool; the nonspatial intention channels within 1e-7, like the GPU tests).
 Seeds 5000+ are used by no test.  Prints one JSON line per configuration and a total.
 
-    python tools/fuzz_states.py [envs_per_config] [procs] [--perturb] [--plain]
+    python tools/fuzz_states.py [envs_per_config] [procs] [--perturb] [--plain] [--mixed]
 
 --plain renders and checks with the plain-dgemv rounding of scipy.ndimage.rotate's out_center
 (rotate_plain.npz's host) instead of the FMA one; --perturb also leaves ~10 % of the robots in the
-never-acted state (None waypoints / target / index, idle).
+never-acted state (None waypoints / target / index, idle).  --mixed renders through the mixed-
+configuration launch instead (MixedStateBatch): every configuration's envs, alternately in the
+FMA and the plain rounding, interleaved env by env into launches of up to 8 configurations.
 """
 import json
 import os
@@ -67,8 +69,58 @@ def _oracle(job):
     return O.agent_state(perturbed_scene(cfg, e, perturb, rounding), a)
 
 
+def _matches(got, ref, flags, nr):
+    from test_gpu_parity import _nonspatial_slice
+    ns = _nonspatial_slice(flags, nr)
+    if ns is None:
+        return np.array_equal(got.view(np.int32), ref.view(np.int32))
+    m = np.ones(got.shape[-1], bool)
+    m[ns] = False
+    return (np.array_equal(np.ascontiguousarray(got[..., m]).view(np.int32), np.ascontiguousarray(ref[..., m]).view(np.int32))
+            and np.abs(got[..., ns] - ref[..., ns]).max() <= 1e-7)
+
+
+def main_mixed(envs, procs, perturb):
+    import torch
+    from simaps import _lib, batch
+    jobs = [(cfg, e, 'plain' if e % 2 else 'fma') for e in range(envs) for cfg in CONFIGS]  # interleaved
+    launches, cur, keys = [], [], set()
+    for cfg, e, r in jobs:
+        s = perturbed_scene(cfg, e, perturb, r)
+        k = batch.config_key(s)
+        if k not in keys and len(keys) == _lib.MAX_MIXED:
+            launches.append(cur)
+            cur, keys = [], set()
+        keys.add(k)
+        cur.append(((cfg, e, r), s))
+    if cur:
+        launches.append(cur)
+    total = bad = 0
+    with get_context('spawn').Pool(procs) as pool:
+        for li, launch in enumerate(launches):
+            t0 = time.time()
+            scenes = [s for _, s in launch]
+            mb = batch.MixedStateBatch(scenes, layout='hwc')
+            views = [v.cpu().numpy() for v in mb.states(mb.render())]
+            torch.cuda.synchronize()
+            _lib.check_faults()
+            refs = pool.map(_oracle, [launch[e][0][:2] + (a, perturb, launch[e][0][2]) for e, a in mb.agents], chunksize=4)
+            nb = sum(not _matches(views[n], refs[n], scenes[e]['flags'], len(scenes[e]['robots']))
+                     for n, (e, a) in enumerate(mb.agents))
+            assert len(mb.agents) < 2 or not np.array_equal(views[0].view(np.int32), refs[1].view(np.int32)), \
+                'checker is vacuous'
+            total += mb.N
+            bad += nb
+            print(json.dumps({'launch': li, 'configurations': len(mb.plan['cfgs']), 'envs': len(scenes), 'stacks': mb.N,
+                              'mismatches': nb, 's': round(time.time() - t0, 1), 'perturbed': perturb}), flush=True)
+    print(json.dumps({'mixed': True, 'launches': len(launches), 'total_stacks': total, 'mismatches': bad,
+                      'seeds': [SEED0, SEED0 + envs - 1], 'perturbed': perturb, 'rotate_rounding': 'fma + plain'}), flush=True)
+
+
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith('--')]
+    if '--mixed' in sys.argv:
+        return main_mixed(int(args[0]) if args else 16, int(args[1]) if len(args) > 1 else 16, '--perturb' in sys.argv)
     perturb = '--perturb' in sys.argv
     rounding = 'plain' if '--plain' in sys.argv else 'fma'
     envs = int(args[0]) if len(args) > 0 else 16
