@@ -16,7 +16,7 @@ bash tools/gpu_session.sh \
   "400|r5k_extra|python tools/bench_extra.py" \
   "200|r5k_env|python tools/bench_extra.py --env-step" \
   "200|r5k_mixed|python tools/bench_extra.py --mixed" \
-  "600|r5k_fuzz_mixed|python tools/fuzz_states.py 64 16 --perturb --mixed" \
-  "600|r5k_fuzz_states|python tools/fuzz_states.py 128 16 --perturb" \
-  "600|r5k_fuzz_states_plain|python tools/fuzz_states.py 128 16 --perturb --plain" \
+  "600|r5k_fuzz_mixed|python tools/fuzz_states.py 128 16 --perturb --mixed" \
+  "600|r5k_fuzz_states|python tools/fuzz_states.py 256 16 --perturb" \
+  "600|r5k_fuzz_states_plain|python tools/fuzz_states.py 256 16 --perturb --plain" \
   "400|r5k_fuzz_rows|python tools/fuzz_rows.py --path-mode 0 --seed0 14000 128 4 16"
