@@ -6,7 +6,8 @@ A StateBatch packs E envs x (their agents) of ONE configuration (same grid / fla
   robots / envs / agents / paths: the per-step scene descriptor (poses, controller state, paths)
 and renders every agent's (96, 96, C) float32 stack in one kernel launch.  The per-agent maps are
 meant to stay resident across steps (the reference keeps them in each robot's Mapper); only the
-descriptor (~100 B per robot) changes per step.
+descriptor (~100 B per robot) changes per step.  A MixedStateBatch renders envs of up to 8
+configurations in one launch (simaps_get_state_mixed).
 """
 import numpy as np
 import torch
@@ -718,15 +719,21 @@ def config_key(scene):
             tuple(sorted(scene['flags'].items())), K.scene_rotate_rounding(scene))
 
 
+def mixed_key(scene):
+    """One entry of a mixed launch's configuration table: config_key, plus the robot count when
+    intention channels are on (their number follows it, simaps_num_channels)."""
+    return config_key(scene) + ((len(scene['robots']) if scene['flags']['use_intention_channels'] else None),)
+
+
 def plan_mixed(scenes, layout='chw'):
-    """Host plan of a mixed-configuration launch (simaps_get_state_mixed): the distinct
-    configurations in order of first appearance (at most _lib.MAX_MIXED), each env's configuration,
-    and for agent n = (env e, robot a) in scene order: its configuration, its map slot's element
-    offset (slot n; maps of H x W of its configuration, back to back) and its stack's float offset
-    (96 * 96 * C of its configuration, back to back)."""
+    """Host plan of a mixed-configuration launch (simaps_get_state_mixed): the distinct table
+    entries (mixed_key) in order of first appearance (at most _lib.MAX_MIXED), each env's entry, and
+    for agent n = (env e, robot a) in scene order: its entry, its map slot's element offset (slot n;
+    maps of H x W of its configuration, back to back) and its stack's float offset (96 * 96 * C of
+    its entry, back to back)."""
     keys, cfg_of_env = [], []
     for s in scenes:
-        k = config_key(s)
+        k = mixed_key(s)
         if k not in keys:
             keys.append(k)
         cfg_of_env.append(keys.index(k))
@@ -737,9 +744,6 @@ def plan_mixed(scenes, layout='chw'):
     for k, e0 in enumerate(first):
         s0 = scenes[e0]
         nr = len(s0['robots'])
-        if s0['flags']['use_intention_channels'] and any(len(scenes[e]['robots']) != nr
-                                                          for e in range(len(scenes)) if cfg_of_env[e] == k):
-            raise ValueError('intention channels need the same robot count in every env of a configuration')
         c = make_config(s0['flags'], s0['room_width'], s0['room_length'], layout, K.scene_rotate_rounding(s0))
         cfgs.append(c)
         nrs.append(nr if s0['flags']['use_intention_channels'] else 0)
@@ -756,8 +760,8 @@ def plan_mixed(scenes, layout='chw'):
 
 
 class MixedStateBatch:
-    """Envs of several configurations (grid, room, flags, rotate rounding; at most _lib.MAX_MIXED)
-    rendered in ONE launch (simaps_get_state_mixed) -- e.g. the envs of several reference workers,
+    """Envs of several configurations (grid, room, flags, rotate rounding, and with intention
+    channels the robot count; at most _lib.MAX_MIXED) rendered in ONE launch (simaps_get_state_mixed) -- e.g. the envs of several reference workers,
     each of which runs one configuration (train_multiprocess.py:159-166).  Every agent of every scene
     is a map slot, in scene order.  render() returns one flat float32 tensor; states() gives each
     agent's (C, 96, 96) (layout 'chw') or (96, 96, C) ('hwc') view of it, C that of its own
@@ -787,7 +791,7 @@ class MixedStateBatch:
 
     def set_descriptors(self, scenes):
         """Upload a new per-step scene descriptor (poses, controller state, paths) of the same envs."""
-        if [config_key(s) for s in scenes] != [config_key(s) for s in self.scenes]:
+        if [mixed_key(s) for s in scenes] != [mixed_key(s) for s in self.scenes]:
             raise ValueError('set_descriptors: the envs and their configurations are fixed at construction')
         robots, envs, ag, paths = pack_descriptors(scenes, self.agents)
         self.scenes = scenes

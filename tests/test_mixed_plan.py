@@ -52,11 +52,18 @@ def test_plan_limits():
     assert len(batch.plan_mixed(_scenes([(c, e) for e, c in enumerate(cfgs[:8])]))['cfgs']) == _lib.MAX_MIXED
     with pytest.raises(ValueError, match='at most 8 configurations'):
         batch.plan_mixed(_scenes([(c, e) for e, c in enumerate(cfgs)]))
+    # with intention channels, each robot count is its own table entry (its own channel count)
     a = synthetic.make_scene('lifting_4-large_empty-nonspatial', 0)
     b = synthetic.make_scene('lifting_4-large_empty-nonspatial', 1)
     b = dict(b, robots=b['robots'][:3], occupancy=b['occupancy'][:3], overhead=b['overhead'][:3])
-    with pytest.raises(ValueError, match='same robot count'):
-        batch.plan_mixed([a, b])
+    p = batch.plan_mixed([a, b, a])
+    assert p['cfg_of_env'] == [0, 1, 0] and p['num_robots'] == [4, 3]
+    assert p['channels'][0] == p['channels'][1] + 2  # nonspatial: 2 channels per other robot
+    # without them, robot counts share an entry
+    c = synthetic.make_scene('lifting_4-small_divider', 0)
+    d = synthetic.make_scene('lifting_4-small_divider', 1)
+    d = dict(d, robots=d['robots'][:2], occupancy=d['occupancy'][:2], overhead=d['overhead'][:2])
+    assert batch.plan_mixed([c, d])['cfg_of_env'] == [0, 0]
 
 
 def test_mixed_needs_a_gpu_device():

@@ -87,7 +87,7 @@ def main_mixed(envs, procs, perturb):
     launches, cur, keys = [], [], set()
     for cfg, e, r in jobs:
         s = perturbed_scene(cfg, e, perturb, r)
-        k = batch.config_key(s)
+        k = batch.mixed_key(s)
         if k not in keys and len(keys) == _lib.MAX_MIXED:
             launches.append(cur)
             cur, keys = [], set()
