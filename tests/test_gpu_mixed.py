@@ -207,3 +207,27 @@ def test_mixed_set_maps(S):
         mb.set_maps(occupancy=[small], slots=[0])
     with pytest.raises(ValueError, match='one map per slot'):
         mb.set_maps(occupancy=[small, small], slots=[0])
+
+
+@pytest.mark.parametrize('cfg', ['lifting_4-large_empty-nonspatial', 'lifting_4-small_divider-spatial'])
+def test_mixed_intention_channels_ragged_robot_counts(S, cfg):
+    """Intention channels with 4-, 3- and 2-robot envs of one configuration: one table entry per
+    robot count (their channel counts differ), one launch, each agent as its own StateBatch and the
+    oracle render it."""
+    _lib, batch, synthetic = S
+
+    def trimmed(e, n):
+        s = synthetic.make_scene(cfg, 1300 + e)
+        return dict(s, robots=s['robots'][:n], occupancy=s['occupancy'][:n], overhead=s['overhead'][:n])
+    scenes = [trimmed(0, 4), trimmed(1, 3), trimmed(2, 2), trimmed(3, 3), trimmed(4, 4)]
+    mb = batch.MixedStateBatch(scenes, layout='hwc')
+    assert len(mb.plan['cfgs']) == 3
+    got = [v.cpu().numpy() for v in mb.states(mb.render())]
+    _lib.check_faults()
+    for n, (e, a) in enumerate(mb.agents):
+        _check_state(got[n], O.agent_state(scenes[e], a), scenes[e]['flags'], len(scenes[e]['robots']))
+    for e in range(len(scenes)):
+        ref = batch.StateBatch([scenes[e]], layout='hwc').render().cpu().numpy()
+        for n, (e2, a) in enumerate(mb.agents):
+            if e2 == e:
+                assert _bitwise(got[n], ref[a]), (e, a)
