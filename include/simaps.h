@@ -209,8 +209,9 @@ int simaps_robot_mask(int type, int with_cube, float *out);
  *   agents[n].map_slot (M = number of map slots, any N <= M of them rendered per call);
  *   state: [N, 96, 96, C] (or [N, C, 96, 96] if cfg->layout_chw) float32, DEVICE, C =
  *   simaps_num_channels(cfg, num_robots) -- every env of one call must have the same robot count
- *   when intention channels are on.  `num_robots_per_env` is that count (or 0 if unused).
- *   dbg may be NULL. */
+ *   when intention channels are on.  `num_robots_per_env` is that count (or 0 if unused); an env
+ *   with another count is clamped to it and reported (SIMAPS_FAULT_DESCRIPTOR), never written past
+ *   its agents' stacks.  dbg may be NULL. */
 int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
                      const simaps_robot *robots, const double *paths, const uint8_t *occupancy,
                      const float *overhead, float *state, int num_robots_per_env, const simaps_debug *dbg,
@@ -227,8 +228,12 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
  *   out_off   [N] int64   float offset of agent n's stack in state (96 * 96 * C of its configuration,
  *                         in its configuration's layout)
  * agents / envs / robots / paths as for simaps_get_state (one combined descriptor for all envs).
- * Bit-identical to one simaps_get_state launch per configuration.  No debug outputs or receptacle cache.
- * SIMAPS_EINVAL for n_cfgs outside [1, SIMAPS_MAX_MIXED] or a bad configuration. */
+ * With intention channels, num_robots_per_env[k] is the robot count of every env of entry k (two
+ * robot counts of one configuration are two entries).  Bit-identical to one simaps_get_state launch
+ * per configuration.  No debug outputs or receptacle cache.  The offsets are the caller's: they are
+ * not range-checked on the device (an agent_cfg outside [0, n_cfgs) is clamped to 0 and reported,
+ * SIMAPS_FAULT_DESCRIPTOR).  SIMAPS_EINVAL for n_cfgs outside [1, SIMAPS_MAX_MIXED] or a bad
+ * configuration. */
 #define SIMAPS_MAX_MIXED 8
 int simaps_get_state_mixed(const simaps_config *cfgs, const int32_t *num_robots_per_env, int n_cfgs, int N,
                            const simaps_agent *agents, const int32_t *agent_cfg, const simaps_env *envs,
