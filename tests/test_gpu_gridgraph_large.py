@@ -142,3 +142,25 @@ def test_gridgraph_large_refuses_graph_capture(M):
         finally:
             g.capture_end()
     assert rc == _lib.EUNSUPPORTED and b'captured' in _lib.lib.simaps_last_error()
+
+
+@pytest.mark.parametrize('w', [4, 6, 9])
+def test_gridgraph_large_narrow_windows(M, w):
+    """Tall windows of 4, 6 and 9 columns (pitch 6, 8, 11: below, at and above the pipelined pop's
+    P >= 8, whose neighbour forwarding needs unambiguous cell offsets): paths equal the oracle's."""
+    batch, vector_env = M
+    rs = np.random.RandomState(40 + w)
+    grid = (rs.random_sample((2000, w)) > 0.2).astype(np.uint8)
+    gg = vector_env.GridGraph(grid)
+    assert gg.large
+    free = np.argwhere(grid != 0)
+    src = tuple(int(x) for x in free[rs.randint(len(free))])
+    assert _bitwise(gg.shortest_path_image(src), O.spfa_image(grid, src))
+    tgts = [tuple(int(x) for x in free[rs.randint(len(free))]) for _ in range(8)]
+    n_tie = 0
+    for t, p in zip(tgts, gg.shortest_paths([(src, t) for t in tgts])):
+        want = O.grid_shortest_path(grid, src, t)
+        if not np.array_equal(np.array(p, dtype=np.int64).reshape(-1, 2), np.array(want, dtype=np.int64).reshape(-1, 2)):
+            assert _dp_tie(grid, src, t), (w, src, t)
+            n_tie += 1
+    assert n_tie <= 1
