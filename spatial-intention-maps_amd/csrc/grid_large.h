@@ -302,12 +302,19 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
     uint64_t pw_imp = 0;                    //   improved edges
     int pw_pvu = 0;                         //   the popped vertex's new pin
     long pw_q4 = -1;                        //   a push into the next pop's third slot: its content
+#ifdef SIMAPS_GL_PIPE_STATS
+    long n_fast = 0, n_slow = 0;
+    const long t_start = __builtin_readcyclecounter();
+#endif
     while (cnt > 0) {
         const long q2 = qh + 1 == QR ? 0 : qh + 1, q3 = q2 + 1 == QR ? 0 : q2 + 1, q4 = q3 + 1 == QR ? 0 : q3 + 1;
         const long v = u + off;
         float dv, dfr;
         int pv;
         long third;
+#ifdef SIMAPS_GL_PIPE_STATS
+        if (pf_u == u && (cnt < 2 || pf_s2 == s2)) n_fast++; else n_slow++;
+#endif
         if (pf_u == u && (cnt < 2 || pf_s2 == s2)) {
             // the pending reads are this pop's: patch them with the last pop's writes
             dv = pdv;
@@ -421,7 +428,13 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
         lim = pops + gap;
         gap = gap < (1 << 20) ? 2 * gap : gap;
     }
+#ifdef SIMAPS_GL_PIPE_STATS
+    if (lane == 0) printf("glpipe pops %ld fast %ld slow %ld cycles %ld\n", pops, n_fast, n_slow, (long)__builtin_readcyclecounter() - t_start);
+#endif
 #else
+#ifdef SIMAPS_GL_PIPE_STATS
+    const long t_start = __builtin_readcyclecounter();
+#endif
     while (cnt > 0) {
         // (2) pop u; its edges in pyx order on lanes 0-7 (pyx:89-101), lane 8 u itself
         const long q2 = qh + 1 == QR ? 0 : qh + 1, q3 = q2 + 1 == QR ? 0 : q2 + 1;
@@ -493,6 +506,9 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
         lim = pops + gap;
         gap = gap < (1 << 20) ? 2 * gap : gap;
     }
+#ifdef SIMAPS_GL_PIPE_STATS
+    if (lane == 0) printf("glser pops %ld cycles %ld\n", pops, (long)__builtin_readcyclecounter() - t_start);
+#endif
 #endif
     (void)early;
     // (5) dense path: parents from the target back to the source (pyx:131-138)
