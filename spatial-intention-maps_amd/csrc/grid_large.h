@@ -189,31 +189,12 @@ __global__ void __launch_bounds__(GL_NT) gl_sssp_kernel(int H, int W, const uint
 
 // Per-query scratch of gl_path_kernel, in int32 / float32 units of `cells` (padded cells) and `n`
 // (window cells + 1): fix [cells] (gl_sssp_kernel's fixpoint), dist [cells], pin [cells], queue [n]
-// (ring: live entries <= free cells), dense [n], chain [n], stack [2 n], and 64 per-lane dummy
-// words (the pipelined pop's stores of lanes with nothing to write).
+// (ring: live entries <= free cells), dense [n], chain [n], stack [2 n].
 __host__ __device__ inline long gl_path_words(int wh, int ww)
 {
     const long cells = (long)(wh + 2) * (ww + 2), n = (long)wh * ww + 1;
-    return 3 * cells + 5 * n + 64;
+    return 3 * cells + 5 * n;
 }
-
-#ifndef SIMAPS_GL_PIPE
-#define SIMAPS_GL_PIPE 1  // gl_path_kernel: the pipelined pop (0: one read round + a store drain per pop)
-#endif
-
-// d = Di * P + Dj with Di, Dj in [-2, 2] (unique for P >= 5): true and (Di, Dj) if d has that form
-__device__ __forceinline__ bool gl_rel(long d, int P, int &Di, int &Dj)
-{
-    const long e = d + 2L * P + 2;
-    if (e < 0 || e > 4L * P + 4) return false;
-    const int q = (e >= P) + (e >= 2L * P) + (e >= 3L * P) + (e >= 4L * P);
-    const int r = (int)(e - (long)q * P);
-    Di = q - 2;
-    Dj = r - 2;
-    return r <= 4;
-}
-// the pyx:30 direction k (8: the vertex itself) of the cell offset (di, dj) in [-1, 1]^2
-__device__ __forceinline__ int gl_dir_of(int di, int dj) { return (int)((0x765180432ull >> (4 * ((di + 1) * 3 + dj + 1))) & 15); }
 
 // pyx:30 directions: 1 + k in pin bits 0-3; the edge's cell offset in the padded layout
 __device__ __forceinline__ long gl_dir_off(int k, int pitch)
@@ -279,160 +260,7 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
     long qh = 0, qt = 0, cnt = 1, u = su, s2 = -1;
     long pops = 0, lim = finT != INFINITY ? 32 : SIMAPS_POP_CAP, gap = 64;
     bool early = false;
-#if SIMAPS_GL_PIPE
-    // Pipelined pops.  The serial pop waited for its own reads and then for its stores (a load issued
-    // after a store waits for it: the vector memory counter retires in order) -- two L2 round trips per
-    // pop.  Here each pop first issues the NEXT pop's reads, for the front it will have in the common
-    // case (the current second: no SLF swap, queue not emptied), and only then its own stores, so the
-    // reads are in flight during this pop and do not wait for its stores.  The next pop patches what
-    // its reads missed from this pop's writes, which it knows: the improved edge heads (distance,
-    // pin), the popped vertex's pin, and a push into the slot it reads its third entry from.  A pop
-    // whose front or second is not the one read for (an SLF swap, a front or second from a push)
-    // reads again.  Every pop issues the same memory instructions (lanes with nothing to read or write
-    // use a per-lane dummy word), so the reads' wait counts the stores after them exactly.
-    int *dummy = stack + 2 * n1;
-    const bool pipe = P >= 8;  // (gl_rel needs P >= 5; narrow windows keep the read-again path)
-    const int oi = lane < 2 ? 0 : (lane < 5 ? -1 : (lane < 8 ? 1 : 0));
-    const int oj = lane < 2 ? (lane == 0 ? -1 : 1) : (lane < 8 ? ((lane - 2) % 3) - 1 : 0);
-    long pf_u = -1, pf_s2 = -1;            // the front / second the pending reads were issued for
-    float pdv = 0.0f, pdfr = 0.0f;          // their results: edge-head distances, the second's distance
-    int ppv = 0, pthird = -1;               //   edge-head pins, the entry after the second
-    long pw_u = -1;                         // the last pop's vertex (-1: none), its writes:
-    float pw_nd = 0.0f;                     //   candidate distances (lanes 0-7)
-    uint64_t pw_imp = 0;                    //   improved edges
-    int pw_pvu = 0;                         //   the popped vertex's new pin
-    long pw_q4 = -1;                        //   a push into the next pop's third slot: its content
-#ifdef SIMAPS_GL_PIPE_STATS
-    long n_fast = 0, n_slow = 0;
-    const long t_start = __builtin_readcyclecounter();
-#endif
-    while (cnt > 0) {
-        const long q2 = qh + 1 == QR ? 0 : qh + 1, q3 = q2 + 1 == QR ? 0 : q2 + 1, q4 = q3 + 1 == QR ? 0 : q3 + 1;
-        const long v = u + off;
-        float dv, dfr;
-        int pv;
-        long third;
-#ifdef SIMAPS_GL_PIPE_STATS
-        if (pf_u == u && (cnt < 2 || pf_s2 == s2)) n_fast++; else n_slow++;
-#endif
-        if (pf_u == u && (cnt < 2 || pf_s2 == s2)) {
-            // the pending reads are this pop's: patch them with the last pop's writes
-            dv = pdv;
-            pv = ppv;
-            dfr = pdfr;
-            third = pthird;
-            int Di, Dj;
-            if (pw_u >= 0 && gl_rel(u - pw_u, P, Di, Dj)) {
-                const int di = Di + oi, dj = Dj + oj;
-                const bool hit = lane <= 8 && di >= -1 && di <= 1 && dj >= -1 && dj <= 1;
-                const int k = hit ? gl_dir_of(di, dj) : 0;
-                const float fnd = __shfl(pw_nd, k);
-                if (hit && k == 8) pv = pw_pvu;
-                else if (hit && ((pw_imp >> k) & 1)) {
-                    dv = fnd;
-                    pv = GL_INQ | (k + 1);
-                }
-            }
-            if (cnt >= 2 && pw_u >= 0 && gl_rel(s2 - pw_u, P, Di, Dj) && Di >= -1 && Di <= 1 && Dj >= -1 && Dj <= 1) {
-                const int k = gl_dir_of(Di, Dj);
-                const float fnd = __shfl(pw_nd, k < 8 ? k : 0);
-                if (k < 8 && ((pw_imp >> k) & 1)) dfr = fnd;
-            }
-            if (pw_q4 >= 0) third = pw_q4;
-        } else {
-            dv = lane <= 8 ? dist[v] : 0.0f;
-            pv = lane <= 8 ? pin[v] : 0;
-            const int third_l = (lane == 9 && cnt >= 3) ? queue[q3] : -1;
-            const float dfr_l = (lane == 10 && cnt >= 2) ? dist[s2] : 0.0f;
-            third = __shfl(third_l, 9);
-            dfr = __shfl(dfr_l, 10);
-        }
-        const long fr = cnt >= 2 ? s2 : -1;  // the front after this pop (queue[head + 1])
-        qh = q2;
-        cnt--;
-        // the next pop's reads: front fr, second `third` (cnt >= 2 now), the entry after it (slot q4)
-        pf_u = pipe ? fr : -1;
-        pf_s2 = cnt >= 2 ? third : -1;
-        {
-            const long vn = pf_u + off;
-            pdv = (pf_u >= 0 && lane <= 8) ? dist[vn] : __int_as_float(dummy[lane]);
-            ppv = (pf_u >= 0 && lane <= 8) ? pin[vn] : dummy[lane];
-            pthird = queue[q4];
-            pdfr = pf_s2 >= 0 ? dist[pf_s2] : __int_as_float(dummy[0]);
-        }
-        const float du = __shfl(dv, 8);
-        const float nd = du + wl;
-        const bool imp = lane < 8 && nd < dv;
-        // (3) pushes in edge order with the SLF swap against the front (pyx:102-107), as the serial
-        // pop below; the slots and contents are gathered first (lane p: the p-th push, lane 9: the
-        // front slot after swaps) and stored with one instruction
-        uint64_t todo = __ballot(imp && ((pv & GL_INQ) == 0 || v == fr));
-        long f = fr, nsec = cnt >= 2 ? third : -1;
-        const long q2n = qh + 1 == QR ? 0 : qh + 1;
-        float df = dfr;
-        long qslot = -1, qval = 0, q4w = -1;
-        int np = 0;
-        while (todo) {
-            const int k = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const long vk = __shfl(v, k);
-            const float ndk = __shfl(nd, k);
-            if (__shfl(pv, k) & GL_INQ) {
-                if (vk == f) df = ndk;
-                continue;
-            }
-            qt = qt + 1 == QR ? 0 : qt + 1;
-            cnt++;
-            long content = vk;
-            if (cnt == 1) {
-                f = vk;
-                df = ndk;
-            } else if (ndk < df) {
-                if (lane == 9) { qslot = qh; qval = vk; }
-                content = f;
-                f = vk;
-                df = ndk;
-            }
-            if (lane == np) { qslot = qt; qval = content; }
-            np++;
-            if (qt == q2n) nsec = content;
-            if (qt == q4) q4w = content;
-        }
-        {   // this pop's stores: edge heads (distance, pin), the popped vertex's pin, the pushes
-            float *da = imp ? dist + v : reinterpret_cast<float *>(dummy + lane);
-            *da = nd;
-            int *pa = imp ? pin + v : (lane == 8 ? pin + u : dummy + lane);
-            *pa = lane == 8 ? (pv & 15) : (GL_INQ | (k8 + 1));
-            int *qa = qslot >= 0 ? queue + qslot : dummy + lane;
-            *qa = (int)qval;
-        }
-        pw_u = u;
-        pw_nd = nd;
-        pw_imp = __ballot(imp);
-        pw_pvu = __shfl(pv, 8) & 15;
-        pw_q4 = q4w;
-        u = f;
-        s2 = nsec;
-        if (++pops < lim) continue;
-        if (pops >= SIMAPS_POP_CAP) {
-            if (cnt > 0) fault_bits |= SIMAPS_FAULT_ROUNDS;
-            break;
-        }
-        bool ok = dist[tv] == finT;
-        for (long w = tv, steps = 0; ok && w != su; steps++) {
-            const int p = pin[w] & 15;
-            if (!p || dist[w] != fix[w] || steps > n1) { ok = false; break; }
-            w -= gl_dir_off(p - 1, P);
-        }
-        if (ok) { early = true; break; }
-        lim = pops + gap;
-        gap = gap < (1 << 20) ? 2 * gap : gap;
-    }
-#ifdef SIMAPS_GL_PIPE_STATS
-    if (lane == 0) printf("glpipe pops %ld fast %ld slow %ld cycles %ld\n", pops, n_fast, n_slow, (long)__builtin_readcyclecounter() - t_start);
-#endif
-#else
-#ifdef SIMAPS_GL_PIPE_STATS
+#ifdef SIMAPS_GL_STATS
     const long t_start = __builtin_readcyclecounter();
 #endif
     while (cnt > 0) {
@@ -506,9 +334,8 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
         lim = pops + gap;
         gap = gap < (1 << 20) ? 2 * gap : gap;
     }
-#ifdef SIMAPS_GL_PIPE_STATS
+#ifdef SIMAPS_GL_STATS  // (diagnostic build: tools/debug/gl_pipe_stats.py)
     if (lane == 0) printf("glser pops %ld cycles %ld\n", pops, (long)__builtin_readcyclecounter() - t_start);
-#endif
 #endif
     (void)early;
     // (5) dense path: parents from the target back to the source (pyx:131-138)

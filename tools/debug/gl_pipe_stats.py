@@ -1,6 +1,7 @@
 """Pops and cycles of one large-grid path (the gridgraph_large bench's B = 1 query) under a stats
-build of gl_path_kernel (-DSIMAPS_GL_PIPE_STATS: the kernel printfs pops, fast / slow pops of the
-pipelined pop, and s_memtime-style cycles).  Run with SIMAPS_LIB=<stats build>."""
+build of gl_path_kernel (-DSIMAPS_GL_STATS: the kernel printfs its pops and the cycles of its pop
+loop).  Run with SIMAPS_LIB=<stats build>.  (Round 5 also measured a pipelined pop this way, commit
+5a28ec7: profiles/r5m_gl_pop_stats.txt.)"""
 import os
 import sys
 
