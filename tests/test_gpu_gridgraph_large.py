@@ -146,8 +146,8 @@ def test_gridgraph_large_refuses_graph_capture(M):
 
 @pytest.mark.parametrize('w', [4, 6, 9])
 def test_gridgraph_large_narrow_windows(M, w):
-    """Tall windows of 4, 6 and 9 columns (pitch 6, 8, 11: below, at and above the pipelined pop's
-    P >= 8, whose neighbour forwarding needs unambiguous cell offsets): paths equal the oracle's."""
+    """Tall windows of 4, 6 and 9 columns (pitch 6, 8, 11; beyond the LDS window by their 2,000
+    rows): the image and the paths equal the oracle's."""
     batch, vector_env = M
     rs = np.random.RandomState(40 + w)
     grid = (rs.random_sample((2000, w)) > 0.2).astype(np.uint8)
