@@ -170,7 +170,54 @@ def hold(s, cur, *tensors):
                 t.record_stream(s)
 
 
-class StateBatch:
+class _ArrayUpload:
+    """The array fast path of the per-step robot state, shared by StateBatch and
+    MixedStateBatch: needs self.device, self.n_robots and self._type_group ([R, 2] int32 robot class
+    and group, all robots of all envs in order)."""
+
+    def set_descriptor_arrays(self, pose, target, idle, lifting, waypoints, wp_count, wp_index):
+        """Per-step robot state as arrays, all robots of all envs in order (R = robots in the batch;
+        shapes as descriptor_arrays() returns, [E, A, ...] accepted): packed into the C structs by
+        the native simaps_pack_robots (no per-robot Python), staged in pinned host memory and
+        uploaded with ONE asynchronous copy on the current stream.  Robot classes / groups, the envs
+        and the agent list are the batch's (fixed at construction); only poses, targets, flags and
+        paths change per step."""
+        R = self.n_robots
+        f64 = lambda a, *shape: np.ascontiguousarray(a, dtype=np.float64).reshape(*shape)  # noqa: E731
+        pose, target = f64(pose, R, 3), f64(target, R, 2)
+        wps = np.ascontiguousarray(waypoints, dtype=np.float64)
+        K = wps.shape[-2] if wps.ndim >= 2 else 0
+        wps = wps.reshape(R, K, 2)
+        flags = (np.asarray(idle, dtype=np.int32).reshape(R) | (np.asarray(lifting, dtype=np.int32).reshape(R) << 1))
+        cnt = np.ascontiguousarray(wp_count, dtype=np.int32).reshape(R)
+        idx = np.ascontiguousarray(wp_index, dtype=np.int32).reshape(R)
+        if getattr(self, '_stage', None) is None:
+            self._rob_bytes = -(-R * _lib.ROBOT_DTYPE.itemsize // 256) * 256
+            nb = self._rob_bytes + R * 2 * _lib.MAX_PATH * 16
+            # a ring of pinned staging buffers: one is rewritten only after its copy has completed
+            self._stage = [torch.empty(max(nb, 256), dtype=torch.uint8).pin_memory() for _ in range(3)]
+            self._stage_ev = [None] * 3
+            self._stage_k = 0
+        k = self._stage_k
+        self._stage_k = (k + 1) % len(self._stage)
+        if self._stage_ev[k] is not None:
+            self._stage_ev[k].synchronize()
+        host = self._stage[k]
+        hp = host.data_ptr()
+        _lib.check(_lib.lib.simaps_pack_robots(
+            R, pose.ctypes.data, target.ctypes.data, flags.ctypes.data, self._type_group.ctypes.data,
+            wps.ctypes.data if K else None, K, cnt.ctypes.data, idx.ctypes.data, hp, hp + self._rob_bytes))
+        dev = torch.empty(host.shape, dtype=torch.uint8, device=self.device)
+        dev.copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._stage_ev[k] = ev
+        self.robots_d = dev[:R * _lib.ROBOT_DTYPE.itemsize]
+        self.paths_d = dev[self._rob_bytes:]
+        self.pose_host = pose.copy()  # the poses packed above (the caller may update its array in place)
+
+
+class StateBatch(_ArrayUpload):
     """One configuration's batch of agent-state stacks, resident on `device`.
 
     layout='chw' (default, device-native: every channel plane is written with full cache lines and is
@@ -244,48 +291,6 @@ class StateBatch:
         self.robots_d, self.envs_d, self.agents_d, self.paths_d = (dev[o:o + p.nbytes] for o, p in zip(offs, parts))
         if not hasattr(self, '_subsets'):
             self._subsets = {}  # subset agent lists depend on self.agents only: kept across steps
-
-    # -- the array fast path ----------------------------------------------------
-    def set_descriptor_arrays(self, pose, target, idle, lifting, waypoints, wp_count, wp_index):
-        """Per-step robot state as arrays, all robots of all envs in order (R = robots in the batch;
-        shapes as descriptor_arrays() returns, [E, A, ...] accepted): packed into the C structs by
-        the native simaps_pack_robots (no per-robot Python), staged in pinned host memory and
-        uploaded with ONE asynchronous copy on the current stream.  Robot classes / groups, the envs
-        and the agent list are the batch's (fixed at construction); only poses, targets, flags and
-        paths change per step."""
-        R = self.n_robots
-        f64 = lambda a, *shape: np.ascontiguousarray(a, dtype=np.float64).reshape(*shape)  # noqa: E731
-        pose, target = f64(pose, R, 3), f64(target, R, 2)
-        wps = np.ascontiguousarray(waypoints, dtype=np.float64)
-        K = wps.shape[-2] if wps.ndim >= 2 else 0
-        wps = wps.reshape(R, K, 2)
-        flags = (np.asarray(idle, dtype=np.int32).reshape(R) | (np.asarray(lifting, dtype=np.int32).reshape(R) << 1))
-        cnt = np.ascontiguousarray(wp_count, dtype=np.int32).reshape(R)
-        idx = np.ascontiguousarray(wp_index, dtype=np.int32).reshape(R)
-        if getattr(self, '_stage', None) is None:
-            self._rob_bytes = -(-R * _lib.ROBOT_DTYPE.itemsize // 256) * 256
-            nb = self._rob_bytes + R * 2 * _lib.MAX_PATH * 16
-            # a ring of pinned staging buffers: one is rewritten only after its copy has completed
-            self._stage = [torch.empty(max(nb, 256), dtype=torch.uint8).pin_memory() for _ in range(3)]
-            self._stage_ev = [None] * 3
-            self._stage_k = 0
-        k = self._stage_k
-        self._stage_k = (k + 1) % len(self._stage)
-        if self._stage_ev[k] is not None:
-            self._stage_ev[k].synchronize()
-        host = self._stage[k]
-        hp = host.data_ptr()
-        _lib.check(_lib.lib.simaps_pack_robots(
-            R, pose.ctypes.data, target.ctypes.data, flags.ctypes.data, self._type_group.ctypes.data,
-            wps.ctypes.data if K else None, K, cnt.ctypes.data, idx.ctypes.data, hp, hp + self._rob_bytes))
-        dev = torch.empty(host.shape, dtype=torch.uint8, device=self.device)
-        dev.copy_(host, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        self._stage_ev[k] = ev
-        self.robots_d = dev[:R * _lib.ROBOT_DTYPE.itemsize]
-        self.paths_d = dev[self._rob_bytes:]
-        self.pose_host = pose.copy()  # the poses packed above (the caller may update its array in place)
 
     def set_maps(self, occupancy=None, overhead=None, slots=None):
         """Replace the per-agent global maps -- what Mapper.update / OccupancyMap.update produce each
@@ -759,7 +764,7 @@ def plan_mixed(scenes, layout='chw'):
             'out_numel': int(per.sum())}
 
 
-class MixedStateBatch:
+class MixedStateBatch(_ArrayUpload):
     """Envs of several configurations (grid, room, flags, rotate rounding, and with intention
     channels the robot count; at most _lib.MAX_MIXED) rendered in ONE launch (simaps_get_state_mixed) -- e.g. the envs of several reference workers,
     each of which runs one configuration (train_multiprocess.py:159-166).  Every agent of every scene
@@ -784,6 +789,9 @@ class MixedStateBatch:
         self.overhead = torch.from_numpy(ovh).to(self.device)
         self._cfgs = (_lib.Config * len(self.plan['cfgs']))(*self.plan['cfgs'])
         self._nrs = np.asarray(self.plan['num_robots'], dtype=np.int32)
+        self.n_robots = sum(len(s['robots']) for s in scenes)
+        self._type_group = np.array([(_lib.TYPE_IDS[r['type']], r['group_index']) for s in scenes for r in s['robots']],
+                                    dtype=np.int32).reshape(-1, 2)
         self.agent_cfg_d = torch.from_numpy(self.plan['agent_cfg']).to(self.device)
         self.map_off_d = torch.from_numpy(self.plan['map_off']).to(self.device)
         self.out_off_d = torch.from_numpy(self.plan['out_off']).to(self.device)

@@ -231,3 +231,19 @@ def test_mixed_intention_channels_ragged_robot_counts(S, cfg):
         for n, (e2, a) in enumerate(mb.agents):
             if e2 == e:
                 assert _bitwise(got[n], ref[a]), (e, a)
+
+
+def test_mixed_descriptor_arrays_match_scene_update(S):
+    """The array fast path (native simaps_pack_robots, one pinned upload) on a mixed batch renders
+    what set_descriptors of the same scenes renders."""
+    _lib, batch, synthetic = S
+    scenes = _mixed_scenes(synthetic, seed=1400)
+    moved = _mixed_scenes(synthetic, seed=1500)  # other poses, targets and paths of the same robots
+    mb = batch.MixedStateBatch(scenes)
+    mb.set_descriptor_arrays(**batch.descriptor_arrays(moved))
+    got = mb.render().cpu().numpy()
+    mb.set_descriptors([dict(s, robots=m['robots'], receptacle_position=s['receptacle_position'])
+                        for s, m in zip(scenes, moved)])
+    want = mb.render().cpu().numpy()
+    _lib.check_faults()
+    assert _bitwise(got, want)
