@@ -18,7 +18,7 @@ import numpy as np  # noqa: E402
 
 CASES = [('lifting_4-small_divider', 'forward'), ('pushing_4-large_empty', 'forward'), ('rescue_4-small_empty', 'forward'),
          ('lifting_4-large_doors', 'forward'), ('lifting_4-small_divider', 'overhead'), ('lifting_4-large_rooms', 'overhead')]
-SEED0 = 7000
+SEED0 = int(os.environ.get('SIMAPS_FUZZ_SEED0', '7000'))  # (inherited by the spawned oracle workers)
 
 
 def _oracle(job):

@@ -27,7 +27,7 @@ CONFIGS = ['lifting_1-small_empty', 'lifting_4-small_divider', 'pushing_4-large_
            'lifting_4-small_empty-circle', 'lifting_4-small_divider-spatial', 'lifting_4-large_empty-nonspatial',
            'lifting_2_pushing_2-large_empty-all', 'lifting_4-large_doors', 'lifting_4-large_tunnels',
            'lifting_4-large_rooms', 'lifting_2_throwing_2-large_doors', 'lifting_4-large_rooms-history']
-SEED0 = 5000
+SEED0 = int(os.environ.get('SIMAPS_FUZZ_SEED0', '5000'))  # (inherited by the spawned oracle workers)
 
 
 def perturbed_scene(cfg, e, perturb, rounding='fma'):
