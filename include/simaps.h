@@ -218,8 +218,9 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
                      void *stream);
 
 /* simaps_get_state over agents of up to SIMAPS_MAX_MIXED configurations in ONE launch (the
- * reference's multiprocess collector runs one configuration per worker, train_multiprocess.py:159-166;
- * several workers' envs then share a launch).  cfgs[n_cfgs] and num_robots_per_env[n_cfgs] are HOST
+ * reference's multiprocess collector runs all its workers on one configuration,
+ * train_multiprocess.py:159-166, 217-228; collectors of different configurations then share a
+ * launch).  cfgs[n_cfgs] and num_robots_per_env[n_cfgs] are HOST
  * arrays (copied into the launch); everything else is DEVICE:
  *   agent_cfg [N] int32   the configuration of agent n (index into cfgs)
  *   map_off   [M] int64   element offset of map slot m in occupancy / overhead (its maps are

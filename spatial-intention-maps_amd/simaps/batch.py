@@ -766,8 +766,9 @@ def plan_mixed(scenes, layout='chw'):
 
 class MixedStateBatch(_ArrayUpload):
     """Envs of several configurations (grid, room, flags, rotate rounding, and with intention
-    channels the robot count; at most _lib.MAX_MIXED) rendered in ONE launch (simaps_get_state_mixed) -- e.g. the envs of several reference workers,
-    each of which runs one configuration (train_multiprocess.py:159-166).  Every agent of every scene
+    channels the robot count; at most _lib.MAX_MIXED) rendered in ONE launch (simaps_get_state_mixed)
+    -- e.g. the envs of collectors of different configurations (the reference's collector runs all
+    its workers on one, train_multiprocess.py:159-166, 217-228).  Every agent of every scene
     is a map slot, in scene order.  render() returns one flat float32 tensor; states() gives each
     agent's (C, 96, 96) (layout 'chw') or (96, 96, C) ('hwc') view of it, C that of its own
     configuration.  The results equal one StateBatch.render per configuration, bit for bit."""
