@@ -227,10 +227,23 @@ def make_scene(config_name, env_idx, seed_base=1234, observe_all=False):
       overhead: f32 [A, H, W]  (per agent, Mapper.global_overhead_map_without_robots)
       obstacle_mask: bool [H, W] (ground truth, for the point cloud of the golden generator)
     """
-    cfg = CONFIGS[config_name]
+    return _scene(config_name, CONFIGS[config_name], config_flags(config_name), env_idx, seed_base, observe_all)
+
+
+def reference_config_scene(row, env_idx, seed_base=4321):
+    """A scene for one reference experiment config as tests/golden/reference_configs.json holds it
+    (config/**/*.yml: env_name, robot_config, the state-representation flags): the obstacle layout
+    of its env_name (the maze layouts' longer paths included), its robots, its flags."""
+    maze = row['env_name'] in ('large_doors', 'large_tunnels', 'large_rooms')
+    cfg = dict(env_name=row['env_name'], robot_config=row['robot_config'], long_paths=maze)
+    flags = dict(_BASE_FLAGS)
+    flags.update(row['flags'])
+    return _scene(row['config'], cfg, flags, env_idx, seed_base, False)
+
+
+def _scene(config_name, cfg, flags, env_idx, seed_base, observe_all):
     rs = np.random.RandomState(seed_base + env_idx)
     room_length, room_width, num_cubes = K.room_dims(cfg['env_name'])
-    flags = config_flags(config_name)
     H, W = K.padded_room_shape(room_width, room_length)
     is_rescue = any('rescue_robot' in g for g in cfg['robot_config'])
     receptacle = None if is_rescue else (room_length / 2 - K.RECEPTACLE_WIDTH / 2,
