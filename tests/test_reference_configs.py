@@ -27,3 +27,16 @@ def test_channel_count_matches_the_config(row):
         assert (cfg.H, cfg.W) == K.padded_room_shape(row['room_width'], row['room_length'])
         assert _lib.lib.simaps_num_channels(cfg, robots) == row['num_input_channels'], row['config']
         assert _lib.lib.simaps_rec_cache_bytes(cfg) > 0, _lib.lib.simaps_last_error()  # (the C ABI's config check)
+
+
+def test_every_config_has_a_scene():
+    """synthetic.reference_config_scene (the GPU test's inputs) builds for every config, with its
+    robots, its flags, and descriptors the C structs take."""
+    from simaps import synthetic
+    for k, row in enumerate(ROWS):
+        s = synthetic.reference_config_scene(row, k)
+        assert [r['type'] for r in s['robots']] == [t for g in row['robot_config'] for t, c in g.items() for _ in range(c)]
+        assert all(s['flags'][f] == v for f, v in row['flags'].items())
+        agents = [(0, a) for a in range(len(s['robots']))]
+        robots, envs, ag, paths = batch.pack_descriptors([s], agents)
+        assert len(robots) == len(s['robots']) and s['occupancy'].shape == (len(agents), s['H'], s['W'])
