@@ -230,7 +230,7 @@ def make_scene(config_name, env_idx, seed_base=1234, observe_all=False):
     return _scene(config_name, CONFIGS[config_name], config_flags(config_name), env_idx, seed_base, observe_all)
 
 
-def reference_config_scene(row, env_idx, seed_base=4321):
+def reference_config_scene(row, env_idx, seed_base=4321, observe_all=False):
     """A scene for one reference experiment config as tests/golden/reference_configs.json holds it
     (config/**/*.yml: env_name, robot_config, the state-representation flags): the obstacle layout
     of its env_name (the maze layouts' longer paths included), its robots, its flags."""
@@ -238,7 +238,7 @@ def reference_config_scene(row, env_idx, seed_base=4321):
     cfg = dict(env_name=row['env_name'], robot_config=row['robot_config'], long_paths=maze)
     flags = dict(_BASE_FLAGS)
     flags.update(row['flags'])
-    return _scene(row['config'], cfg, flags, env_idx, seed_base, False)
+    return _scene(row['config'], cfg, flags, env_idx, seed_base, observe_all)
 
 
 def _scene(config_name, cfg, flags, env_idx, seed_base, observe_all):
