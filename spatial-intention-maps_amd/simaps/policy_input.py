@@ -33,3 +33,23 @@ def group_batches(state):
         idx = [j for j, s in enumerate(g) if s is not None]
         out.append((idx, torch.cat([apply_transform(g[j]) for j in idx]) if idx else None))
     return out
+
+
+def without_intention_map(batch):
+    """DQNIntentionPolicy.step in training (policies.py:126-131): the ground-truth intention map,
+    the state's last channel, removed before the intention network runs -- s[:, :, :-1] on a
+    (96, 96, C) state; here a zero-copy view of an [n, C, 96, 96] batch (its first C - 1 planes)."""
+    if batch.dim() != 4:
+        raise ValueError('expected an [n, C, 96, 96] batch')
+    return batch[:, :-1]
+
+
+def with_predicted_intention(batch, intention):
+    """DQNIntentionPolicy.step_intention (policies.py:97-108): the intention network's sigmoid
+    output appended as the last channel -- np.concatenate((s, o[:, :, None]), axis=2) on a
+    (96, 96, C) state; here [n, C, 96, 96] + [n, 96, 96] (or [n, 1, 96, 96]) -> [n, C + 1, 96, 96]."""
+    if intention.dim() == 3:
+        intention = intention.unsqueeze(1)
+    if batch.dim() != 4 or intention.shape != (batch.shape[0], 1) + tuple(batch.shape[2:]):
+        raise ValueError('expected [n, C, H, W] states and [n, H, W] intention maps')
+    return torch.cat([batch, intention.to(batch.dtype)], 1)
