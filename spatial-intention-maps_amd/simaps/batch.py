@@ -263,8 +263,9 @@ class StateBatch(_ArrayUpload):
         # slots whose maps a captured ingest graph may change on any replay, unseen by the host
         # versions above: their cached records are never served (always a miss, full SSSP)
         self._replayed = np.zeros(self.N, dtype=bool)
-        # the last launch that wrote or read the cache: every next one on another stream waits for it
-        self._rec_ev = None
+        # the stream of the last launch that wrote or read the cache: a next one on another stream
+        # waits for it (_rec_wait)
+        self._rec_stream = None
 
     def set_descriptors(self, scenes):
         """Upload a new per-step scene descriptor (poses, controller state, paths)."""
@@ -418,22 +419,25 @@ class StateBatch(_ArrayUpload):
         """Order a launch on stream `s` that writes or reads the receptacle cache after the previous
         such launch (on whatever stream it ran): render() and the miss path write records, the lookup
         reads them, and the caller never sees the buffer to order these itself.  Chained: each user
-        waits for the one before, so all of them are ordered.  (Inside a graph capture the capture's
-        own stream order applies; an event recorded outside it cannot be waited on.)"""
-        if self._rec_ev is None:
+        waits for the one before, so all of them are ordered.  On the previous user's own stream the
+        stream order does it (no event); on another, an event recorded now on that stream (it covers
+        the previous user and whatever followed it there).  (Inside a graph capture the capture's own
+        stream order applies; an event recorded outside it cannot be waited on.)"""
+        prev = self._rec_stream
+        if prev is None or prev == s:
             return
         with torch.cuda.stream(s):
             if torch.cuda.is_current_stream_capturing():
                 return
-        s.wait_event(self._rec_ev)
-
-    def _rec_record(self, s):
-        with torch.cuda.stream(s):
+        with torch.cuda.stream(prev):
             if torch.cuda.is_current_stream_capturing():
                 return
         ev = torch.cuda.Event()
-        ev.record(s)
-        self._rec_ev = ev
+        ev.record(prev)
+        s.wait_event(ev)
+
+    def _rec_record(self, s):
+        self._rec_stream = s
 
     def enable_receptacle_cache(self):
         """Allocate the receptacle distance cache (one simaps_rec_cache_bytes record per map slot): from

@@ -324,7 +324,8 @@ def test_receptacle_cache_after_graph_replayed_ingest(V):
 
 def test_receptacle_cache_across_streams(V):
     """the receptacle cache is written by render() and the miss path and read by
-    the lookups; launches on different streams are ordered through the batch's cache event.  A render
+    the lookups; a launch on another stream than the last cache user's waits for an event recorded
+    on that stream (on the same stream, stream order suffices).  A render
     on a side stream followed at once by lookups on the current stream (and the other way round)
     equals the oracle."""
     synthetic, vector_env = V
@@ -337,7 +338,7 @@ def test_receptacle_cache_across_streams(V):
     side = torch.cuda.Stream()
     torch.cuda.synchronize()
     side_out = b.render(stream=side)
-    assert b._rec_ev is not None and (b._rec_ver == b._map_ver).all()
+    assert b._rec_stream == side and (b._rec_ver == b._map_ver).all()
     _rec_check(b, scenes, tgt, 'render on side, lookup on current')
     out = b.receptacle_distances(tgt, stream=side)   # lookups on the side stream ...
     b.render()                                       # ... then a render on the current one
