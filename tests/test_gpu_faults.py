@@ -6,7 +6,6 @@ waiting, the SSSP round cap, or a descriptor field clamped to this build's limit
 to the library's host-mapped fault word.  simaps_fault_status reads it after a sync, and the next
 compute call fails with SIMAPS_EDEVICE, with or without debug buffers.
 """
-import ctypes
 import os
 
 import numpy as np

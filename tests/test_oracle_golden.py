@@ -5,7 +5,6 @@ These tests pin the oracle; the GPU tests then check the HIP path against the or
 """
 import hashlib
 import os
-import math
 
 import numpy as np
 import pytest

@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'spatial-intention-maps_amd'))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-from simaps import _lib, batch, synthetic  # noqa: E402
+from simaps import batch, synthetic  # noqa: E402
 
 for kind in ('forward', 'overhead'):
     scenes = [synthetic.make_scene('lifting_4-small_divider', e) for e in range(16)]

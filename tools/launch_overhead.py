@@ -2,7 +2,6 @@
 bare simaps_get_state call with pre-built arguments, timed over back-to-back launches without a
 synchronize in between (the GPU queue absorbs them).  If a launch costs the host more than the
 kernel lasts (~31 us), the bench's timed region is host-bound.  Test infrastructure only."""
-import ctypes
 import json
 import os
 import sys
