@@ -599,9 +599,15 @@ class StateBatch(_ArrayUpload):
         self._epoch = 0
 
     def _wait_last_ingest(self, s):
-        ev = getattr(self, '_ingest_ev', None)
-        if ev is not None:
-            s.wait_event(ev)  # the key map may still be in use by a launch on another stream
+        """Before the key map is zeroed on stream `s`: the last eager ingest launch may still use it
+        on another stream -- wait for an event recorded now on that stream (on the same stream,
+        stream order suffices)."""
+        prev = getattr(self, '_ingest_stream', None)
+        if prev is None or prev == s:
+            return
+        ev = torch.cuda.Event()
+        ev.record(prev)
+        s.wait_event(ev)
 
     def launch_ingest(self, prep, stream=None):
         if prep['n'] == 0:
@@ -637,8 +643,7 @@ class StateBatch(_ArrayUpload):
             _lib.ptr(prep['depth']), _lib.ptr(prep['seg']), _lib.ptr(self.overhead), _lib.ptr(self.occupancy),
             _lib.ptr(self._keys), _lib.ptr(self._boxes), epoch, _lib.stream_handle(s)))
         if not capturing:
-            self._ingest_ev = torch.cuda.Event()
-            self._ingest_ev.record(s)
+            self._ingest_stream = s
         hold(s, cur, prep['ids'], prep['params'], prep['depth'], prep['seg'], prep['agents'], self.overhead,
              self.occupancy, self._keys, self._boxes)
 
