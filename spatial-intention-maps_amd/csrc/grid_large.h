@@ -324,7 +324,17 @@ __device__ bool gl_spfa_lds(GlTiles &L, float *dist, int *pin, int *queue, const
             if (L.tag[sl] >= 0 && L.dirty[sl]) gl_tile_store(L, sl, L.tag[sl], TPR, dist, pin, rows, P);
         gl_drain();
     };
+#ifdef SIMAPS_GL_STATS
+    long st_lookup = 0, st_second = 0, st_relax = 0, st_push = 0, st_check = 0, st_miss = 0;
+    const long st_t0 = __builtin_readcyclecounter();
+#define GL_ST(acc) do { const long t_ = __builtin_readcyclecounter(); acc += t_ - st_t; st_t = t_; } while (0)
+#else
+#define GL_ST(acc) do { } while (0)
+#endif
     while (lcnt > 0) {
+#ifdef SIMAPS_GL_STATS
+        long st_t = __builtin_readcyclecounter();
+#endif
         if (lcnt > GLT_QCAP - 9) {  // the ring could overflow in this pop: hand over to the memory loop
             flush();
             for (int k = lane; k < lcnt; k += 64) queue[k] = L.q[(lqh + k) & QM];
@@ -349,11 +359,15 @@ __device__ bool gl_spfa_lds(GlTiles &L, float *dist, int *pin, int *queue, const
             gl_tile_load(L, slot, tid, TPR, dist, pin, rows, P);
             if (lane == 0) { L.tag[slot] = tid; L.dirty[slot] = 0; L.repl[set] = (uint8_t)((w + 1) & 3); }
             if (lane <= 8 && (vr >> 4) == mtr && (vc >> 4) == mtc) sl = slot;
+#ifdef SIMAPS_GL_STATS
+            st_miss++;
+#endif
         }
         const int o = (vr & 15) * 16 + (vc & 15);
         const float dv = lane <= 8 ? L.dist[sl][o] : 0.0f;
         const int pv = lane <= 8 ? L.pin[sl][o] : 0;
         const int v = vr * P + vc;
+        GL_ST(st_lookup);
         // the second's distance and the entry after it (pyx:104-107's front, the next second)
         float dfr = 0.0f;
         int third = -1;
@@ -366,6 +380,7 @@ __device__ bool gl_spfa_lds(GlTiles &L, float *dist, int *pin, int *queue, const
         const int fr = lcnt >= 2 ? ls2 : -1;
         lqh = q2;
         lcnt--;
+        GL_ST(st_second);
         // (2) pop u: edges in pyx order on lanes 0-7 (pyx:89-101)
         const float du = __shfl(dv, 8);
         const float nd = du + wl;
@@ -379,6 +394,7 @@ __device__ bool gl_spfa_lds(GlTiles &L, float *dist, int *pin, int *queue, const
             L.pin[sl][o] = (uint8_t)(pv & 15);  // in_queue[u] = 0 (pyx:92)
             L.dirty[sl] = 1;
         }
+        GL_ST(st_relax);
         // (3) pushes in edge order with the SLF swap (pyx:102-107), as the memory loop
         uint64_t todo = __ballot(imp && ((pv & GL_INQ) == 0 || v == fr));
         int f = fr, nsec = lcnt >= 2 ? third : -1;
@@ -410,6 +426,7 @@ __device__ bool gl_spfa_lds(GlTiles &L, float *dist, int *pin, int *queue, const
         }
         lu = f;
         ls2 = nsec;
+        GL_ST(st_push);
         if (++pops < lim) continue;
         if (pops >= SIMAPS_POP_CAP) {
             if (lcnt > 0) fault_bits |= SIMAPS_FAULT_ROUNDS;
@@ -433,9 +450,16 @@ __device__ bool gl_spfa_lds(GlTiles &L, float *dist, int *pin, int *queue, const
             }
             if (ok) { early = true; break; }
         }
+        GL_ST(st_check);
         lim = pops + gap;
         gap = gap < (1 << 20) ? 2 * gap : gap;
     }
+#ifdef SIMAPS_GL_STATS
+    if (lane == 0)
+        printf("gllds pops %ld misses %ld cycles %ld lookup %ld second %ld relax %ld push %ld check %ld\n", pops, st_miss,
+               (long)__builtin_readcyclecounter() - st_t0, st_lookup, st_second, st_relax, st_push, st_check);
+#endif
+#undef GL_ST
     flush();
     cnt = 0;
     return true;
