@@ -274,8 +274,15 @@ __device__ __forceinline__ void gl_tile_store(const GlTiles &L, int slot, int ti
 __device__ __forceinline__ int gl_tile_find(const GlTiles &L, int tr, int tc, int TPR)
 {
     const int set = gl_tile_set(tr, tc), tid = tr * TPR + tc;
-    const int4 t = *reinterpret_cast<const int4 *>(&L.tag[set * 4]);
-    return t.x == tid ? set * 4 : t.y == tid ? set * 4 + 1 : t.z == tid ? set * 4 + 2 : t.w == tid ? set * 4 + 3 : -1;
+    // the set's 4 tags in one 16-byte LDS read, compared with selects (a ?: chain became a branch
+    // and a dependent LDS read per way)
+    int4 t = *reinterpret_cast<const int4 *>(&L.tag[set * 4]);
+    asm volatile("" : "+v"(t.x), "+v"(t.y), "+v"(t.z), "+v"(t.w));
+    int w = t.w == tid ? 3 : -1;
+    w = t.z == tid ? 2 : w;
+    w = t.y == tid ? 1 : w;
+    w = t.x == tid ? 0 : w;
+    return w < 0 ? -1 : set * 4 + w;
 }
 
 // one cell (row r, column c), read-only: from its tile if resident, else from memory (current)
