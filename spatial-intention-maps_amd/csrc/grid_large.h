@@ -205,7 +205,7 @@ __device__ __forceinline__ long gl_dir_off(int k, int pitch)
 }
 
 #ifndef SIMAPS_GL_LDS
-#define SIMAPS_GL_LDS 1  // gl_path_kernel: the SPFA's cells cached in LDS tiles (0: every access to memory)
+#define SIMAPS_GL_LDS 0  // gl_path_kernel: 1 caches the SPFA's cells in LDS tiles (A/B build; 0, the product: every access to memory)
 #endif
 
 // ---- the SPFA's cells in an LDS tile cache (round 5) ------------------------------------------
