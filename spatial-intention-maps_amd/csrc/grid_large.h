@@ -204,274 +204,6 @@ __device__ __forceinline__ long gl_dir_off(int k, int pitch)
     return (long)di * pitch + dj;
 }
 
-#ifndef SIMAPS_GL_LDS
-#define SIMAPS_GL_LDS 0  // gl_path_kernel: 1 caches the SPFA's cells in LDS tiles (A/B build; 0, the product: every access to memory)
-#endif
-
-// ---- the SPFA's cells in an LDS tile cache (round 5) ------------------------------------------
-// The serial pop of gl_path_kernel waits for a memory round trip per pop that its previous pop's
-// stores to the same cache lines gate (~1,500 cycles per pop).  The SPFA's
-// queue order walks a narrow frontier, so its cells are cached in LDS: 16 x 16-cell tiles (dist
-// f32 + pin byte), 96 slots in 24 sets of 4 ways, and the live queue in an LDS ring.  A set index
-// carries the tile row's and column's parity, so the <= 4 tiles of one pop's 3 x 3 neighbourhood
-// lie in 4 different sets: loading one never evicts another.  Resident tiles are authoritative;
-// a tile is written back when evicted (if written) and at the end, so memory holds every
-// non-resident cell's current value, and a read of a non-resident cell goes to memory directly.
-// Host model of the pop order of the bench's 500 x 500 path: ~1 % of pops load a tile.  A queue
-// longer than the ring hands the state over to the memory loop below (exact either way).
-#ifndef SIMAPS_GL_QCAP
-#define SIMAPS_GL_QCAP 4096  // (a diagnostic build sets it small, so that every test exercises the hand-over)
-#endif
-constexpr int GLT_SETS = 24, GLT_WAYS = 4, GLT_SLOTS = GLT_SETS * GLT_WAYS, GLT_QCAP = SIMAPS_GL_QCAP;
-static_assert((GLT_QCAP & (GLT_QCAP - 1)) == 0 && GLT_QCAP >= 16, "the ring is a power of two");
-struct GlTiles {
-    float dist[GLT_SLOTS][256];
-    uint8_t pin[GLT_SLOTS][256];
-    int tag[GLT_SLOTS];
-    uint8_t dirty[GLT_SLOTS];
-    uint8_t repl[GLT_SETS];
-    int q[GLT_QCAP];
-};
-
-__device__ __forceinline__ int gl_tile_set(int tr, int tc)
-{
-    return (((tr >> 1) * 7 + (tc >> 1)) % (GLT_SETS / 4)) * 4 + ((tr & 1) << 1) + (tc & 1);
-}
-
-// tile `tid` (row tr, column tc of TPR tiles per row) <-> slot: 64 lanes x 4 cells (a 16 x 16 tile:
-// lane l -> tile row l / 4, columns 4 (l % 4) .. + 3); cells outside the padded window are -inf, pin 0
-__device__ __forceinline__ void gl_tile_load(GlTiles &L, int slot, int tid, int TPR, const float *dist, const int *pin,
-                                             int rows, int P)
-{
-    const int lane = threadIdx.x & 63, tr = tid / TPR, tc = tid - tr * TPR;
-    const int r = tr * 16 + (lane >> 2), c0 = tc * 16 + (lane & 3) * 4;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int c = c0 + k;
-        const bool in = r < rows && c < P;
-        const long g = (long)r * P + c;
-        L.dist[slot][(lane >> 2) * 16 + (lane & 3) * 4 + k] = in ? dist[g] : -INFINITY;
-        L.pin[slot][(lane >> 2) * 16 + (lane & 3) * 4 + k] = in ? (uint8_t)pin[g] : (uint8_t)0;
-    }
-}
-__device__ __forceinline__ void gl_tile_store(const GlTiles &L, int slot, int tid, int TPR, float *dist, int *pin,
-                                              int rows, int P)
-{
-    const int lane = threadIdx.x & 63, tr = tid / TPR, tc = tid - tr * TPR;
-    const int r = tr * 16 + (lane >> 2), c0 = tc * 16 + (lane & 3) * 4;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int c = c0 + k;
-        if (r < rows && c < P) {
-            const long g = (long)r * P + c;
-            dist[g] = L.dist[slot][(lane >> 2) * 16 + (lane & 3) * 4 + k];
-            pin[g] = L.pin[slot][(lane >> 2) * 16 + (lane & 3) * 4 + k];
-        }
-    }
-}
-
-// the slot holding tile (tr, tc), or -1
-__device__ __forceinline__ int gl_tile_find(const GlTiles &L, int tr, int tc, int TPR)
-{
-    const int set = gl_tile_set(tr, tc), tid = tr * TPR + tc;
-    // the set's 4 tags in one 16-byte LDS read, compared with selects (a ?: chain became a branch
-    // and a dependent LDS read per way)
-    int4 t = *reinterpret_cast<const int4 *>(&L.tag[set * 4]);
-    asm volatile("" : "+v"(t.x), "+v"(t.y), "+v"(t.z), "+v"(t.w));
-    int w = t.w == tid ? 3 : -1;
-    w = t.z == tid ? 2 : w;
-    w = t.y == tid ? 1 : w;
-    w = t.x == tid ? 0 : w;
-    return w < 0 ? -1 : set * 4 + w;
-}
-
-// one cell (row r, column c), read-only: from its tile if resident, else from memory (current)
-__device__ __forceinline__ void gl_cell_read(const GlTiles &L, int r, int c, int TPR, int P, const float *dist,
-                                             const int *pin, float &d, int &p)
-{
-    const int sl = gl_tile_find(L, r >> 4, c >> 4, TPR);
-    if (sl >= 0) {
-        d = L.dist[sl][(r & 15) * 16 + (c & 15)];
-        p = L.pin[sl][(r & 15) * 16 + (c & 15)];
-    } else {
-        d = dist[(long)r * P + c];
-        p = pin[(long)r * P + c];
-    }
-}
-
-// The SPFA of gl_path_kernel (pyx:69-114, the same pop as the memory loop there) on the LDS tiles.
-// Returns true when it ran to its end (queue empty, early exit, or the pop cap); false when the
-// queue outgrew the ring: the tiles are written back, the live queue is copied to `queue` slots
-// 0 .. cnt - 1 and (qh, qt, cnt, u, s2) describe it for the memory loop.
-__device__ bool gl_spfa_lds(GlTiles &L, float *dist, int *pin, int *queue, const float *fix, int rows, int P,
-                            long su, long tv, float finT, long n1, long &qh, long &qt, long &cnt, long &u, long &s2,
-                            long &pops, long &lim, long &gap, bool &early, unsigned &fault_bits)
-{
-    const int lane = threadIdx.x & 63;
-    const int TPR = (P + 15) >> 4, TPC = (rows + 15) >> 4;
-    (void)TPC;
-    const int oi = lane < 2 ? 0 : (lane < 5 ? -1 : (lane < 8 ? 1 : 0));
-    const int oj = lane < 2 ? (lane == 0 ? -1 : 1) : (lane < 8 ? ((lane - 2) % 3) - 1 : 0);
-    const int k8 = lane < 8 ? lane : 8;
-    const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
-    const float invP = 1.0f / (float)P;
-    constexpr int QM = GLT_QCAP - 1;
-    for (int k = lane; k < GLT_SLOTS; k += 64) { L.tag[k] = -1; L.dirty[k] = 0; }
-    if (lane < GLT_SETS) L.repl[lane] = 0;
-    if (lane == 0) L.q[0] = (int)su;
-    int lqh = 0, lqt = 0;
-    int lcnt = 1, lu = (int)su, ls2 = -1;
-    auto rc_of = [&](int v, int &r, int &c) {
-        r = (int)((float)v * invP);
-        c = v - r * P;
-        if (c < 0) { r--; c += P; } else if (c >= P) { r++; c -= P; }
-    };
-    auto flush = [&]() {
-        for (int sl = 0; sl < GLT_SLOTS; sl++)
-            if (L.tag[sl] >= 0 && L.dirty[sl]) gl_tile_store(L, sl, L.tag[sl], TPR, dist, pin, rows, P);
-        gl_drain();
-    };
-#ifdef SIMAPS_GL_STATS
-    long st_lookup = 0, st_second = 0, st_relax = 0, st_push = 0, st_check = 0, st_miss = 0;
-    const long st_t0 = __builtin_readcyclecounter();
-#define GL_ST(acc) do { const long t_ = __builtin_readcyclecounter(); acc += t_ - st_t; st_t = t_; } while (0)
-#else
-#define GL_ST(acc) do { } while (0)
-#endif
-    while (lcnt > 0) {
-#ifdef SIMAPS_GL_STATS
-        long st_t = __builtin_readcyclecounter();
-#endif
-        if (lcnt > GLT_QCAP - 9) {  // the ring could overflow in this pop: hand over to the memory loop
-            flush();
-            for (int k = lane; k < lcnt; k += 64) queue[k] = L.q[(lqh + k) & QM];
-            gl_drain();
-            qh = 0; qt = lcnt - 1; cnt = lcnt; u = lu; s2 = ls2;
-            return false;
-        }
-        const int q2 = (lqh + 1) & QM, q3 = (q2 + 1) & QM;
-        int ur, uc;
-        rc_of(lu, ur, uc);
-        // (1) the 3 x 3 neighbourhood's tiles resident (lanes 0-8; lane 8: u itself)
-        const int vr = ur + oi, vc = uc + oj;
-        int sl = lane <= 8 ? gl_tile_find(L, vr >> 4, vc >> 4, TPR) : 0;
-        for (uint64_t mm = __ballot(lane <= 8 && sl < 0); mm; mm = __ballot(lane <= 8 && sl < 0)) {
-            const int l = __builtin_ctzll(mm);
-            const int mtr = __shfl(vr >> 4, l), mtc = __shfl(vc >> 4, l);
-            const int set = gl_tile_set(mtr, mtc), tid = mtr * TPR + mtc;
-            const int w = L.repl[set];
-            const int slot = set * 4 + w;
-            const int old = L.tag[slot];
-            if (old >= 0 && L.dirty[slot]) gl_tile_store(L, slot, old, TPR, dist, pin, rows, P);
-            gl_tile_load(L, slot, tid, TPR, dist, pin, rows, P);
-            if (lane == 0) { L.tag[slot] = tid; L.dirty[slot] = 0; L.repl[set] = (uint8_t)((w + 1) & 3); }
-            if (lane <= 8 && (vr >> 4) == mtr && (vc >> 4) == mtc) sl = slot;
-#ifdef SIMAPS_GL_STATS
-            st_miss++;
-#endif
-        }
-        const int o = (vr & 15) * 16 + (vc & 15);
-        const float dv = lane <= 8 ? L.dist[sl][o] : 0.0f;
-        const int pv = lane <= 8 ? L.pin[sl][o] : 0;
-        const int v = vr * P + vc;
-        GL_ST(st_lookup);
-        // the second's distance and the entry after it (pyx:104-107's front, the next second)
-        float dfr = 0.0f;
-        int third = -1;
-        if (lcnt >= 2) {
-            int r2, c2, p2;
-            rc_of(ls2, r2, c2);
-            gl_cell_read(L, r2, c2, TPR, P, dist, pin, dfr, p2);
-        }
-        if (lcnt >= 3) third = L.q[q3];
-        const int fr = lcnt >= 2 ? ls2 : -1;
-        lqh = q2;
-        lcnt--;
-        GL_ST(st_second);
-        // (2) pop u: edges in pyx order on lanes 0-7 (pyx:89-101)
-        const float du = __shfl(dv, 8);
-        const float nd = du + wl;
-        const bool imp = lane < 8 && nd < dv;
-        if (imp) {
-            L.dist[sl][o] = nd;
-            L.pin[sl][o] = (uint8_t)(GL_INQ | (k8 + 1));
-            L.dirty[sl] = 1;
-        }
-        if (lane == 8) {
-            L.pin[sl][o] = (uint8_t)(pv & 15);  // in_queue[u] = 0 (pyx:92)
-            L.dirty[sl] = 1;
-        }
-        GL_ST(st_relax);
-        // (3) pushes in edge order with the SLF swap (pyx:102-107), as the memory loop
-        uint64_t todo = __ballot(imp && ((pv & GL_INQ) == 0 || v == fr));
-        int f = fr, nsec = lcnt >= 2 ? third : -1;
-        const int q2n = (lqh + 1) & QM;
-        float df = dfr;
-        while (todo) {
-            const int k = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const int vk = __shfl(v, k);
-            const float ndk = __shfl(nd, k);
-            if (__shfl(pv, k) & GL_INQ) {
-                if (vk == f) df = ndk;
-                continue;
-            }
-            lqt = (lqt + 1) & QM;
-            lcnt++;
-            int content = vk;
-            if (lcnt == 1) {
-                f = vk;
-                df = ndk;
-            } else if (ndk < df) {
-                if (lane == 0) L.q[lqh] = vk;
-                content = f;
-                f = vk;
-                df = ndk;
-            }
-            if (lane == 0) L.q[lqt] = content;
-            if (lqt == q2n) nsec = content;
-        }
-        lu = f;
-        ls2 = nsec;
-        GL_ST(st_push);
-        if (++pops < lim) continue;
-        if (pops >= SIMAPS_POP_CAP) {
-            if (lcnt > 0) fault_bits |= SIMAPS_FAULT_ROUNDS;
-            break;
-        }
-        // (4) early exit (as the memory loop): the target at its fixpoint distance, then its chain
-        {
-            int tr_, tc_, tp;
-            float td;
-            rc_of((int)tv, tr_, tc_);
-            gl_cell_read(L, tr_, tc_, TPR, P, dist, pin, td, tp);
-            bool ok = td == finT;
-            for (long w = tv, steps = 0; ok && w != su; steps++) {
-                int wr, wc, p;
-                float dw;
-                rc_of((int)w, wr, wc);
-                gl_cell_read(L, wr, wc, TPR, P, dist, pin, dw, p);
-                p &= 15;
-                if (!p || dw != fix[w] || steps > n1) { ok = false; break; }
-                w -= gl_dir_off(p - 1, P);
-            }
-            if (ok) { early = true; break; }
-        }
-        GL_ST(st_check);
-        lim = pops + gap;
-        gap = gap < (1 << 20) ? 2 * gap : gap;
-    }
-#ifdef SIMAPS_GL_STATS
-    if (lane == 0)
-        printf("gllds pops %ld misses %ld cycles %ld lookup %ld second %ld relax %ld push %ld check %ld\n", pops, st_miss,
-               (long)__builtin_readcyclecounter() - st_t0, st_lookup, st_second, st_relax, st_push, st_check);
-#endif
-#undef GL_ST
-    flush();
-    cnt = 0;
-    return true;
-}
-
 // GridGraph(grid).shortest_path(source, target) (pyx:121-154) on windows of any size, one wave per
 // query, after gl_sssp_kernel left the fixpoint from the same source in `fix`.  Output as
 // grid_path_kernel: waypoint cells source first, count or -needed.
@@ -528,13 +260,6 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
     long qh = 0, qt = 0, cnt = 1, u = su, s2 = -1;
     long pops = 0, lim = finT != INFINITY ? 32 : SIMAPS_POP_CAP, gap = 64;
     bool early = false;
-#if SIMAPS_GL_LDS
-    if (g.cells < (1L << 24)) {  // (gl_spfa_lds maps cells to rows through a float reciprocal)
-        __shared__ GlTiles tiles;
-        gl_spfa_lds(tiles, dist, pin, queue, fix, wh + 2, P, su, tv, finT, n1, qh, qt, cnt, u, s2, pops, lim, gap,
-                    early, fault_bits);
-    }
-#endif
 #ifdef SIMAPS_GL_STATS
     const long t_start = __builtin_readcyclecounter();
 #endif
