@@ -88,11 +88,13 @@ def rank_envs(rank, envs_per_rank, world=1, total_envs=None):
 
 def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu', own=None):
     """The bench contract's timed region: `warmup` untimed steps, then barrier + sync, EXACTLY
-    `steps` steps, sync + barrier; returns the wall time, max-reduced over ranks (every rank gets
-    the job time).  step(k) runs step k (k < 0 for warmup); sync() waits for the device.  Each
-    rank's clock runs from the common start (after the opening barrier) to its own sync after its
-    K steps; the closing barrier follows, untimed -- an RCCL barrier costs ~0.1 ms, ~15 % of a
-    20-step region, and is no part of the K steps -- and the max over ranks is the job's time."""
+    `steps` steps, sync + barrier; returns the job's wall time (every rank gets it).  step(k) runs
+    step k (k < 0 for warmup); sync() waits for the device.  The job's time runs from the EARLIEST
+    rank's start (its exit from the opening barrier) to the LATEST rank's end (its sync after its K
+    steps): one max-reduction of (-start, end) over the ranks' CLOCK_MONOTONIC stamps
+    (time.perf_counter, one clock for every process of the node), so skew between ranks leaving the
+    opening barrier is counted.  The closing barrier itself is not: an RCCL barrier costs ~0.1 ms,
+    ~15 % of a 20-step region, and is no part of the K steps."""
     import torch
     import torch.distributed as dist
     coll = world > 1 or (dist.is_available() and dist.is_initialized())  # (--init-dist: one rank, real collectives)
@@ -106,12 +108,13 @@ def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu', own=None)
     for k in range(steps):
         step(k)
     sync()
-    elapsed = time.perf_counter() - t0
+    t1 = time.perf_counter()
     if coll:
         dist.barrier()
     if own is not None:
-        own.append(elapsed)  # this rank's own timed region (the rank report)
-    return max_over_ranks([elapsed], world, reduce_device)[0]
+        own.append(t1 - t0)  # this rank's own timed region (the rank report)
+    neg_start, end = max_over_ranks([-t0, t1], world, reduce_device)
+    return end + neg_start
 
 
 def max_over_ranks(values, world, device='cpu'):

@@ -58,8 +58,9 @@ extern "C" {
 #define SIMAPS_FAULT_DESCRIPTOR 4u /* a descriptor field outside this build's limits was clamped: num_robots
                                       > SIMAPS_MAX_ROBOTS, robot index >= num_robots, an env's num_robots
                                       other than num_robots_per_env with intention channels on, a used
-                                      intention / history path longer than SIMAPS_MAX_PATH points, or (mixed
-                                      launch) a configuration index >= n_cfgs */
+                                      intention / history path longer than SIMAPS_MAX_PATH points; or (mixed
+                                      launch) a configuration index outside [0, n_cfgs): reported, and
+                                      that agent's stack is left unwritten */
 
 /* robot classes (envs.py: LiftingRobot 1169, PushingRobot 1059, ThrowingRobot 1279, RescueRobot 1346) */
 #define SIMAPS_LIFTING 0
@@ -177,6 +178,11 @@ typedef struct simaps_debug {
 
 int simaps_abi_version(void);
 const char *simaps_last_error(void);
+/* sha256 (hex) of the sources this library was built from (the .hip / .h / .inc files of csrc/ and this header, as
+ * simaps/_srchash.py computes it; "unknown" if built without it).  No reference counterpart: the
+ * reference rebuilds its Cython extension from source (shortest_paths/setup.py:1-6); the Python
+ * binding refuses a library whose hash differs from the tree's, i.e. a stale binary. */
+const char *simaps_source_hash(void);
 
 /* The device-side fault word (SIMAPS_FAULT_* bits) as of the launches that have completed: call
  * after synchronising the stream to cover a given launch.  clear != 0 resets it.  Returns the bits
@@ -232,8 +238,8 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
  * With intention channels, num_robots_per_env[k] is the robot count of every env of entry k (two
  * robot counts of one configuration are two entries).  Bit-identical to one simaps_get_state launch
  * per configuration.  No debug outputs or receptacle cache.  The offsets are the caller's: they are
- * not range-checked on the device (an agent_cfg outside [0, n_cfgs) is clamped to 0 and reported,
- * SIMAPS_FAULT_DESCRIPTOR).  SIMAPS_EINVAL for n_cfgs outside [1, SIMAPS_MAX_MIXED] or a bad
+ * not range-checked on the device (an agent_cfg outside [0, n_cfgs) is reported,
+ * SIMAPS_FAULT_DESCRIPTOR, and that agent's stack is not written).  SIMAPS_EINVAL for n_cfgs outside [1, SIMAPS_MAX_MIXED] or a bad
  * configuration. */
 #define SIMAPS_MAX_MIXED 8
 int simaps_get_state_mixed(const simaps_config *cfgs, const int32_t *num_robots_per_env, int n_cfgs, int N,

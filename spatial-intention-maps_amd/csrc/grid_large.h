@@ -206,12 +206,13 @@ __device__ __forceinline__ long gl_dir_off(int k, int pitch)
 
 // GridGraph(grid).shortest_path(source, target) (pyx:121-154) on windows of any size, one wave per
 // query, after gl_sssp_kernel left the fixpoint from the same source in `fix`.  Output as
-// grid_path_kernel: waypoint cells source first, count or -needed.
+// grid_path_kernel: waypoint cells source first, count or -needed.  fixp 1 / 2 (simaps_path_mode 4 /
+// 5, opt-in): no SPFA; the chain is walked on the fixpoint with path_core's FIXP rule.
 __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t *__restrict__ grids, long grid_stride,
                                                     const int32_t *__restrict__ sources, const int32_t *__restrict__ targets,
                                                     int wi0, int wj0, int wh, int ww, int *scratch, long scratch_stride,
                                                     int max_pts, int32_t *__restrict__ out_ij, int32_t *__restrict__ out_n,
-                                                    unsigned *fault)
+                                                    int fixp, unsigned *fault)
 {
     const int b = blockIdx.x, lane = threadIdx.x;
     const uint8_t *grid = grids + b * grid_stride;
@@ -249,7 +250,10 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
     if (lane == 0) queue[0] = (int)su;
     gl_drain();
     unsigned fault_bits = 0;
-    const float finT = fix[tv];  // the target's fixpoint distance (+inf: unreachable, no early exit)
+    const float finT = fix[tv];  // the target's fixpoint distance
+    // The pop cap (a bug guard: a correct SPFA never reaches it) scales with the window: the
+    // reference's linear queue holds 8 V entries (pyx:78), so its SPFA never pops more than that.
+    const long pop_cap = SIMAPS_POP_CAP > 8L * wh * ww + 1 ? (long)SIMAPS_POP_CAP : 8L * wh * ww + 1;
     const int k8 = lane < 8 ? lane : 8;
     const long off = lane < 8 ? gl_dir_off(lane, P) : 0;  // lane 8: the popped vertex itself
     const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
@@ -258,8 +262,11 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
     // out together in one round
     const long QR = n1;
     long qh = 0, qt = 0, cnt = 1, u = su, s2 = -1;
-    long pops = 0, lim = finT != INFINITY ? 32 : SIMAPS_POP_CAP, gap = 64;
+    long pops = 0, lim = 32, gap = 64;
     bool early = false;
+    // an unreachable (+inf) or blocked (-inf) target never gets a parent (pin[tv] stays 0 unless it is
+    // the source): the path is [target] whatever the SPFA does, so it is not run
+    if (!(finT > -INFINITY && finT < INFINITY) || fixp) cnt = 0;
 #ifdef SIMAPS_GL_STATS
     const long t_start = __builtin_readcyclecounter();
 #endif
@@ -319,7 +326,7 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
         s2 = nsec;
         gl_drain();  // (a timing variant without this wait was only 4 % faster: profiles/r5h_*)
         if (++pops < lim) continue;
-        if (pops >= SIMAPS_POP_CAP) {
+        if (pops >= pop_cap) {
             if (cnt > 0) fault_bits |= SIMAPS_FAULT_ROUNDS;  // the cap stopped a live queue
             break;
         }
@@ -333,6 +340,7 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
         if (ok) { early = true; break; }
         lim = pops + gap;
         gap = gap < (1 << 20) ? 2 * gap : gap;
+        lim = lim < pop_cap ? lim : pop_cap;
     }
 #ifdef SIMAPS_GL_STATS  // (diagnostic build: tools/debug/gl_pipe_stats.py)
     if (lane == 0) printf("glser pops %ld cycles %ld\n", pops, (long)__builtin_readcyclecounter() - t_start);
@@ -340,7 +348,30 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
     (void)early;
     // (5) dense path: parents from the target back to the source (pyx:131-138)
     int nd = 0;
-    if (lane == 0) {
+    if (fixp) {  // path_core's FIXP walk on the fixpoint (lanes 0..7: the neighbours of the chain's head)
+        const float wl8 = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
+        long w = tv;
+        float dw = finT;
+        if (lane == 0) dense[0] = (int)w;
+        nd = 1;
+        if (finT > -INFINITY && finT < INFINITY)
+            while (w != su && nd < n1) {
+                const float du = lane < 8 ? fix[w - off] : INFINITY;
+                const bool ok = lane < 8 && du + wl8 == dw;
+                uint64_t m = __ballot(ok);
+                if (!m) break;
+                if (fixp == 1) {
+                    float key = ok ? du : INFINITY;
+                    for (int o2 = 4; o2 > 0; o2 >>= 1) key = fminf(key, __shfl_xor(key, o2));
+                    m = __ballot(ok && du == __shfl(key, 0));
+                }
+                const int k = __builtin_ctzll(m);
+                w -= __shfl((int)off, k);
+                dw = __shfl(du, k);
+                if (lane == 0) dense[nd] = (int)w;
+                nd++;
+            }
+    } else if (lane == 0) {
         long w = tv;
         dense[nd++] = (int)w;
         while (w != su) {

@@ -13,10 +13,12 @@ __global__ void __launch_bounds__(NT) get_state_mixed_kernel(
     const double *__restrict__ paths, const uint8_t *__restrict__ occupancy, const int64_t *__restrict__ map_off,
     const float *__restrict__ overhead, float *__restrict__ state, const int64_t *__restrict__ out_off, unsigned *fault)
 {
-    int k = __builtin_amdgcn_readfirstlane(agent_cfg[blockIdx.x]);
-    if ((unsigned)k >= (unsigned)mx.n) {  // a configuration index past the table: clamped, reported
+    const int k = __builtin_amdgcn_readfirstlane(agent_cfg[blockIdx.x]);
+    if ((unsigned)k >= (unsigned)mx.n) {
+        // a configuration index past the table: reported, and the workgroup writes nothing (any
+        // configuration's C channels at out_off[n] could run past the agent's own stack)
         if (threadIdx.x == 0) post_faults(fault, SIMAPS_FAULT_DESCRIPTOR);
-        k = 0;
+        return;
     }
     const simaps_config cfg = mx.cfg[k];
     const int C = mx.C[k];

@@ -64,6 +64,29 @@ class SimapsError(RuntimeError):
     pass
 
 
+class StaleLibraryError(ImportError):
+    """libsimaps.so was built from sources other than the tree's (simaps_source_hash)."""
+
+
+def _check_source_hash(L, path):
+    """Refuse a library built from other sources than this tree's csrc/ + include/ (a stale .so left
+    over from before a kernel edit would otherwise run silently, on the GPU box too).  An A/B
+    timing of another revision's build names the hash it expects in SIMAPS_AB_SOURCE_HASH."""
+    from . import _srchash
+    if not hasattr(L, 'simaps_source_hash'):
+        if os.environ.get('SIMAPS_AB_OLD_ABI'):  # (an older revision's A/B build predates the export)
+            return
+        raise StaleLibraryError('%s has no simaps_source_hash: built before the stale-binary guard; rebuild it with '
+                                '`make -C spatial-intention-maps_amd/csrc`' % path)
+    L.simaps_source_hash.restype = ctypes.c_char_p
+    built = L.simaps_source_hash().decode()
+    want = os.environ.get('SIMAPS_AB_SOURCE_HASH') or _srchash.source_hash()
+    if built != want:
+        raise StaleLibraryError('%s was built from other sources (hash %s) than this tree\'s (%s): a stale binary -- '
+                                'rebuild it with `make -C spatial-intention-maps_amd/csrc` (and `... diag` for the '
+                                'diagnostic builds)' % (path, built[:16], want[:16]))
+
+
 def _load(path=LIB_PATH):
     """Bind the C ABI of the library at `path` (the product libsimaps.so by default; tests also load
     diagnostic builds of the same ABI through this)."""
@@ -73,6 +96,7 @@ def _load(path=LIB_PATH):
     L = ctypes.CDLL(path)
     vp, i32 = ctypes.c_void_p, ctypes.c_int
     L.simaps_abi_version.restype = i32
+    _check_source_hash(L, path)
     L.simaps_last_error.restype = ctypes.c_char_p
     L.simaps_num_channels.argtypes = [ctypes.POINTER(Config), i32]
     L.simaps_num_channels.restype = i32
@@ -139,7 +163,7 @@ lib = _load()
 EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_fault_status', 'simaps_num_channels',
             'simaps_robot_mask', 'simaps_pack_robots', 'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest', 'simaps_ingest_chunks', 'simaps_path_mode',
             'simaps_sssp_grid', 'simaps_grid_path', 'simaps_rec_cache_bytes', 'simaps_sp_lookup',
-            'simaps_get_state_mixed')
+            'simaps_get_state_mixed', 'simaps_source_hash')
 
 # error codes and device fault bits (include/simaps.h)
 EINVAL, EUNSUPPORTED, EHIP, EDEVICE = -1, -2, -3, -4

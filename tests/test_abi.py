@@ -23,7 +23,7 @@ def test_header_declares_the_abi():
                                          'simaps_ingest', 'simaps_ingest_chunks', 'simaps_path_mode', 'simaps_robot_mask', 'simaps_pack_robots',
                                          'simaps_get_state', 'simaps_sssp_grid',
                                          'simaps_grid_path', 'simaps_rec_cache_bytes', 'simaps_sp_lookup',
-                                         'simaps_get_state_mixed'])
+                                         'simaps_get_state_mixed', 'simaps_source_hash'])
 
 
 def test_library_exports_every_declared_symbol():
@@ -163,3 +163,36 @@ def test_gridgraph_window_limits_match_header():
     for h in range(1, 200, 7):
         for w in range(1, 130, 3):
             assert fits(h, w) == (w <= maxw and (h + 2) * ((w + 2) | 1) <= cells)
+
+
+def test_library_source_hash_matches_the_tree():
+    """simaps_source_hash: the library carries the hash of the sources it was
+    built from, and it is this tree's (else simaps._lib would have refused to load it)."""
+    from simaps import _lib, _srchash
+    _lib.lib.simaps_source_hash.restype = ctypes.c_char_p
+    assert _lib.lib.simaps_source_hash().decode() == _srchash.source_hash()
+    rels = [r for r, _ in _srchash.source_files()]
+    assert 'include/simaps.h' in rels and 'csrc/simaps.hip' in rels and 'csrc/grid_large.h' in rels
+
+
+def test_stale_library_is_refused(tmp_path):
+    """A copy of the tree whose kernel source differs from what its libsimaps.so was built from -- here
+    only a comment -- refuses to load the library; the unmodified copy loads it."""
+    import shutil
+    import subprocess
+    import sys
+    pkg = os.path.join(ROOT, 'spatial-intention-maps_amd')
+    dst = tmp_path / 'repo'
+    shutil.copytree(os.path.join(pkg, 'simaps'), dst / 'spatial-intention-maps_amd' / 'simaps',
+                    ignore=shutil.ignore_patterns('__pycache__', 'libsimaps_*.so'))
+    shutil.copytree(os.path.join(pkg, 'csrc'), dst / 'spatial-intention-maps_amd' / 'csrc')
+    shutil.copytree(os.path.join(ROOT, 'include'), dst / 'include')
+    code = 'import sys; sys.path.insert(0, %r); import simaps._lib' % str(dst / 'spatial-intention-maps_amd')
+    env = {k: v for k, v in os.environ.items() if not k.startswith('SIMAPS_')}
+    ok = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, env=env, timeout=300)
+    assert ok.returncode == 0, ok.stderr
+    src = dst / 'spatial-intention-maps_amd' / 'csrc' / 'simaps.hip'
+    src.write_text(src.read_text().replace('// simaps.hip --', '// simaps.hip (edited) --', 1))
+    bad = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, env=env, timeout=300)
+    assert bad.returncode != 0
+    assert 'StaleLibraryError' in bad.stderr and 'stale binary' in bad.stderr

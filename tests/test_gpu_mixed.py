@@ -143,16 +143,19 @@ def test_mixed_bad_configuration_index_is_reported(S):
     _lib, batch, synthetic = S
     scenes = _mixed_scenes(synthetic, seed=900)
     mb = batch.MixedStateBatch(scenes)
-    clean = mb.render().cpu().numpy()
+    clean = [v.cpu().numpy() for v in mb.states(mb.render())]
     _lib.check_faults()
-    # agent 0's configuration is 0: an out-of-table index clamps to it, so only the fault is visible
-    assert int(mb.plan['agent_cfg'][0]) == 0
+    # agent 0's configuration index past the table: the fault is reported and its workgroup writes
+    # nothing (no configuration's channel count is known to fit its stack); every other agent renders
     mb.agent_cfg_d[0] = 99
+    out = mb.alloc_state().fill_(float("nan"))
     torch.cuda.synchronize()
-    got = mb.render().cpu().numpy()
+    got = [v.cpu().numpy() for v in mb.states(mb.render(out=out))]
     with pytest.raises(_lib.DeviceFault, match='descriptor-clamped'):
         _lib.check_faults()
-    assert _bitwise(got, clean)
+    assert np.isnan(got[0]).all()
+    for n in range(1, mb.N):
+        assert _bitwise(got[n], clean[n]), n
 
 
 @pytest.mark.parametrize('count', [3, 5])
