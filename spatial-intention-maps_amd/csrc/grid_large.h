@@ -360,14 +360,17 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
                 const bool ok = lane < 8 && du + wl8 == dw;
                 uint64_t m = __ballot(ok);
                 if (!m) break;
-                if (fixp == 1) {
+                if (fixp == 1) {  // (as path_core: quad minima by DPP, lanes 0-3 / 4-7, then two readlanes)
                     float key = ok ? du : INFINITY;
-                    for (int o2 = 4; o2 > 0; o2 >>= 1) key = fminf(key, __shfl_xor(key, o2));
-                    m = __ballot(ok && du == __shfl(key, 0));
+                    key = fminf(key, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0xB1, 0xf, 0xf, false)));
+                    key = fminf(key, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0x4E, 0xf, 0xf, false)));
+                    const float mn = fminf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(key), 0)),
+                                           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(key), 4)));
+                    m = __ballot(ok && du == mn);
                 }
                 const int k = __builtin_ctzll(m);
-                w -= __shfl((int)off, k);
-                dw = __shfl(du, k);
+                w -= __builtin_amdgcn_readlane((int)off, k);
+                dw = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(du), k));
                 if (lane == 0) dense[nd] = (int)w;
                 nd++;
             }

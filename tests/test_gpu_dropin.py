@@ -686,6 +686,11 @@ def _dp_tie(grid, src, tgt):
         if v < 0:
             break
         dense.append([v // W, v % W])
+    return _dp_tie_dense(dense)
+
+
+def _dp_tie_dense(dense):
+    """_dp_tie on a given dense chain (target first)."""
     c = np.array(dense)
     stack = [(0, len(c) - 1)]
     while stack:

@@ -9,7 +9,7 @@
 #   pytest smoke bench bench20 prof configs extra env mixed large spawn2 rccl
 #   fuzz_states fuzz_states_plain fuzz_mixed fuzz_rows fuzz_ingest path_modes
 #   phase (needs the stamp build: make -C spatial-intention-maps_amd/csrc prof first)
-# Environment: SEED0 (fuzz seed base, default 50000), PYTEST_ARGS (default: tests -m gpu).
+# Environment: SEED0 (fuzz seed base, default 50000).  pytest=a.py,b.py runs those test files instead of tests/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag="$1"; shift
@@ -19,7 +19,7 @@ for step in "$@"; do
   name="${step%%=*}"; extra=""
   [ "$name" != "$step" ] && extra="${step#*=}" && extra="${extra//,/ }"
   case "$name" in
-    pytest)  c="600|python -u -m pytest ${PYTEST_ARGS:-tests -m gpu} -x -q --timeout 120 --timeout-method thread" ;;
+    pytest)  c="600|python -u -m pytest ${extra:-tests} -m gpu -x -q --timeout 120 --timeout-method thread"; extra="" ;;
     smoke)   c="120|python -c 'import __graft_entry__ as g; g.smoke()'" ;;
     bench)   c="300|python bench.py" ;;
     bench20) c="200|python bench.py --gpus 1 --steps 20 --warmup 5" ;;
