@@ -295,14 +295,9 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
  * fixpoint in LDS: no scratch, graph capture keeps it; half the queries per CU of mode 2);
  * 0 automatic: 3 while the whole launch is resident at once at mode 3's residency (N <= CUs x 2
  * small-room / x 1 large-room queries), else 2.  Modes 0-3 return the reference's waypoints
- * exactly.
- * 4 / 5, OPT-IN, not the reference's rule: no SPFA at all -- after the sweeps reach the f32 fixpoint D,
- * the target's chain is walked on D (parent of v: a neighbour u with fl(D(u) + w) == D(v); where
- * several tie, 4 takes the smallest D(u), then the first in pyx:30 edge order, 5 the first in edge
- * order), then approximate_polygon and the line-of-sight pruning as usual.  The chain is a shortest
- * path of length D(target) exactly, but where the SPFA would have picked another tied parent the
- * waypoints differ (SURVEY.md 8(f) row 1's looser parity: demo.py's atol=2; measured agreement in
- * DESIGN.md section 5).  No scratch, graph-capturable; large windows run gl_path_kernel's walk. */
+ * exactly.  (Round 6 measured an opt-in parent rule on the SSSP fixpoint instead of the SPFA:
+ * 5-7x faster, but 88.7 % of fuzz paths within demo.py's atol=2 against a 99.9 % bar -- not kept,
+ * DESIGN.md section 9.) */
 int simaps_path_mode(int mode);
 
 /* Batched observation ingest into the per-agent maps (occupancy / overhead [M, H, W], slot

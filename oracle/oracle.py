@@ -125,65 +125,20 @@ def approximate_polygon(coords, tolerance):
     return coords[chain, :]
 
 
-# pyx:30-32: direction k's (di, dj) and float32 length, in the reference's edge order
-DIRS = [(0, -1), (0, 1), (-1, -1), (-1, 0), (-1, 1), (1, -1), (1, 0), (1, 1)]
-DIR_LEN = [np.float32(1), np.float32(1)] + [np.float32(np.sqrt(2)), np.float32(1), np.float32(np.sqrt(2))] * 2
-
-
-def fixpoint_chain(grid_u8, source, target, rule):
-    """The dense chain target -> source of the opt-in fixpoint-parent path modes (simaps_path_mode 4 /
-    5; NOT the reference's rule -- the reference takes the SPFA's parents, pyx:131-138): on the f32
-    fixpoint D (= the SPFA's final distances, pyx:69-114), the parent of v is a neighbour u = v - dir_k
-    with float32(D(u) + len_k) == D(v); among several, rule 1 takes the smallest D(u) and then the
-    first k, rule 2 the first k.  Every step is a tight edge, so the chain's left-fold float32 length
-    from the source is D(target) exactly.  An unreachable or blocked target gives [target]."""
-    grid = np.ascontiguousarray(grid_u8, dtype=np.uint8)
-    H, W = grid.shape
-    d, _ = spfa(grid, source)
-    D = d.reshape(H, W)
-    si, sj = int(source[0]), int(source[1])
-    i, j = int(target[0]), int(target[1])
-    dense = [[i, j]]
-    if grid[i, j] == 0 or D[i, j] < 0 or grid[si, sj] == 0:
-        return dense
-    while (i, j) != (si, sj):
-        best = None
-        for k, ((di, dj), wk) in enumerate(zip(DIRS, DIR_LEN)):
-            ui, uj = i - di, j - dj
-            if not (0 <= ui < H and 0 <= uj < W) or grid[ui, uj] == 0 or D[ui, uj] < 0:
-                continue
-            if np.float32(D[ui, uj] + wk) != D[i, j]:
-                continue
-            if best is None or (rule == 1 and D[ui, uj] < D[best[0], best[1]]):
-                best = (ui, uj)
-            if rule == 2:
-                break
-        if best is None:
-            raise AssertionError('no tight edge into (%d, %d): not a fixpoint' % (i, j))
-        i, j = best
-        dense.append([i, j])
-    return dense
-
-
-def grid_shortest_path(grid_u8, source, target, fixpoint_rule=0):
+def grid_shortest_path(grid_u8, source, target):
     """GridGraph.shortest_path (pyx:121-154): parent walk target -> source, approximate_polygon
-    (tolerance 1), drop waypoints whose neighbours see each other on the grid, reversed.
-    fixpoint_rule 1 / 2: the chain of the opt-in fixpoint-parent modes (fixpoint_chain) instead of the
-    SPFA's parents; the rest unchanged."""
+    (tolerance 1), drop waypoints whose neighbours see each other on the grid, reversed."""
     grid = np.ascontiguousarray(grid_u8, dtype=np.uint8)
     H, W = grid.shape
-    if fixpoint_rule:
-        dense = fixpoint_chain(grid, source, target, fixpoint_rule)
-    else:
-        _, parents = spfa(grid, source)
-        u = int(source[0]) * W + int(source[1])
-        v = int(target[0]) * W + int(target[1])
-        dense = [[v // W, v % W]]
-        while v != u:
-            v = int(parents[v])
-            if v < 0:
-                break
-            dense.append([v // W, v % W])
+    _, parents = spfa(grid, source)
+    u = int(source[0]) * W + int(source[1])
+    v = int(target[0]) * W + int(target[1])
+    dense = [[v // W, v % W]]
+    while v != u:
+        v = int(parents[v])
+        if v < 0:
+            break
+        dense.append([v // W, v % W])
     sparse = approximate_polygon(np.array(dense), tolerance=1)
     path = [sparse[0]]
     for k in range(1, sparse.shape[0] - 1):
@@ -465,17 +420,15 @@ class AgentOracle:
             self._sp_cache[src] = spfa_image(self.cspace, src)
         return float(self._sp_cache[src][tgt]) / PPM
 
-    def shortest_path(self, source_position, target_position, fixpoint_rule=0):
-        """OccupancyMap.shortest_path (envs.py:2478-2505) -> list of (x, y) positions.  fixpoint_rule
-        1 / 2: the opt-in fixpoint-parent chain (grid_shortest_path) instead of the SPFA's parents."""
+    def shortest_path(self, source_position, target_position):
+        """OccupancyMap.shortest_path (envs.py:2478-2505) -> list of (x, y) positions."""
         si, sj = position_to_pixel_indices(source_position[0], source_position[1], self.shape)
         ti, tj = position_to_pixel_indices(target_position[0], target_position[1], self.shape)
         rr, cc = line(si, sj, ti, tj)
         if (1 - self.cspace_thin[rr, cc]).sum() == 0:
             return [tuple(source_position[:2]), tuple(target_position[:2])]
         src, tgt = self.snap(source_position), self.snap(target_position)
-        path = [pixel_indices_to_position(i, j, self.shape)
-                for i, j in grid_shortest_path(self.cspace, src, tgt, fixpoint_rule)]
+        path = [pixel_indices_to_position(i, j, self.shape) for i, j in grid_shortest_path(self.cspace, src, tgt)]
         if len(path) < 2:
             return [tuple(source_position[:2]), tuple(target_position[:2])]
         path[0] = tuple(source_position[:2])

@@ -206,13 +206,12 @@ __device__ __forceinline__ long gl_dir_off(int k, int pitch)
 
 // GridGraph(grid).shortest_path(source, target) (pyx:121-154) on windows of any size, one wave per
 // query, after gl_sssp_kernel left the fixpoint from the same source in `fix`.  Output as
-// grid_path_kernel: waypoint cells source first, count or -needed.  fixp 1 / 2 (simaps_path_mode 4 /
-// 5, opt-in): no SPFA; the chain is walked on the fixpoint with path_core's FIXP rule.
+// grid_path_kernel: waypoint cells source first, count or -needed.
 __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t *__restrict__ grids, long grid_stride,
                                                     const int32_t *__restrict__ sources, const int32_t *__restrict__ targets,
                                                     int wi0, int wj0, int wh, int ww, int *scratch, long scratch_stride,
                                                     int max_pts, int32_t *__restrict__ out_ij, int32_t *__restrict__ out_n,
-                                                    int fixp, unsigned *fault)
+                                                    unsigned *fault)
 {
     const int b = blockIdx.x, lane = threadIdx.x;
     const uint8_t *grid = grids + b * grid_stride;
@@ -266,7 +265,7 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
     bool early = false;
     // an unreachable (+inf) or blocked (-inf) target never gets a parent (pin[tv] stays 0 unless it is
     // the source): the path is [target] whatever the SPFA does, so it is not run
-    if (!(finT > -INFINITY && finT < INFINITY) || fixp) cnt = 0;
+    if (!(finT > -INFINITY && finT < INFINITY)) cnt = 0;
 #ifdef SIMAPS_GL_STATS
     const long t_start = __builtin_readcyclecounter();
 #endif
@@ -348,33 +347,7 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
     (void)early;
     // (5) dense path: parents from the target back to the source (pyx:131-138)
     int nd = 0;
-    if (fixp) {  // path_core's FIXP walk on the fixpoint (lanes 0..7: the neighbours of the chain's head)
-        const float wl8 = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
-        long w = tv;
-        float dw = finT;
-        if (lane == 0) dense[0] = (int)w;
-        nd = 1;
-        if (finT > -INFINITY && finT < INFINITY)
-            while (w != su && nd < n1) {
-                const float du = lane < 8 ? fix[w - off] : INFINITY;
-                const bool ok = lane < 8 && du + wl8 == dw;
-                uint64_t m = __ballot(ok);
-                if (!m) break;
-                if (fixp == 1) {  // (as path_core: quad minima by DPP, lanes 0-3 / 4-7, then two readlanes)
-                    float key = ok ? du : INFINITY;
-                    key = fminf(key, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0xB1, 0xf, 0xf, false)));
-                    key = fminf(key, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0x4E, 0xf, 0xf, false)));
-                    const float mn = fminf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(key), 0)),
-                                           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(key), 4)));
-                    m = __ballot(ok && du == mn);
-                }
-                const int k = __builtin_ctzll(m);
-                w -= __builtin_amdgcn_readlane((int)off, k);
-                dw = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(du), k));
-                if (lane == 0) dense[nd] = (int)w;
-                nd++;
-            }
-    } else if (lane == 0) {
+    if (lane == 0) {
         long w = tv;
         dense[nd++] = (int)w;
         while (w != su) {

@@ -2896,19 +2896,10 @@ __device__ __forceinline__ void spfa_fast_pops(int &u, int &F0, int &qn, int &qt
 // relaxations reaches the same unique f32 fixpoint and the SPFA never reads `fix` before `swept`, so
 // the results are those of EARLY; the fixpoint stays in LDS (no global scratch, no copy, chain checks
 // read LDS), so the launch also runs under graph capture.
-//
-// FIXP (round 6, simaps_path_mode 4 / 5, opt-in; needs EARLY, not OVL): no SPFA at all.  After the
-// sweeps, the target's chain is walked on the fixpoint itself: the parent of v is a neighbour u with
-// fl(D(u) + w(u, v)) == D(v) -- a real shortest-path edge, so the chain's length is D(target) exactly,
-// but where several u tie, the SPFA's pick (the first u to reach D(v) in its pop order) is only
-// approximated: FIXP 1 takes the tied u of smallest D(u) (the one an SPFA, which pops roughly by
-// distance, tends to settle first), then the first in edge order (pyx:30); FIXP 2 the first in edge
-// order.  The waypoints then go through the same approximate_polygon and line-of-sight pruning.
-template <int CELLS, bool EARLY, bool OVL = false, int FIXP = 0>
+template <int CELLS, bool EARLY, bool OVL = false>
 __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr, int H, int W, bool run_spfa,
                                          int line_mask, float *gfin, const uint16_t *&outp_ret)
 {
-    static_assert(FIXP == 0 || (EARLY && !OVL), "the fixpoint-parent walk runs after the early-exit sweeps");
     float *dist = reinterpret_cast<float *>(arr);
     uint16_t *queue = reinterpret_cast<uint16_t *>(arr + 4 * CELLS);
     uint8_t *pin = reinterpret_cast<uint8_t *>(arr + 6 * CELLS);
@@ -3004,18 +2995,16 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
         }
         if (tid == 0 && round >= h * w + 16) fault_or(sh.fault, SIMAPS_FAULT_ROUNDS);
         if (tid == 0) sh.finT = dist[tv];
-        if constexpr (FIXP == 0) {
-            for (int k = tid; k < cells; k += PNT) {
-                const float f = dist[k];
-                gfin[k] = f;
-                dist[k] = f == -INFINITY ? -INFINITY : INFR;
-            }
-            __syncthreads();  // (global stores of the other waves -> wave 0's chain checks; LDS likewise)
+        for (int k = tid; k < cells; k += PNT) {
+            const float f = dist[k];
+            gfin[k] = f;
+            dist[k] = f == -INFINITY ? -INFINITY : INFR;
         }
+        __syncthreads();  // (global stores of the other waves -> wave 0's chain checks; LDS likewise)
         if (tid == 0) STAMP_VAL(8, round + 1);
         if (tid == 0) STAMP_NB(10);  // (stamp build: the sweeps' end)
     }
-    if (FIXP == 0 && tid < 64 && run_spfa) {
+    if (tid < 64 && run_spfa) {
         const int doff = lane < 8 ? dir_off(lane, pw) : 0;
         const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
         const uint8_t pbits = (uint8_t)((lane + 1) | 0x10);  // a relaxed head: parent edge `lane`, queued
@@ -3345,44 +3334,9 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
     lds_barrier();
     if (tid == 0) STAMP_NB(3);
     // (4) dense path: parents from the target back to the source (pyx:131-138), as rect cells
-    auto pack = [&](int c) { const int rr = c / pw; return (uint16_t)(((rr - 1) << 8) | (c - rr * pw - 1)); };
-    if (FIXP != 0) {
-        // the fixpoint-parent walk (wave 0): lanes 0..7 test the 8 neighbours u = v - off(k) of the
-        // chain's head v; +-inf neighbours never satisfy the equality (D(v) is finite)
-        if (tid < 64) {
-            int cnt = 0;
-            if (run_spfa) {
-                const int doffl = lane < 8 ? dir_off(lane, pw) : 0;
-                const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
-                int v = tv;
-                float dv = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(dist[tv])));
-                if (lane == 0) dense[0] = pack(v);
-                cnt = 1;
-                if (dv > -INFINITY && dv < INFINITY)  // (unreachable / blocked target: [target], pyx:136-137)
-                    while (v != su && cnt < cells) {
-                        const float du = lane < 8 ? dist[v - doffl] : INFINITY;
-                        const bool ok = lane < 8 && du + wl == dv;
-                        uint64_t m = __ballot(ok);
-                        if (!m) break;  // (never at the fixpoint: every reached v != source has a tight edge)
-                        if (FIXP == 1) {  // the tied neighbour of smallest D(u) (quad minima, lanes 0-3 / 4-7)
-                            float key = ok ? du : INFINITY;
-                            key = fminf(key, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0xB1, 0xf, 0xf, false)));
-                            key = fminf(key, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0x4E, 0xf, 0xf, false)));
-                            const float mn = fminf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(key), 0)),
-                                                   __int_as_float(__builtin_amdgcn_readlane(__float_as_int(key), 4)));
-                            m = __ballot(ok && du == mn);
-                        }
-                        const int k = __builtin_ctzll(m);
-                        v -= __builtin_amdgcn_readlane(doffl, k);
-                        dv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(du), k));
-                        if (lane == 0) dense[cnt] = pack(v);
-                        cnt++;
-                    }
-            }
-            if (lane == 0) sh.nseg = cnt;
-        }
-    } else if (tid == 0) {
+    if (tid == 0) {
         int cnt = 0, v = tv;
+        auto pack = [&](int c) { const int rr = c / pw; return (uint16_t)(((rr - 1) << 8) | (c - rr * pw - 1)); };
         if (run_spfa) {
             dense[cnt++] = pack(v);
             while (v != su) {
@@ -3478,7 +3432,7 @@ __device__ __forceinline__ int path_core(PathHdr &sh, SsspScratch &S, char *arr,
     return 0;
 }
 
-template <int CELLS, bool EARLY, bool OVL, int FIXP = 0>
+template <int CELLS, bool EARLY, bool OVL>
 __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents,
                                                    const simaps_env *__restrict__ envs,
                                                    const simaps_robot *__restrict__ robots,
@@ -3530,9 +3484,8 @@ __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry g
     if (tid == 0) STAMP_NB(1);
     snap_sources(sh, S, 2, g);
     const uint16_t *outp;
-    const int cnt = path_core<CELLS, EARLY, OVL, FIXP>(sh, S, smem + OFF_PA, H, W, sh.src_ok[0] && sh.src_ok[1],
-                                                       LINE_CSPACE, EARLY && !OVL && !FIXP ? scratch + (size_t)n * CELLS : nullptr,
-                                                       outp);
+    const int cnt = path_core<CELLS, EARLY, OVL>(sh, S, smem + OFF_PA, H, W, sh.src_ok[0] && sh.src_ok[1], LINE_CSPACE,
+                                                 EARLY && !OVL ? scratch + (size_t)n * CELLS : nullptr, outp);
     if (tid < 64) {
         // (7) positions (envs.py:2494-2503); path[0] / path[-1] replaced by the given positions
         if (cnt < 2) {
@@ -3558,7 +3511,7 @@ __global__ void __launch_bounds__(PNT) path_kernel(simaps_config cfg, Geometry g
 // workgroup per (grid, source, target): the same exact SPFA / parent walk / approximate_polygon as
 // path_kernel, without the cspace, snap and straight-line steps of OccupancyMap.shortest_path, the
 // line-of-sight pruning on the grid itself, and the waypoints returned as cells (target last).
-template <int CELLS, bool EARLY, bool OVL, int FIXP = 0>
+template <int CELLS, bool EARLY, bool OVL>
 __global__ void __launch_bounds__(PNT) grid_path_kernel(int H, int W, const uint8_t *__restrict__ grids,
                                                         const int32_t *__restrict__ sources,
                                                         const int32_t *__restrict__ targets, int wi0, int wj0, int wh,
@@ -3599,8 +3552,8 @@ __global__ void __launch_bounds__(PNT) grid_path_kernel(int H, int W, const uint
         return;
     }
     const uint16_t *outp;
-    const int cnt = path_core<CELLS, EARLY, OVL, FIXP>(sh, S, smem + OFF_PA, H, W, true, LINE_GRID_ONE,
-                                                       EARLY && !OVL && !FIXP ? scratch + (size_t)b * CELLS : nullptr, outp);
+    const int cnt = path_core<CELLS, EARLY, OVL>(sh, S, smem + OFF_PA, H, W, true, LINE_GRID_ONE,
+                                                 EARLY && !OVL ? scratch + (size_t)b * CELLS : nullptr, outp);
     if (tid < 64) {
         if (cnt > max_pts) {
             if (lane == 0) out_n[b] = -cnt;  // caller's buffer too small
@@ -4170,7 +4123,7 @@ const Geometry &geometry()
 // queries per CU instead of 4 / 2).  0, automatic: OVL while the launch is resident at once at OVL's
 // residency (N <= CUs x per-CU), else 2 (compact when the launch is being captured).
 std::atomic<int> g_path_mode{0};
-enum PathKind { PK_COMPACT, PK_EARLY, PK_OVL, PK_FIX_MIN, PK_FIX_EDGE };
+enum PathKind { PK_COMPACT, PK_EARLY, PK_OVL };
 int device_cus()
 {
     static std::atomic<int> cache[64];
@@ -4189,8 +4142,6 @@ PathKind path_kind(int n, bool small)
     case 1: return PK_COMPACT;
     case 2: return PK_EARLY;
     case 3: return PK_OVL;
-    case 4: return PK_FIX_MIN;
-    case 5: return PK_FIX_EDGE;
     default: break;
     }
     const int per = small ? path_per_cu<PATH_SMALL_CELLS, true>() : path_per_cu<SIMAPS_MAX_ROOM_CELLS, true>();
@@ -4529,18 +4480,12 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
     PathScratch ps;
     if (kind == PK_EARLY) path_scratch(ps, st, (size_t)N * SIMAPS_MAX_ROOM_CELLS * sizeof(float));
     float *scratch = ps.p;
-#define SIMAPS_PATH_LAUNCH(C, E, O, ...)                                                               \
-    hipLaunchKernelGGL((path_kernel<C, E, O, ##__VA_ARGS__>), dim3(N), dim3(PNT), 0, st, *cfg, geo, agents, envs, robots, occupancy, \
+#define SIMAPS_PATH_LAUNCH(C, E, O)                                                                    \
+    hipLaunchKernelGGL((path_kernel<C, E, O>), dim3(N), dim3(PNT), 0, st, *cfg, geo, agents, envs, robots, occupancy, \
                        sources, targets, max_points, out_xy, out_count, scratch, g_fault_dev)
     if (kind == PK_OVL) {
         if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, true, true);
         else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, true);
-    } else if (kind == PK_FIX_MIN) {
-        if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, true, false, 1);
-        else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, false, 1);
-    } else if (kind == PK_FIX_EDGE) {
-        if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, true, false, 2);
-        else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, false, 2);
     } else if (scratch) {
         if (small) SIMAPS_PATH_LAUNCH(PATH_SMALL_CELLS, true, false);
         else SIMAPS_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, false);
@@ -4556,7 +4501,7 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
 
 int simaps_path_mode(int mode)
 {
-    if (mode < 0 || mode > 5) return fail(SIMAPS_EINVAL, "path mode %d not in 0..5", mode);
+    if (mode < 0 || mode > 3) return fail(SIMAPS_EINVAL, "path mode %d not in 0..3", mode);
     return g_path_mode.exchange(mode);
 }
 
@@ -4630,10 +4575,8 @@ int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *s
         if (const int rc = large_scratch(ps, st, (size_t)B * words * sizeof(int), "grid_path")) return rc;
         hipLaunchKernelGGL(gl_sssp_kernel, dim3(B), dim3(GL_NT), 0, st, H, W, grids, (long)H * W, sources, wi0, wj0, wh,
                            ww, ps.p, words, nullptr, g_fault_dev);
-        const PathKind kind = path_kind(B, false);
-        const int fixp = kind == PK_FIX_MIN ? 1 : kind == PK_FIX_EDGE ? 2 : 0;
         hipLaunchKernelGGL(gl_path_kernel, dim3(B), dim3(64), 0, st, H, W, grids, (long)H * W, sources, targets, wi0, wj0,
-                           wh, ww, reinterpret_cast<int *>(ps.p), words, max_points, out_ij, out_count, fixp, g_fault_dev);
+                           wh, ww, reinterpret_cast<int *>(ps.p), words, max_points, out_ij, out_count, g_fault_dev);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(SIMAPS_EHIP, "grid_path (large window) launch: %s", hipGetErrorString(e));
         return 0;
@@ -4644,18 +4587,12 @@ int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *s
     PathScratch ps;
     if (kind == PK_EARLY) path_scratch(ps, st, (size_t)B * SIMAPS_MAX_ROOM_CELLS * sizeof(float));
     float *scratch = ps.p;
-#define SIMAPS_GRID_PATH_LAUNCH(C, E, O, ...)                                                          \
-    hipLaunchKernelGGL((grid_path_kernel<C, E, O, ##__VA_ARGS__>), dim3(B), dim3(PNT), 0, st, H, W, grids, sources, targets, wi0, wj0, \
+#define SIMAPS_GRID_PATH_LAUNCH(C, E, O)                                                               \
+    hipLaunchKernelGGL((grid_path_kernel<C, E, O>), dim3(B), dim3(PNT), 0, st, H, W, grids, sources, targets, wi0, wj0, \
                        wh, ww, max_points, out_ij, out_count, scratch, g_fault_dev)
     if (kind == PK_OVL) {
         if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, true, true);
         else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, true);
-    } else if (kind == PK_FIX_MIN) {
-        if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, true, false, 1);
-        else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, false, 1);
-    } else if (kind == PK_FIX_EDGE) {
-        if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, true, false, 2);
-        else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, false, 2);
     } else if (scratch) {
         if (small) SIMAPS_GRID_PATH_LAUNCH(PATH_SMALL_CELLS, true, false);
         else SIMAPS_GRID_PATH_LAUNCH(SIMAPS_MAX_ROOM_CELLS, true, false);

@@ -132,18 +132,16 @@ def test_ingest_chunk_count_and_argument_checks():
 
 def test_path_mode_setter():
     """simaps_path_mode returns the previous mode, accepts 0 (automatic), 1 (compact), 2 (early
-    exit), 3 (early exit, sweeps overlapped) and the opt-in fixpoint-parent modes 4 / 5, and refuses
-    anything else without changing the mode (host-side only)."""
+    exit) and 3 (early exit, sweeps overlapped) and refuses anything else without changing the mode
+    (host-side only)."""
     from simaps import _lib
     L = _lib.lib
     prev = L.simaps_path_mode(1)
     try:
         assert L.simaps_path_mode(2) == 1
         assert L.simaps_path_mode(3) == 2
-        assert L.simaps_path_mode(4) == 3
-        assert L.simaps_path_mode(5) == 4
-        assert L.simaps_path_mode(0) == 5
-        for bad in (-1, 6):
+        assert L.simaps_path_mode(0) == 3
+        for bad in (-1, 4):
             assert L.simaps_path_mode(bad) == _lib.EINVAL
         assert L.simaps_path_mode(0) == 0  # unchanged by the refused calls
     finally:

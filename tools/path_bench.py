@@ -54,7 +54,7 @@ def case(cfg, envs, steps, mode=0, targets='across'):
     _lib.check_faults()
     _lib.lib.simaps_path_mode(prev)
     ms = e0.elapsed_time(e1) / steps
-    out = {'config': cfg, 'targets': targets, 'path_mode': {0: 'auto', 1: 'compact', 2: 'early_exit', 3: 'overlap', 4: 'fixpoint_min', 5: 'fixpoint_edge'}[mode],
+    out = {'config': cfg, 'targets': targets, 'path_mode': {0: 'auto', 1: 'compact', 2: 'early_exit', 3: 'overlap'}[mode],
            'paths_per_launch': N, 'ms_per_launch': ms, 'paths_per_s': N / (ms * 1e-3),
            'detours': int((cnt.cpu().numpy() > 2).sum())}
     if '--stamps' in sys.argv:
