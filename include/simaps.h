@@ -351,6 +351,37 @@ int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *s
                      int wi0, int wj0, int wh, int ww, int max_points, int32_t *out_ij, int32_t *out_count,
                      void *stream);
 
+/* ---- OccupancyMap (envs.py:2409-2524) as its own drop-in (round 6) ----------------------------------
+ * The per-agent maps of simaps_get_state / simaps_ingest ([M, H, W], slot agents[n].map_slot), with the
+ * agent's robot class (envs / robots records as for simaps_get_state) choosing the cspace disk.  All
+ * buffers DEVICE. */
+
+/* OccupancyMap.update's obstacle scatter (envs.py:2445-2450) from a point cloud: for agent n, points
+ *   [N][P][3] float32 (x, y, z) and seg [N][P] float32 (Camera.capture_image's outputs, flattened);
+ *   every point with np.isclose(seg, obstacle_seg_value) (|seg - v| <= 1e-8 + 1e-5 |v|, float64) sets
+ *   occupancy[slot][i][j] = 1 at Mapper.position_to_pixel_indices(x, y) (envs.py:2391-2397, float32,
+ *   clipped).  Points are never removed (the reference only ever sets obstacles). */
+int simaps_occupancy_scatter(const simaps_config *cfg, int N, const simaps_agent *agents, const float *points,
+                             const float *seg, int P, double obstacle_seg_value, uint8_t *occupancy, void *stream);
+
+/* The maps OccupancyMap.update derives (envs.py:2453-2456), over the whole grid, per agent n:
+ *   cspace [N][H][W] u8 = configuration_space: 1 - max(1 - room_mask, binary_dilation(occupancy,
+ *   disk(floor(RADIUS * 96)))) -- 1 = free, 0 outside the room rect;
+ *   cspace_thin [N][H][W] u8 = 1 - binary_dilation(min(room_mask, occupancy), disk(3)).
+ *   Either may be NULL (not both).  Replaces reading om.configuration_space / om.cspace_thin. */
+int simaps_build_cspace(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                        const simaps_robot *robots, const uint8_t *occupancy, uint8_t *cspace, uint8_t *cspace_thin,
+                        void *stream);
+
+/* OccupancyMap._closest_valid_cspace_indices (envs.py:2523-2524) = closest_cspace_indices[:, i, j], the
+ *   scipy distance_transform_edt(1 - cspace, return_indices=True) feature transform (its tie rule) at
+ *   query pixels: pixels [N][Q][2] int32 (i, j) -> out [N][Q][2] int32 (snapped i, j).  A free pixel is
+ *   itself.  A pixel outside the grid, or a map without any free cell, gives (-1, -1) (numpy would
+ *   wrap negative indices / return scipy's value for an all-background image). */
+int simaps_snap_sources(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                        const simaps_robot *robots, const uint8_t *occupancy, const int32_t *pixels, int Q,
+                        int32_t *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -795,6 +795,58 @@ __device__ __forceinline__ void snap_sources(SH &sh, SC &S, int nsrc, const Grou
     g.sync();
 }
 
+// snap_sources' slow path for one query pixel (qi, qj) on one wave (wave-uniform, anywhere in the grid;
+// occupancy_map_kernel).  The same algorithm, kept apart so that the kernels calling snap_sources keep
+// their code bit for bit (tools/isa_digest.py: folding snap_sources onto it moved the get_state
+// kernel's register allocation).  scipy's
+// feature transform at the query (pass 1 along axis 0: per column the nearest free row, ties low;
+// pass 2 along axis 1 at the query row: the lower envelope of (row - qi)^2 + (col - qj)^2, which yields
+// the minimising column, the lowest one on a tie -- a member is dropped only if its interval is
+// strictly empty and the query scan stops at the first member the next one does not strictly beat;
+// checked against scipy's serial envelope code on 2 x 10^5 random cases, 1.2 x 10^4 of them with
+// ties).  Lane l owns rect columns l and l + 64: rows are scanned outward from the query row (qr - d
+// before qr + d: ties low), every column at once, until no column still searching can reach the best
+// (d^2 + dc^2, column) key found so far.  found(si, sj) is called by every lane with the snapped cell,
+// not at all if the rect has no free cell.
+template <class F>
+__device__ __forceinline__ void snap_wave(const B128 *freeb, int h, int w, int i0, int j0, int qi, int qj, F &&found)
+{
+    const int lane = threadIdx.x & 63;
+    const int qr = qi - i0, qc = qj - j0;
+    int rowd[2] = {-1, -1}, row[2] = {0, 0};  // per column: the nearest free row's distance / row
+    // (d^2 + dc^2) << 7 | column: the lexicographic minimum, 64-bit (the query is clamped to the
+    // grid only, so d and dc reach the grid size)
+    long long best = 0x7fffffffffffffffll;
+    const int dmax = max(abs(qr), abs(qr - (h - 1)));  // the farthest rect row from the query row
+    for (int d = 0; d <= dmax; d++) {
+        const long long dd = (long long)d * d;
+        if (dd << 7 > best) break;  // no column still searching can reach the best key
+        const int ra = qr - d, rb = qr + d;
+        const bool va = ra >= 0 && ra < h, vb = d > 0 && rb >= 0 && rb < h;
+        if (!va && !vb && ra < 0 && rb >= h) break;  // every row visited
+        const B128 fa = va ? freeb[ra] : B128{0ull, 0ull};
+        const B128 fb = vb ? freeb[rb] : B128{0ull, 0ull};
+        for (int k = 0; k < 2; k++) {
+            const int c = lane + 64 * k;
+            if (c < w && rowd[k] < 0) {
+                if (b_test(fa, c)) { rowd[k] = d; row[k] = ra; }
+                else if (b_test(fb, c)) { rowd[k] = d; row[k] = rb; }
+                if (rowd[k] >= 0) {
+                    const long long key = (((long long)d * d + (long long)(c - qc) * (c - qc)) << 7) | c;
+                    best = min(best, key);
+                }
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) best = min(best, __shfl_xor(best, off));
+    }
+    if (best != 0x7fffffffffffffffll) {  // (no free cell at all: not found)
+        const int c = (int)(best & 127);
+        const int owner = c & 63, k = c >> 6;
+        const int r = __shfl(k ? row[1] : row[0], owner);
+        found(i0 + r, j0 + c);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Phase: single-source shortest paths for nsrc sources over the free cells of the rect
 // ------------------------------------------------------------------------------------------------
@@ -3991,6 +4043,7 @@ __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
 
 #ifndef SIMAPS_DEVICE_ONLY
 #include "grid_large.h"
+#include "occupancy_map.h"
 #endif
 
 }  // namespace
@@ -4633,6 +4686,60 @@ int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *s
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "sssp_grid launch: %s", hipGetErrorString(e));
     return 0;
+}
+
+int simaps_occupancy_scatter(const simaps_config *cfg, int N, const simaps_agent *agents, const float *points,
+                             const float *seg, int P, double obstacle_seg_value, uint8_t *occupancy, void *stream)
+{
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (N < 0 || P < 0) return fail(SIMAPS_EINVAL, "N < 0 or P < 0");
+    if (N == 0 || P == 0) return 0;
+    if (!agents || !points || !seg || !occupancy) return fail(SIMAPS_EINVAL, "NULL buffer");
+    if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d maps per launch (grid y <= 65535)", N);
+    if ((rc = pending_faults())) return rc;
+    hipLaunchKernelGGL(occupancy_scatter_kernel, dim3((P + 255) / 256, N), dim3(256), 0, (hipStream_t)stream, cfg->H,
+                       cfg->W, P, agents, points, seg, obstacle_seg_value, occupancy);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "occupancy_scatter launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
+static int occupancy_map_launch(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                         const simaps_robot *robots, const uint8_t *occupancy, uint8_t *cspace, uint8_t *thin,
+                         const int32_t *pixels, int Q, int32_t *snapped, void *stream)
+{
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (N < 0 || Q < 0) return fail(SIMAPS_EINVAL, "N < 0 or Q < 0");
+    if (N == 0) return 0;
+    if (!agents || !envs || !robots || !occupancy) return fail(SIMAPS_EINVAL, "NULL buffer");
+    if (N > 65535) return fail(SIMAPS_EUNSUPPORTED, "%d agents per launch (grid y <= 65535)", N);
+    if ((rc = pending_faults())) return rc;
+    const int chunks = snapped ? (Q + OCC_SNAP_PER_WG - 1) / OCC_SNAP_PER_WG : 1;
+    if (chunks == 0) return 0;
+    hipLaunchKernelGGL(occupancy_map_kernel, dim3(chunks, N), dim3(PNT), 0, (hipStream_t)stream, *cfg, geometry(), agents,
+                       envs, robots, occupancy, cspace, thin, pixels, Q, snapped, g_fault_dev);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "occupancy_map launch: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int simaps_build_cspace(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                        const simaps_robot *robots, const uint8_t *occupancy, uint8_t *cspace, uint8_t *cspace_thin,
+                        void *stream)
+{
+    if (!cspace && !cspace_thin) return fail(SIMAPS_EINVAL, "neither cspace nor cspace_thin requested");
+    return occupancy_map_launch(cfg, N, agents, envs, robots, occupancy, cspace, cspace_thin, nullptr, 0, nullptr, stream);
+}
+
+int simaps_snap_sources(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                        const simaps_robot *robots, const uint8_t *occupancy, const int32_t *pixels, int Q,
+                        int32_t *out, void *stream)
+{
+    if (Q > 0 && (!pixels || !out)) return fail(SIMAPS_EINVAL, "NULL buffer");
+    if (Q == 0) return 0;
+    return occupancy_map_launch(cfg, N, agents, envs, robots, occupancy, nullptr, nullptr, pixels, Q, out, stream);
 }
 
 }  // extern "C"

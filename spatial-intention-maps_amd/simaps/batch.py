@@ -504,6 +504,58 @@ class StateBatch(_ArrayUpload):
         return out
 
 
+    # -- OccupancyMap (envs.py:2409-2524) outputs (round 6) ---------------------------------------------
+    def scatter_obstacles(self, points, seg, obstacle_seg_value, slots=None, stream=None):
+        """OccupancyMap.update's obstacle scatter (envs.py:2445-2450) into the occupancy maps of map slots
+        `slots` (all if None): points [n, P, 3] float32 (x, y, z), seg [n, P] float32 -- every point with
+        np.isclose(seg, obstacle_seg_value) marks its pixel occupied.  One launch (simaps_occupancy_scatter)."""
+        agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
+        pts = torch.as_tensor(points, dtype=torch.float32).to(self.device).reshape(n, -1, 3).contiguous()
+        sg = torch.as_tensor(seg, dtype=torch.float32).to(self.device).reshape(n, -1).contiguous()
+        if sg.shape[1] != pts.shape[1]:
+            raise ValueError('points [n, P, 3] and seg [n, P] must have the same P')
+        if n == 0 or pts.shape[1] == 0:
+            return
+        self._map_ver[slice(None) if slots is None else np.asarray(list(slots), dtype=np.int64)] += 1
+        s, cur = launch_stream(self.device, stream)
+        _lib.check(_lib.lib.simaps_occupancy_scatter(self.cfg, n, _lib.ptr(agents_d), _lib.ptr(pts), _lib.ptr(sg),
+                                                     pts.shape[1], float(obstacle_seg_value), _lib.ptr(self.occupancy),
+                                                     _lib.stream_handle(s)))
+        hold(s, cur, agents_d, pts, sg, self.occupancy)
+
+    def build_cspace(self, slots=None, cspace=True, thin=True, stream=None):
+        """OccupancyMap.configuration_space / cspace_thin (envs.py:2453, 2456) of map slots `slots` (all
+        if None) over the whole grid: (cspace [n, H, W] uint8 or None, cspace_thin [n, H, W] uint8 or
+        None) device tensors.  One launch (simaps_build_cspace)."""
+        agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
+        z = lambda on: torch.empty((n, self.H, self.W), dtype=torch.uint8, device=self.device) if on else None  # noqa: E731
+        cs, th = z(cspace), z(thin)
+        if n == 0 or (cs is None and th is None):
+            return cs, th
+        s, cur = launch_stream(self.device, stream)
+        _lib.check(_lib.lib.simaps_build_cspace(self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d),
+                                                _lib.ptr(self.occupancy), _lib.ptr(cs), _lib.ptr(th), _lib.stream_handle(s)))
+        hold(s, cur, agents_d, self.occupancy, cs, th)
+        return cs, th
+
+    def snap_pixels(self, pixels, slots=None, stream=None):
+        """OccupancyMap._closest_valid_cspace_indices (envs.py:2523-2524) = closest_cspace_indices[:, i, j]
+        of each agent's own map at query pixels [n, Q, 2] int (i, j) -> [n, Q, 2] int32 device tensor
+        ((-1, -1) for pixels outside the grid).  One launch (simaps_snap_sources)."""
+        agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
+        px = torch.as_tensor(pixels).to(device=self.device, dtype=torch.int32).contiguous()
+        if px.dim() != 3 or px.shape[0] != n or px.shape[2] != 2:
+            raise ValueError('pixels must be [%d, Q, 2]' % n)
+        out = torch.empty(px.shape, dtype=torch.int32, device=self.device)
+        Q = px.shape[1]
+        if n == 0 or Q == 0:
+            return out
+        s, cur = launch_stream(self.device, stream)
+        _lib.check(_lib.lib.simaps_snap_sources(self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d),
+                                                _lib.ptr(self.occupancy), _lib.ptr(px), Q, _lib.ptr(out), _lib.stream_handle(s)))
+        hold(s, cur, agents_d, self.occupancy, px, out)
+        return out
+
     def shortest_paths(self, sources, targets, slots=None, max_points=64, stream=None):
         """OccupancyMap.shortest_path(source, target) (envs.py:2478-2505) on each agent's own map:
         sources / targets [n, 2] fp64 (x, y) for map slots `slots` (all agents if None) -> list of n

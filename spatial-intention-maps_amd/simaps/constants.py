@@ -156,3 +156,11 @@ def host_rotate_rounding():
     raise RuntimeError('numpy matmul rounds rot_matrix @ v in neither the fused nor the plain form '
                        '(%d / %d / %d): the drop-in cannot reproduce this host\'s scipy.ndimage.rotate' % (
                            votes['fma'], votes['plain'], n))
+
+
+def position_to_pixel_indices(x, y, shape):
+    """Mapper.position_to_pixel_indices (envs.py:2391-2397) of one position given as Python floats
+    (float64 arithmetic, as numpy does for them): (i, j) ints, clipped to the grid."""
+    i = math.floor(shape[0] / 2 - y * LOCAL_MAP_PIXELS_PER_METER)
+    j = math.floor(shape[1] / 2 + x * LOCAL_MAP_PIXELS_PER_METER)
+    return min(max(i, 0), shape[0] - 1), min(max(j, 0), shape[1] - 1)

@@ -278,4 +278,137 @@ class GridGraph:
         return float(self.shortest_path_images([source])[0][i, j])
 
 
-__all__ = ['VectorEnvObservations', 'GridGraph', 'robot_groups', 'window_fits']
+def _robot_type(robot):
+    """'lifting_robot' ... from a type name or a reference Robot object (reference_adapter.robot_type)."""
+    if isinstance(robot, str):
+        if robot not in _lib.TYPE_IDS:
+            raise ValueError('unknown robot type %r' % robot)
+        return robot
+    from .reference_adapter import robot_type
+    return robot_type(robot)
+
+
+class OccupancyMap:
+    """envs.OccupancyMap (envs.py:2409-2524) on the device, for one robot's map.
+
+    The reference keeps the occupancy grid of one robot, and on update() derives from it the
+    configuration space (disk of the robot's radius), the EDT snap table (closest_cspace_indices),
+    cspace_thin and a GridGraph; shortest_path / shortest_path_distance / shortest_path_image answer
+    movement and reward queries on them.  Here the grid lives on the device and every derived map is a
+    kernel output of the C ABI (simaps_occupancy_scatter, simaps_build_cspace, simaps_snap_sources,
+    simaps_shortest_path, simaps_sp_distance, simaps_sssp_grid), bit for bit the reference's.
+    `robot`: a reference Robot object or a type name ('lifting_robot', ...).  The NumPy views
+    (occupancy_map, configuration_space, cspace_thin, closest_cspace_indices) are copies made on
+    access; closest_cspace_indices (the whole [2, H, W] table) is computed on first access after an
+    update."""
+
+    def __init__(self, robot, room_length, room_width, show_map=False, device='cuda'):
+        if show_map:
+            raise NotImplementedError('show_map is the reference\'s matplotlib window (out of scope)')
+        from . import constants as K
+        self.robot = robot
+        self.room_length, self.room_width = room_length, room_width
+        self.show_map = False
+        typ = _robot_type(robot)
+        H, W = K.padded_room_shape(room_width, room_length)
+        rob = {'type': typ, 'cls': K.ROBOT_TYPES.index(typ), 'group_index': 0, 'position': (0.0, 0.0, 0.0),
+               'heading': 0.0, 'lift_state': None, 'idle': True, 'waypoint_positions': None, 'waypoint_index': None,
+               'target_ee': None}
+        scene = {'env_name': 'occupancy_map', 'room_length': room_length, 'room_width': room_width,
+                 'flags': dict(K.DEFAULT_FLAGS), 'robot_config': [{typ: 1}], 'H': H, 'W': W,
+                 'receptacle_position': None, 'robots': [rob],
+                 'occupancy': np.zeros((1, H, W), np.uint8), 'overhead': np.zeros((1, H, W), np.float32)}
+        self._b = _batch.StateBatch([scene], device=device)
+        self._cspace = self._thin = self._closest = None
+        self.grid_graph = None
+
+    # -- the reference's attributes, as host copies ------------------------------------------------------
+    @property
+    def occupancy_map(self):
+        return self._b.occupancy[0].cpu().numpy()
+
+    @occupancy_map.setter
+    def occupancy_map(self, grid):
+        self._b.set_maps(occupancy=torch.as_tensor(np.asarray(grid, dtype=np.uint8))[None])
+        self._derive()
+
+    @property
+    def configuration_space(self):
+        return None if self._cspace is None else self._cspace.cpu().numpy()
+
+    @property
+    def cspace_thin(self):
+        return None if self._thin is None else self._thin.cpu().numpy()
+
+    @property
+    def closest_cspace_indices(self):
+        """[2, H, W] int32: scipy distance_transform_edt(1 - cspace, return_indices=True) (envs.py:2455)."""
+        if self._cspace is None:
+            return None
+        if self._closest is None:
+            H, W = self._b.H, self._b.W
+            ii, jj = torch.meshgrid(torch.arange(H, dtype=torch.int32), torch.arange(W, dtype=torch.int32), indexing='ij')
+            px = torch.stack([ii, jj], -1).reshape(1, H * W, 2)
+            out = self._b.snap_pixels(px).cpu().numpy()
+            _lib.check_faults()
+            self._closest = out[0].T.reshape(2, H, W).copy()
+        return self._closest
+
+    # -- OccupancyMap.update (envs.py:2445-2466) -----------------------------------------------------------
+    def update(self, points, seg, obstacle_seg_value):
+        """points [..., 3] / seg [...] (Camera.capture_image, envs.py:1927-1955): the obstacle points mark
+        the occupancy grid, then the cspace, cspace_thin and the grid graph are rebuilt."""
+        pts = np.asarray(points, dtype=np.float32).reshape(1, -1, 3)
+        sg = np.asarray(seg, dtype=np.float32).reshape(1, -1)
+        self._b.scatter_obstacles(pts, sg, obstacle_seg_value)
+        self._derive()
+
+    def _derive(self):
+        cs, th = self._b.build_cspace()
+        self._cspace, self._thin, self._closest = cs[0], th[0], None
+        self.grid_graph = GridGraph(self._cspace, device=self._b.device)
+
+    def _need_update(self):
+        if self._cspace is None:
+            raise RuntimeError('OccupancyMap: call update() first (the reference has no cspace before it)')
+
+    def _closest_valid_cspace_indices(self, i, j):
+        self._need_update()
+        out = self._b.snap_pixels(torch.tensor([[[int(i), int(j)]]], dtype=torch.int32)).cpu().numpy()
+        _lib.check_faults()
+        return out[0, 0]
+
+    def _pixel(self, position):
+        from . import constants as K
+        return K.position_to_pixel_indices(position[0], position[1], (self._b.H, self._b.W))
+
+    # -- queries (envs.py:2478-2517) --------------------------------------------------------------------
+    def shortest_path(self, source_position, target_position):
+        """Waypoints [source_position, (x, y, 0), ..., target_position] (envs.py:2478-2505)."""
+        self._need_update()
+        path = self._b.shortest_paths(np.array([[float(source_position[0]), float(source_position[1])]]),
+                                      np.array([[float(target_position[0]), float(target_position[1])]]))[0]
+        path[0], path[-1] = source_position, target_position
+        return path
+
+    def shortest_path_distance(self, source_position, target_position):
+        """Shortest-path length in metres (envs.py:2507-2512); -1/96 if unreachable."""
+        self._need_update()
+        d = self._b.shortest_path_distances(np.array([[float(source_position[0]), float(source_position[1])]]),
+                                            np.array([[[float(target_position[0]), float(target_position[1])]]]))
+        d = float(d.cpu().numpy()[0, 0])
+        _lib.check_faults()
+        return d
+
+    def shortest_path_image(self, position):
+        """[H, W] float32 image of shortest-path distances (metres) from `position`'s snapped pixel,
+        -1/96 where unreachable (envs.py:2514-2517)."""
+        self._need_update()
+        i, j = self._closest_valid_cspace_indices(*self._pixel(position))
+        return self.grid_graph.shortest_path_image((int(i), int(j))) / np.float32(96)
+
+    def save_figure(self, output_path):
+        raise NotImplementedError('save_figure needs show_map (the reference\'s matplotlib window, out of scope)')
+
+
+__all__ = ['VectorEnvObservations', 'GridGraph', 'OccupancyMap', 'robot_groups', 'window_fits']

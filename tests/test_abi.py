@@ -23,7 +23,8 @@ def test_header_declares_the_abi():
                                          'simaps_ingest', 'simaps_ingest_chunks', 'simaps_path_mode', 'simaps_robot_mask', 'simaps_pack_robots',
                                          'simaps_get_state', 'simaps_sssp_grid',
                                          'simaps_grid_path', 'simaps_rec_cache_bytes', 'simaps_sp_lookup',
-                                         'simaps_get_state_mixed', 'simaps_source_hash'])
+                                         'simaps_get_state_mixed', 'simaps_source_hash', 'simaps_occupancy_scatter',
+                                         'simaps_build_cspace', 'simaps_snap_sources'])
 
 
 def test_library_exports_every_declared_symbol():
@@ -196,3 +197,33 @@ def test_stale_library_is_refused(tmp_path):
     bad = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, env=env, timeout=300)
     assert bad.returncode != 0
     assert 'StaleLibraryError' in bad.stderr and 'stale binary' in bad.stderr
+
+
+def test_occupancy_map_host_side():
+    """The OccupancyMap drop-in: no CPU path (the grid and every derived map live on the device),
+    show_map / save_figure (matplotlib windows) refused; the host pixel-index helper equals the
+    oracle's Mapper.position_to_pixel_indices (envs.py:2391-2397) on random and pixel-edge positions;
+    the three OccupancyMap entries refuse bad arguments before any launch."""
+    import oracle as O
+    from simaps import _lib, batch, constants as K, synthetic, vector_env
+    with pytest.raises(ValueError):
+        vector_env.OccupancyMap('lifting_robot', 1.0, 0.5, device='cpu')
+    with pytest.raises(NotImplementedError):
+        vector_env.OccupancyMap('lifting_robot', 1.0, 0.5, show_map=True)
+    with pytest.raises(ValueError):
+        vector_env.OccupancyMap('flying_robot', 1.0, 0.5)
+    rs = np.random.RandomState(3)
+    for _ in range(5000):
+        x, y = rs.uniform(-1.5, 1.5, 2)
+        if rs.rand() < 0.3:
+            x, y = round(x * 96) / 96, round(y * 96) / 96
+        want = O.position_to_pixel_indices(x, y, (184, 232))
+        assert K.position_to_pixel_indices(x, y, (184, 232)) == (int(want[0]), int(want[1]))
+    c = batch.make_config(synthetic.config_flags('lifting_4-small_divider'), 0.5, 1.0)
+    L = _lib.lib
+    assert L.simaps_build_cspace(c, 1, None, None, None, None, None, None, None) == _lib.EINVAL   # nothing asked
+    assert L.simaps_build_cspace(c, 0, None, None, None, None, ctypes.c_void_p(8), None, None) == 0
+    assert L.simaps_snap_sources(c, 1, None, None, None, None, None, 3, None, None) == _lib.EINVAL
+    assert L.simaps_snap_sources(c, 1, None, None, None, None, None, 0, None, None) == 0
+    assert L.simaps_occupancy_scatter(c, 1, None, None, None, 5, 0.25, None, None) == _lib.EINVAL
+    assert L.simaps_occupancy_scatter(c, 2, None, None, None, 0, 0.25, None, None) == 0
