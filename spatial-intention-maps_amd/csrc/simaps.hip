@@ -2355,7 +2355,14 @@ __device__ __forceinline__ void sweep_track(Shared &sh, SsspScratch &S, float *d
 }
 
 #ifndef SIMAPS_DEVICE_ONLY  // (simaps_mixed.hip includes this file for its device helpers only)
-__global__ void __launch_bounds__(NT) get_state_kernel(
+#ifdef SIMAPS_VGPR_CAP  // timing-only A/B build (tools/coresidency_model.py): the kernel squeezed to 8 waves
+                        // per SIMD (<= 64 VGPRs, spills included) -- what two co-resident 16-wave stacks per
+                        // CU would need; its LDS is dynamic so that the occupancy target is honoured
+#define SIMAPS_GS_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#else
+#define SIMAPS_GS_ATTR
+#endif
+__global__ void __launch_bounds__(NT) SIMAPS_GS_ATTR get_state_kernel(
     simaps_config cfg, Geometry geo, const simaps_agent *__restrict__ agents, const simaps_env *__restrict__ envs,
     const simaps_robot *__restrict__ robots, const double *__restrict__ paths, const uint8_t *__restrict__ occupancy,
     const float *__restrict__ overhead, float *__restrict__ state, int C, simaps_debug dbg, unsigned *fault)
@@ -4428,8 +4435,16 @@ int simaps_get_state(const simaps_config *cfg, int N, const simaps_agent *agents
     simaps_debug d;
     memset(&d, 0, sizeof(d));
     if (dbg) d = *dbg;
+#ifdef SIMAPS_VGPR_CAP
+    static const hipError_t lds_ok =
+        hipFuncSetAttribute((const void *)get_state_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (lds_ok != hipSuccess) return fail(SIMAPS_EHIP, "dynamic LDS of the VGPR-cap build");
+    hipLaunchKernelGGL(get_state_kernel, dim3(N), dim3(NT), LDS_BYTES, (hipStream_t)stream, *cfg, geo, agents, envs,
+                       robots, paths, occupancy, overhead, state, C, d, g_fault_dev);
+#else
     hipLaunchKernelGGL(get_state_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, geo, agents, envs,
                        robots, paths, occupancy, overhead, state, C, d, g_fault_dev);
+#endif
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SIMAPS_EHIP, "get_state launch: %s", hipGetErrorString(e));
     return 0;
