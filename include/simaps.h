@@ -382,6 +382,17 @@ int simaps_snap_sources(const simaps_config *cfg, int N, const simaps_agent *age
                         const simaps_robot *robots, const uint8_t *occupancy, const int32_t *pixels, int Q,
                         int32_t *out, void *stream);
 
+/* The global maps of Mapper.get_state(save_figures=True) (envs.py:2115-2182), per agent n over the whole
+ * grid, [N][H][W] float32 each (any may be NULL; DEVICE): overhead_map = _create_global_overhead_map
+ * (2244-2249), robot_map = _create_global_robot_map(seg=False) (2251-2276), history_map / intention_map =
+ * _create_global_intention_or_history_map('history' / the configuration's encoding) (2302-2347).
+ * Descriptors as for simaps_get_state (overhead [M][H][W]: the maps without robots, slot
+ * agents[n].map_slot).  A debug export (the fused kernel keeps only each agent's 136 x 136 crop); the
+ * shortest-path maps come from simaps_build_cspace + simaps_snap_sources + simaps_sssp_grid. */
+int simaps_global_maps(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                       const simaps_robot *robots, const double *paths, const float *overhead, float *overhead_map,
+                       float *robot_map, float *history_map, float *intention_map, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

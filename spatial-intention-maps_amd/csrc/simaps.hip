@@ -1889,6 +1889,42 @@ struct RenderCtx {
     }
 };
 
+// A robot's stamp geometry (Mapper._create_global_robot_map, envs.py:2251-2276): the scipy rotate of
+// its class mask (angle = degrees(heading) - 90), the placement pixel - S // 2, a conservative box of
+// global pixels outside which the rotated mask is surely 0, its robot-code bits and seg value.  (Also
+// the global-maps debug kernel's, global_maps.h.)
+__device__ __forceinline__ void robot_params(RobotP &P, const simaps_robot &r, const simaps_config &cfg, const Geometry &geo,
+                                             int H, int W)
+{
+    const Rot R = rot_params(LW, r.heading * RAD_TO_DEG - 90.0, cfg.rotate_rounding == SIMAPS_ROT_PLAIN);
+    P.c = R.c; P.s = R.s; P.f0 = R.f0; P.f1 = R.f1; P.S0 = R.S0; P.S1 = R.S1;
+    int pi, pj;
+    pos_to_pix(r.x, r.y, H, W, pi, pj);
+    P.st_i = pi - R.S0 / 2;
+    P.st_j = pj - R.S1 / 2;
+    P.type = r.type; P.lifting = r.lifting; P.idle = r.idle; P.group = r.group_index;
+    P.x = r.x; P.y = r.y; P.tx = r.target_x; P.ty = r.target_y;
+    pos_to_pix(r.target_x, r.target_y, H, W, P.tpi, P.tpj);
+    {   // conservative prefilter box: inverse-rotate the mask's nonzero window (+-2 px)
+        const int st = geo.mask_start[r.type], wd = geo.mask_width[r.type];
+        const double lo0 = st - (r.type == SIMAPS_LIFTING ? geo.cube_w : 0) - 1.0, hi0 = st + wd + 1.0;
+        const double lo1 = st - 1.0, hi1 = st + wd + 1.0;
+        double mn0 = 1e30, mx0 = -1e30, mn1 = 1e30, mx1 = -1e30;
+        for (int q = 0; q < 4; q++) {
+            const double a = ((q & 1) ? hi0 : lo0) - R.f0, b = ((q & 2) ? hi1 : lo1) - R.f1;
+            const double o0 = R.c * a - R.s * b, o1 = R.s * a + R.c * b;
+            mn0 = fmin(mn0, o0); mx0 = fmax(mx0, o0); mn1 = fmin(mn1, o1); mx1 = fmax(mx1, o1);
+        }
+        P.bi0 = max(P.st_i, P.st_i + (int)floor(mn0) - 2);
+        P.bi1 = min(P.st_i + R.S0 - 1, P.st_i + (int)ceil(mx0) + 2);
+        P.bj0 = max(P.st_j, P.st_j + (int)floor(mn1) - 2);
+        P.bj1 = min(P.st_j + R.S1 - 1, P.st_j + (int)ceil(mx1) + 2);
+        P.bi1 = min(P.bi1, P.bi0 + 31);  // the window is <= 17 x 13 px: its rotated box fits 32 x 32
+        P.bj1 = min(P.bj1, P.bj0 + 31);
+    }
+    P.seg_val = (float)((r.group_index + 1 + 4) / 8.0);  // SEG_VALUES['robot_group_{g+1}'] (envs.py:1885-1889)
+    P.code0 = (1u << r.group_index) | (r.type != SIMAPS_LIFTING ? 1u << 5 : (!r.lifting ? 1u << 4 : 0u));}
+
 // Mapper._get_intention_channels (envs.py:2349-2378), the per-agent part: robots ordered by
 // distance (np.argsort -> stable insertion sort) and the nonspatial (dist * sin, dist * cos) pairs.
 // One thread, in the params phase (fp64 libm calls need registers the render phase does not have).
@@ -4051,6 +4087,7 @@ __global__ void __launch_bounds__(INGEST_RES_WG) ingest_resolve_kernel(
 #ifndef SIMAPS_DEVICE_ONLY
 #include "grid_large.h"
 #include "occupancy_map.h"
+#include "global_maps.h"
 #endif
 
 }  // namespace
@@ -4755,6 +4792,23 @@ int simaps_snap_sources(const simaps_config *cfg, int N, const simaps_agent *age
     if (Q > 0 && (!pixels || !out)) return fail(SIMAPS_EINVAL, "NULL buffer");
     if (Q == 0) return 0;
     return occupancy_map_launch(cfg, N, agents, envs, robots, occupancy, nullptr, nullptr, pixels, Q, out, stream);
+}
+
+int simaps_global_maps(const simaps_config *cfg, int N, const simaps_agent *agents, const simaps_env *envs,
+                       const simaps_robot *robots, const double *paths, const float *overhead, float *overhead_map,
+                       float *robot_map, float *history_map, float *intention_map, void *stream)
+{
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (N < 0) return fail(SIMAPS_EINVAL, "N < 0");
+    if (N == 0 || (!overhead_map && !robot_map && !history_map && !intention_map)) return 0;
+    if (!agents || !envs || !robots || !paths || (overhead_map && !overhead)) return fail(SIMAPS_EINVAL, "NULL buffer");
+    if ((rc = pending_faults())) return rc;
+    hipLaunchKernelGGL(global_maps_kernel, dim3(N), dim3(NT), 0, (hipStream_t)stream, *cfg, geometry(), agents, envs,
+                       robots, paths, overhead, overhead_map, robot_map, history_map, intention_map, g_fault_dev);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SIMAPS_EHIP, "global_maps launch: %s", hipGetErrorString(e));
+    return 0;
 }
 
 }  // extern "C"

@@ -139,6 +139,8 @@ def _load(path=LIB_PATH):
         L.simaps_build_cspace.restype = i32
         L.simaps_snap_sources.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, i32, vp, vp]
         L.simaps_snap_sources.restype = i32
+        L.simaps_global_maps.argtypes = [ctypes.POINTER(Config), i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.simaps_global_maps.restype = i32
     v = L.simaps_abi_version()
     if v != ABI_VERSION:
         if os.environ.get('SIMAPS_AB_OLD_ABI') != str(v):
@@ -171,7 +173,7 @@ EXPORTED = ('simaps_abi_version', 'simaps_last_error', 'simaps_fault_status', 's
             'simaps_robot_mask', 'simaps_pack_robots', 'simaps_get_state', 'simaps_sp_distance', 'simaps_shortest_path', 'simaps_ingest', 'simaps_ingest_chunks', 'simaps_path_mode',
             'simaps_sssp_grid', 'simaps_grid_path', 'simaps_rec_cache_bytes', 'simaps_sp_lookup',
             'simaps_get_state_mixed', 'simaps_source_hash', 'simaps_occupancy_scatter', 'simaps_build_cspace',
-            'simaps_snap_sources')
+            'simaps_snap_sources', 'simaps_global_maps')
 
 # error codes and device fault bits (include/simaps.h)
 EINVAL, EUNSUPPORTED, EHIP, EDEVICE = -1, -2, -3, -4

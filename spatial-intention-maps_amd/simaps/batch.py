@@ -556,6 +556,45 @@ class StateBatch(_ArrayUpload):
         hold(s, cur, agents_d, self.occupancy, px, out)
         return out
 
+    def global_maps(self, slots=None, stream=None):
+        """The whole-grid maps of Mapper.get_state(save_figures=True) (envs.py:2115-2182) for map slots
+        `slots` (all if None), one launch (simaps_global_maps): {'overhead': _create_global_overhead_map,
+        'robot': _create_global_robot_map(seg=False) (if use_robot_map), 'history' / 'intention':
+        _create_global_intention_or_history_map (if use_history_map / use_intention_map)} as [n, H, W]
+        float32 device tensors."""
+        agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
+        z = lambda: torch.empty((n, self.H, self.W), dtype=torch.float32, device=self.device)  # noqa: E731
+        out = {'overhead': z()}
+        if self.flags['use_robot_map']:
+            out['robot'] = z()
+        if self.flags['use_history_map']:
+            out['history'] = z()
+        if self.flags['use_intention_map']:
+            out['intention'] = z()
+        if n == 0:
+            return out
+        s, cur = launch_stream(self.device, stream)
+        _lib.check(_lib.lib.simaps_global_maps(self.cfg, n, _lib.ptr(agents_d), _lib.ptr(self.envs_d), _lib.ptr(self.robots_d),
+                                               _lib.ptr(self.paths_d), _lib.ptr(self.overhead), _lib.ptr(out['overhead']),
+                                               _lib.ptr(out.get('robot')), _lib.ptr(out.get('history')),
+                                               _lib.ptr(out.get('intention')), _lib.stream_handle(s)))
+        hold(s, cur, agents_d, self.envs_d, self.robots_d, self.paths_d, self.overhead, *out.values())
+        return out
+
+    def shortest_path_images(self, positions, slots=None):
+        """OccupancyMap.shortest_path_image(position) (envs.py:2514-2517) of each agent's own map:
+        positions [n, 2] (x, y) -> [n, H, W] float32 device tensor of distances / 96 (-1 / 96 where
+        unreachable): simaps_build_cspace + simaps_snap_sources + simaps_sssp_grid, three launches."""
+        sl = list(range(self.N)) if slots is None else [int(k) for k in slots]
+        n = len(sl)
+        cs, _ = self.build_cspace(slots=slots, thin=False)
+        px = np.array([K.position_to_pixel_indices(float(x), float(y), (self.H, self.W)) for x, y in np.asarray(positions)[:, :2]],
+                      dtype=np.int32).reshape(n, 1, 2)
+        src = self.snap_pixels(px, slots=slots)[:, 0, :]
+        i0, j0, h, w = self.cfg.room_i0, self.cfg.room_j0, self.cfg.room_h, self.cfg.room_w
+        img = sssp_grid(cs, src, window=(i0, j0, h, w))
+        return img / np.float32(K.LOCAL_MAP_PIXELS_PER_METER)
+
     def shortest_paths(self, sources, targets, slots=None, max_points=64, stream=None):
         """OccupancyMap.shortest_path(source, target) (envs.py:2478-2505) on each agent's own map:
         sources / targets [n, 2] fp64 (x, y) for map slots `slots` (all agents if None) -> list of n

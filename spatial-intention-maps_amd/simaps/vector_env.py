@@ -88,13 +88,18 @@ class VectorEnvObservations:
                           seg_ids=seg_ids, stream=stream)
 
     # -- VectorEnv.get_state ---------------------------------------------------------------------
-    def get_state(self, all_robots=False, awaiting=None, save_figures=False, numpy=False, stream=None):
+    def get_state(self, all_robots=False, awaiting=None, save_figures=False, numpy=False, stream=None,
+                  figures_dir='figures'):
         """[env][group][robot] -> (96, 96, C) float32 state, or None for robots not awaiting a new
         action (envs.py:322-323).  awaiting: per env, per robot truthy flags
         (robot.awaiting_new_action); None means every robot.  numpy=True returns host NumPy arrays
-        like the reference (one device->host copy for the whole batch); otherwise device tensors."""
+        like the reference (one device->host copy for the whole batch); otherwise device tensors.
+        save_figures=True also writes, for every robot returned, Mapper.get_state's map PNGs
+        (envs.py:2115-2182) into figures_dir/robot_id_<id>/ (<id>: the scene robot's 'id' if it has
+        one -- the reference's pybullet body id --, else <env>_<robot>), from device-exported global
+        maps (simaps.figures; env.png and the occupancy figure are not written)."""
         if save_figures:
-            raise NotImplementedError('save_figures is a host-side matplotlib debug path (out of scope)')
+            return self._get_state_with_figures(all_robots, awaiting, numpy, stream, figures_dir)
         if (all_robots or awaiting is None) and self._ring and not numpy:
             k = self._ring_k
             self._ring_k = (k + 1) % len(self._ring)
@@ -149,6 +154,27 @@ class VectorEnvObservations:
                         for g in self.groups[e]])
         return res
 
+
+    def _get_state_with_figures(self, all_robots, awaiting, numpy, stream, figures_dir):
+        import os
+        from . import figures
+        states = self.get_state(all_robots, awaiting, numpy=numpy, stream=stream)
+        if stream is not None:
+            torch.cuda.current_stream(self.batch.device).wait_stream(stream)
+        todo = [(e, a, st) for e, env in enumerate(states) for grp, g in zip(env, self.groups[e])
+                for a, st in zip(g, grp) if st is not None]
+        if not todo:
+            return states
+        slots = [self.slot[(e, a)] for e, a, _ in todo]
+        pos = [self.batch.scenes[e]['robots'][a]['position'][:2] for e, a, _ in todo]
+        maps = figures.device_global_maps(self.batch, slots, pos)
+        _lib.check_faults()
+        for (e, a, st), gm in zip(todo, maps):
+            s = self.batch.scenes[e]
+            rid = s['robots'][a].get('id', '%d_%d' % (e, a))
+            figures.save_state_figures(os.path.join(figures_dir, 'robot_id_{}'.format(rid)), s['flags'], s['room_length'],
+                                       s['room_width'], len(s['robots']), st if numpy else st.cpu().numpy(), gm)
+        return states
 
     # -- reward lookups -----------------------------------------------------
     def distance_to_receptacle(self, positions, stream=None):

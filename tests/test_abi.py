@@ -24,7 +24,7 @@ def test_header_declares_the_abi():
                                          'simaps_get_state', 'simaps_sssp_grid',
                                          'simaps_grid_path', 'simaps_rec_cache_bytes', 'simaps_sp_lookup',
                                          'simaps_get_state_mixed', 'simaps_source_hash', 'simaps_occupancy_scatter',
-                                         'simaps_build_cspace', 'simaps_snap_sources'])
+                                         'simaps_build_cspace', 'simaps_snap_sources', 'simaps_global_maps'])
 
 
 def test_library_exports_every_declared_symbol():
@@ -227,3 +227,15 @@ def test_occupancy_map_host_side():
     assert L.simaps_snap_sources(c, 1, None, None, None, None, None, 0, None, None) == 0
     assert L.simaps_occupancy_scatter(c, 1, None, None, None, 5, 0.25, None, None) == _lib.EINVAL
     assert L.simaps_occupancy_scatter(c, 2, None, None, None, 0, 0.25, None, None) == 0
+
+
+def test_figure_channel_names_cover_the_state():
+    """simaps.figures names every state channel in envs.py:2071-2113 order: as many names as
+    simaps_num_channels gives channels, for every synthetic configuration."""
+    from simaps import figures, synthetic
+    for name, cfg in synthetic.CONFIGS.items():
+        flags = synthetic.config_flags(name)
+        nr = sum(sum(g.values()) for g in cfg['robot_config'])
+        assert len(figures.channel_names(flags, nr)) == synthetic.num_channels(flags, nr), name
+    img = np.array([[0.0, 0.5, 1.0, 1.33]], dtype=np.float32)
+    assert figures.to_uint8_image(img).tolist() == [[0, 128, 255, 83]]  # (utils.to_uint8_image's uint8 wrap)
