@@ -12,7 +12,7 @@ entry time.  It also evaluates the two levers of the verdict:
   (b) no tail beyond the p90 workgroup (the best any per-agent rebalancing could reach),
 as predicted launch times, so that an A/B is run only where the model shows >= 3 %.
 
-    python tools/tail_model.py profiles/r5b_stamps.npy [--kernel-us 32.3]
+    python tools/tail_model.py profiles/archive/r5b_stamps.npy [--kernel-us 32.3]
 """
 import argparse
 import json
