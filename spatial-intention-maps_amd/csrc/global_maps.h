@@ -84,7 +84,10 @@ __global__ void __launch_bounds__(NT) global_maps_kernel(simaps_config cfg, Geom
         unsigned *ou = reinterpret_cast<unsigned *>(out + base);
         for (int p = tid; p < H * W; p += NT) ou[p] = 0u;
         if (tid < nr) seg_table(sh, cfg, rb, paths, enc, tid, sh.me);
-        __syncthreads();  // (the zeros, device-coherent atomics below; the segment table)
+        // the zeros must be in L2 before any wave's atomicMax on them: a workgroup-scope barrier waits
+        // for LDS only (s_waitcnt lgkmcnt), so an agent-scope fence drains this wave's stores first
+        __threadfence();
+        __syncthreads();  // (the zeros; the segment table)
         auto put = [&](int a, int b, float v) {  // max into (a, b) and, thick, its cross (grey dilation, disk(1))
             const unsigned u = __float_as_uint(v);  // v > 0: the uint order is the float order
             if ((unsigned)a < (unsigned)H && (unsigned)b < (unsigned)W) atomicMax(&ou[a * W + b], u);

@@ -505,23 +505,31 @@ class StateBatch(_ArrayUpload):
 
 
     # -- OccupancyMap (envs.py:2409-2524) outputs (round 6) ---------------------------------------------
-    def scatter_obstacles(self, points, seg, obstacle_seg_value, slots=None, stream=None):
+    def scatter_obstacles(self, points, seg, obstacle_seg_value, slots=None, stream=None, out=None):
         """OccupancyMap.update's obstacle scatter (envs.py:2445-2450) into the occupancy maps of map slots
         `slots` (all if None): points [n, P, 3] float32 (x, y, z), seg [n, P] float32 -- every point with
-        np.isclose(seg, obstacle_seg_value) marks its pixel occupied.  One launch (simaps_occupancy_scatter)."""
+        np.isclose(seg, obstacle_seg_value) marks its pixel occupied.  One launch (simaps_occupancy_scatter).
+        out: another [num_map_slots, H, W] uint8 device tensor to mark instead of the occupancy maps (the
+        show_map free-space map, OccupancyMap.update 2462-2465)."""
         agents_d, n = (self.agents_d, self.N) if slots is None else self.subset_descriptor(slots)
         pts = torch.as_tensor(points, dtype=torch.float32).to(self.device).reshape(n, -1, 3).contiguous()
         sg = torch.as_tensor(seg, dtype=torch.float32).to(self.device).reshape(n, -1).contiguous()
         if sg.shape[1] != pts.shape[1]:
             raise ValueError('points [n, P, 3] and seg [n, P] must have the same P')
+        if out is None:
+            out = self.occupancy
+        elif (out.dtype != torch.uint8 or tuple(out.shape) != tuple(self.occupancy.shape) or not out.is_contiguous()
+              or out.device != self.occupancy.device):
+            raise ValueError('out must be a contiguous uint8 %s tensor on %s' % (tuple(self.occupancy.shape), self.device))
         if n == 0 or pts.shape[1] == 0:
             return
-        self._map_ver[slice(None) if slots is None else np.asarray(list(slots), dtype=np.int64)] += 1
+        if out is self.occupancy:
+            self._map_ver[slice(None) if slots is None else np.asarray(list(slots), dtype=np.int64)] += 1
         s, cur = launch_stream(self.device, stream)
         _lib.check(_lib.lib.simaps_occupancy_scatter(self.cfg, n, _lib.ptr(agents_d), _lib.ptr(pts), _lib.ptr(sg),
-                                                     pts.shape[1], float(obstacle_seg_value), _lib.ptr(self.occupancy),
+                                                     pts.shape[1], float(obstacle_seg_value), _lib.ptr(out),
                                                      _lib.stream_handle(s)))
-        hold(s, cur, agents_d, pts, sg, self.occupancy)
+        hold(s, cur, agents_d, pts, sg, out)
 
     def build_cspace(self, slots=None, cspace=True, thin=True, stream=None):
         """OccupancyMap.configuration_space / cspace_thin (envs.py:2453, 2456) of map slots `slots` (all

@@ -5,9 +5,9 @@ the global and local overhead maps, and for every map channel its global and loc
 the overhead map through the jet colormap (utils.JET / to_uint8_image / enlarge_image, utils.py:95-98,
 153-154), plus the intention channels.  Here the maps come from the device: the local maps are the
 rendered state's channels, the global ones simaps_global_maps / StateBatch.shortest_path_images.  Not
-written: env.png (a pybullet camera render; there is no simulator here) and global-occupancy-map.png
-(OccupancyMap.save_figure needs the reference's matplotlib show_map window).  PIL and matplotlib are
-needed only by this debug path, as in the reference.
+written: env.png (a pybullet camera render; there is no simulator here).  global-occupancy-map.png is
+OccupancyMap.save_figure (vector_env.OccupancyMap with show_map=True, passed to get_state).  PIL and
+matplotlib are needed only by this debug path, as in the reference.
 """
 from pathlib import Path
 

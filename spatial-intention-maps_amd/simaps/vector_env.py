@@ -89,7 +89,7 @@ class VectorEnvObservations:
 
     # -- VectorEnv.get_state ---------------------------------------------------------------------
     def get_state(self, all_robots=False, awaiting=None, save_figures=False, numpy=False, stream=None,
-                  figures_dir='figures'):
+                  figures_dir='figures', occupancy_maps=None):
         """[env][group][robot] -> (96, 96, C) float32 state, or None for robots not awaiting a new
         action (envs.py:322-323).  awaiting: per env, per robot truthy flags
         (robot.awaiting_new_action); None means every robot.  numpy=True returns host NumPy arrays
@@ -97,9 +97,11 @@ class VectorEnvObservations:
         save_figures=True also writes, for every robot returned, Mapper.get_state's map PNGs
         (envs.py:2115-2182) into figures_dir/robot_id_<id>/ (<id>: the scene robot's 'id' if it has
         one -- the reference's pybullet body id --, else <env>_<robot>), from device-exported global
-        maps (simaps.figures; env.png and the occupancy figure are not written)."""
+        maps (simaps.figures; env.png, the simulator's camera image, is not written).  occupancy_maps:
+        {(env, robot): OccupancyMap(show_map=True)}, the env.show_occupancy_maps case (envs.py:2180-2182):
+        each figured robot's map figure is saved there as global-occupancy-map.png."""
         if save_figures:
-            return self._get_state_with_figures(all_robots, awaiting, numpy, stream, figures_dir)
+            return self._get_state_with_figures(all_robots, awaiting, numpy, stream, figures_dir, occupancy_maps)
         if (all_robots or awaiting is None) and self._ring and not numpy:
             k = self._ring_k
             self._ring_k = (k + 1) % len(self._ring)
@@ -155,7 +157,7 @@ class VectorEnvObservations:
         return res
 
 
-    def _get_state_with_figures(self, all_robots, awaiting, numpy, stream, figures_dir):
+    def _get_state_with_figures(self, all_robots, awaiting, numpy, stream, figures_dir, occupancy_maps):
         import os
         from . import figures
         states = self.get_state(all_robots, awaiting, numpy=numpy, stream=stream)
@@ -172,8 +174,11 @@ class VectorEnvObservations:
         for (e, a, st), gm in zip(todo, maps):
             s = self.batch.scenes[e]
             rid = s['robots'][a].get('id', '%d_%d' % (e, a))
-            figures.save_state_figures(os.path.join(figures_dir, 'robot_id_{}'.format(rid)), s['flags'], s['room_length'],
-                                       s['room_width'], len(s['robots']), st if numpy else st.cpu().numpy(), gm)
+            out = os.path.join(figures_dir, 'robot_id_{}'.format(rid))
+            figures.save_state_figures(out, s['flags'], s['room_length'], s['room_width'], len(s['robots']),
+                                       st if numpy else st.cpu().numpy(), gm)
+            if occupancy_maps and (e, a) in occupancy_maps:
+                occupancy_maps[(e, a)].save_figure(os.path.join(out, 'global-occupancy-map.png'))
         return states
 
     # -- reward lookups -----------------------------------------------------
@@ -326,15 +331,15 @@ class OccupancyMap:
     `robot`: a reference Robot object or a type name ('lifting_robot', ...).  The NumPy views
     (occupancy_map, configuration_space, cspace_thin, closest_cspace_indices) are copies made on
     access; closest_cspace_indices (the whole [2, H, W] table) is computed on first access after an
-    update."""
+    update.  show_map=True keeps the reference's map figure (envs.py:2434-2443, 2529-2555) for
+    save_figure: the free-space map is marked on the device by the same scatter kernel, the figure is a
+    headless matplotlib Figure (no window, no plt.pause)."""
 
     def __init__(self, robot, room_length, room_width, show_map=False, device='cuda'):
-        if show_map:
-            raise NotImplementedError('show_map is the reference\'s matplotlib window (out of scope)')
         from . import constants as K
         self.robot = robot
         self.room_length, self.room_width = room_length, room_width
-        self.show_map = False
+        self.show_map = bool(show_map)
         typ = _robot_type(robot)
         H, W = K.padded_room_shape(room_width, room_length)
         rob = {'type': typ, 'cls': K.ROBOT_TYPES.index(typ), 'group_index': 0, 'position': (0.0, 0.0, 0.0),
@@ -347,6 +352,13 @@ class OccupancyMap:
         self._b = _batch.StateBatch([scene], device=device)
         self._cspace = self._thin = self._closest = None
         self.grid_graph = None
+        if self.show_map:  # envs.py:2434-2443
+            from matplotlib.figure import Figure
+            self.fig_width = room_length + 2 * K.HALF_WIDTH
+            self.fig_height = room_width + 2 * K.HALF_WIDTH
+            self.fig = Figure(figsize=(4 * self.fig_width, 4 * self.fig_height))
+            self._free = torch.zeros_like(self._b.occupancy)
+            self._update_map_visualization()
 
     # -- the reference's attributes, as host copies ------------------------------------------------------
     @property
@@ -388,6 +400,40 @@ class OccupancyMap:
         sg = np.asarray(seg, dtype=np.float32).reshape(1, -1)
         self._b.scatter_obstacles(pts, sg, obstacle_seg_value)
         self._derive()
+        if self.show_map:  # envs.py:2462-2466: the points that are not obstacles mark the free-space map
+            v = float(obstacle_seg_value)
+            d = torch.as_tensor(sg, device=self._b.device).double()
+            close = (d - v).abs() <= 1e-8 + 1e-5 * abs(v)  # np.isclose in float64; NaN is never close
+            self._b.scatter_obstacles(pts, (~close).float(), 1.0, out=self._free)
+            self._update_map_visualization()
+
+    @property
+    def free_space_map(self):
+        """show_map only: uint8 [H, W], 1 where a non-obstacle point was seen (envs.py:2442, 2463-2465)."""
+        return self._free[0].cpu().numpy() if self.show_map else None
+
+    def _update_map_visualization(self):
+        """envs.py:2529-2555, drawn into the headless figure."""
+        from . import constants as K
+        occ = self.occupancy_map
+        vis = np.zeros(occ.shape) + 0.5
+        vis[self.free_space_map == 1] = 1
+        vis[occ == 1] = 0
+        self.fig.clf()
+        self.fig.add_axes((0, 0, 1, 1))
+        ax = self.fig.gca()
+        ax.axis('off')
+        ax.axis([-self.fig_width / 2, self.fig_width / 2, -self.fig_height / 2, self.fig_height / 2])
+        height, width = vis.shape
+        height, width = height / K.LOCAL_MAP_PIXELS_PER_METER, width / K.LOCAL_MAP_PIXELS_PER_METER
+        ax.imshow(255.0 * vis, extent=(-width / 2, width / 2, -height / 2, height / 2), cmap='gray', vmin=0, vmax=255.0)
+        wp = getattr(self.robot, 'waypoint_positions', None)
+        if wp is not None:
+            wp = np.array(wp)
+            ax.plot(wp[:, 0], wp[:, 1], color='r', marker='.')
+        ee = getattr(self.robot, 'target_end_effector_position', None)
+        if ee is not None:
+            ax.plot(ee[0], ee[1], color='r', marker='x')
 
     def _derive(self):
         cs, th = self._b.build_cspace()
@@ -434,7 +480,9 @@ class OccupancyMap:
         return self.grid_graph.shortest_path_image((int(i), int(j))) / np.float32(96)
 
     def save_figure(self, output_path):
-        raise NotImplementedError('save_figure needs show_map (the reference\'s matplotlib window, out of scope)')
+        """envs.py:2519-2521: the map figure of the last update, as the reference saves it."""
+        assert self.show_map
+        self.fig.savefig(output_path, bbox_inches='tight', pad_inches=0)
 
 
 __all__ = ['VectorEnvObservations', 'GridGraph', 'OccupancyMap', 'robot_groups', 'window_fits']

@@ -201,15 +201,15 @@ def test_stale_library_is_refused(tmp_path):
 
 def test_occupancy_map_host_side():
     """The OccupancyMap drop-in: no CPU path (the grid and every derived map live on the device),
-    show_map / save_figure (matplotlib windows) refused; the host pixel-index helper equals the
+    an unknown robot type refused; the host pixel-index helper equals the
     oracle's Mapper.position_to_pixel_indices (envs.py:2391-2397) on random and pixel-edge positions;
     the three OccupancyMap entries refuse bad arguments before any launch."""
     import oracle as O
     from simaps import _lib, batch, constants as K, synthetic, vector_env
     with pytest.raises(ValueError):
         vector_env.OccupancyMap('lifting_robot', 1.0, 0.5, device='cpu')
-    with pytest.raises(NotImplementedError):
-        vector_env.OccupancyMap('lifting_robot', 1.0, 0.5, show_map=True)
+    with pytest.raises(ValueError):
+        vector_env.OccupancyMap('lifting_robot', 1.0, 0.5, show_map=True, device='cpu')
     with pytest.raises(ValueError):
         vector_env.OccupancyMap('flying_robot', 1.0, 0.5)
     rs = np.random.RandomState(3)

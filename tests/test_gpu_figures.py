@@ -91,3 +91,21 @@ def test_save_figures_pngs_match_the_oracle(M, cfg, tmp_path):
             assert np.array_equal(st[e][grp][obs.groups[e][grp].index(a)].view(np.int32),
                                   O.agent_state(s, a).view(np.int32))
     assert n >= 20
+
+
+def test_save_figures_writes_the_occupancy_figure(M, tmp_path):
+    """env.show_occupancy_maps (envs.py:2180-2182): the OccupancyMap passed for a figured robot saves its
+    figure as global-occupancy-map.png next to the map PNGs; robots without one get none."""
+    _lib, batch, figures, vector_env = M
+    from simaps import synthetic
+    s = synthetic.make_scene('lifting_4-small_divider', 410)
+    obs = vector_env.VectorEnvObservations([s])
+    om = vector_env.OccupancyMap(s['robots'][1]['type'], s['room_length'], s['room_width'], show_map=True)
+    om.occupancy_map = s['occupancy'][1]
+    om._update_map_visualization()
+    obs.get_state(save_figures=True, numpy=True, figures_dir=str(tmp_path), occupancy_maps={(0, 1): om})
+    om.save_figure(tmp_path / 'want.png')
+    got = tmp_path / 'robot_id_0_1' / 'global-occupancy-map.png'
+    assert np.array_equal(_png_pixels(got), _png_pixels(tmp_path / 'want.png'))
+    assert not (tmp_path / 'robot_id_0_0' / 'global-occupancy-map.png').exists()
+    assert (tmp_path / 'robot_id_0_0' / 'global-overhead-map.png').exists()

@@ -134,3 +134,73 @@ def test_occupancy_map_paths_and_distances_vs_reference(M):
             m += 1
     assert m >= 40
     _lib.check_faults()
+
+
+class LiftingRobot:  # a stand-in of the reference's class (simaps.reference_adapter matches by class name)
+    waypoint_positions = [(0.1, -0.05, 0.0), (0.2, 0.1, 0.0), (0.35, 0.12, 0.0)]
+    target_end_effector_position = (0.36, 0.14, 0.0)
+
+
+def _reference_figure(occ, free, fig_w, fig_h, robot, path):
+    """OccupancyMap._update_map_visualization + save_figure (envs.py:2529-2555, 2519-2521), restated
+    on a pyplot figure (Agg) from the maps the test expects."""
+    import matplotlib
+    matplotlib.use('Agg')
+    import matplotlib.pyplot as plt
+    fig = plt.figure(figsize=(4 * fig_w, 4 * fig_h))
+    vis = np.zeros(occ.shape) + 0.5
+    vis[free == 1] = 1
+    vis[occ == 1] = 0
+    fig.clf()
+    fig.add_axes((0, 0, 1, 1))
+    ax = fig.gca()
+    ax.axis('off')
+    ax.axis([-fig_w / 2, fig_w / 2, -fig_h / 2, fig_h / 2])
+    h, w = vis.shape[0] / 96.0, vis.shape[1] / 96.0
+    ax.imshow(255.0 * vis, extent=(-w / 2, w / 2, -h / 2, h / 2), cmap='gray', vmin=0, vmax=255.0)
+    wp = np.array(robot.waypoint_positions)
+    ax.plot(wp[:, 0], wp[:, 1], color='r', marker='.')
+    ax.plot(robot.target_end_effector_position[0], robot.target_end_effector_position[1], color='r', marker='x')
+    fig.savefig(path, bbox_inches='tight', pad_inches=0)
+    plt.close(fig)
+
+
+def test_occupancy_map_show_map_figure(M, tmp_path):
+    """show_map=True: the free-space map (envs.py:2462-2465: every point whose seg is not np.isclose to
+    the obstacle value, NaN included) equals the host rule's, over two updates; save_figure's PNG equals
+    the reference's drawing steps on the expected maps, pixel for pixel."""
+    from PIL import Image
+    _lib, batch, K, synthetic, vector_env = M
+    cfg, e, a, scene, pre, z = CASES[0]
+    robot = LiftingRobot()
+    om = vector_env.OccupancyMap(robot, scene['room_length'], scene['room_width'], show_map=True)
+    assert not om.free_space_map.any()
+    pts, seg = _cloud(scene, a, synthetic, K)
+    rs = np.random.RandomState(7)
+    # a sparse first frame: a third of the points, some segs NaN or a hair off the obstacle value
+    keep = rs.rand(*seg.shape) < 0.35
+    seg1 = np.where(keep, seg, np.float32(K.SEG_VALUES['floor'])).astype(np.float32)
+    seg1[rs.rand(*seg.shape) < 0.01] = np.nan
+    ob = np.float32(K.SEG_VALUES['obstacle'])
+    seg1[rs.rand(*seg.shape) < 0.01] = ob * np.float32(1 + 4e-6)
+    pts1 = np.where(keep[..., None], pts, np.float32(9.0))  # dropped points land clipped at the border
+    free = np.zeros((scene['H'], scene['W']), np.uint8)
+    occ = np.zeros_like(free)
+    for p, s in ((pts1, seg1), (pts, seg)):
+        om.update(p, s, K.SEG_VALUES['obstacle'])
+        close = np.isclose(s, K.SEG_VALUES['obstacle']).reshape(-1)
+        px, py = p.reshape(-1, 3)[:, 0], p.reshape(-1, 3)[:, 1]  # position_to_pixel_indices on float32
+        pi = np.clip(np.floor(free.shape[0] / 2 - py * 96.0).astype(np.int32), 0, free.shape[0] - 1)
+        pj = np.clip(np.floor(free.shape[1] / 2 + px * 96.0).astype(np.int32), 0, free.shape[1] - 1)
+        free[pi[~close], pj[~close]] = 1
+        occ[pi[close], pj[close]] = 1
+        assert np.array_equal(om.free_space_map, free)
+        assert np.array_equal(om.occupancy_map, occ)
+    assert occ.sum() > 100 and free.sum() > 1000
+    om.save_figure(tmp_path / 'global-occupancy-map.png')
+    _reference_figure(occ, free, om.fig_width, om.fig_height, robot, tmp_path / 'want.png')
+    got = np.asarray(Image.open(tmp_path / 'global-occupancy-map.png'))
+    want = np.asarray(Image.open(tmp_path / 'want.png'))
+    assert got.shape == want.shape and got.shape[0] > 100
+    assert np.array_equal(got, want)
+    _lib.check_faults()
