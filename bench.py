@@ -86,14 +86,18 @@ def rank_envs(rank, envs_per_rank, world=1, total_envs=None):
     return list(range(lo, lo + q + (1 if rank < r else 0)))
 
 
+START_MARGIN_S = 200e-6  # the agreed start's lead over the latest rank's clock (covers the reduction's return skew)
+
+
 def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu', own=None):
     """The bench contract's timed region: `warmup` untimed steps, then barrier + sync, EXACTLY
     `steps` steps, sync + barrier; returns the job's wall time (every rank gets it).  step(k) runs
     step k (k < 0 for warmup); sync() waits for the device.  The job's time runs from the EARLIEST
-    rank's start (its exit from the opening barrier) to the LATEST rank's end (its sync after its K
+    rank's start (after the opening barrier) to the LATEST rank's end (its sync after its K
     steps): one max-reduction of (-start, end) over the ranks' CLOCK_MONOTONIC stamps
-    (time.perf_counter, one clock for every process of the node), so skew between ranks leaving the
-    opening barrier is counted.  The closing barrier itself is not: an RCCL barrier costs ~0.1 ms,
+    (time.perf_counter, one clock for every process of the node), so skew between ranks' starts is
+    counted.  After the barrier the ranks wait for one agreed start instant, so that skew is the
+    clock's, not the barrier's exit.  The closing barrier itself is not: an RCCL barrier costs ~0.1 ms,
     ~15 % of a 20-step region, and is no part of the K steps."""
     import torch
     import torch.distributed as dist
@@ -103,6 +107,13 @@ def timed_steps(step, steps, warmup, sync, world, reduce_device='cpu', own=None)
     sync()
     if coll:
         dist.barrier()
+        # a common start: the ranks leave the barrier up to tens of microseconds apart (host wake-up),
+        # so they agree on a start instant on the node's shared CLOCK_MONOTONIC (the latest rank's
+        # clock after the barrier + START_MARGIN_S) and each waits for it; a rank that still starts
+        # late is counted by the (-start, end) reduction below
+        tc = max_over_ranks([time.perf_counter()], world, reduce_device)[0] + START_MARGIN_S
+        while time.perf_counter() < tc:
+            pass
     sync()
     t0 = time.perf_counter()
     for k in range(steps):
