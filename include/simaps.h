@@ -296,7 +296,7 @@ int simaps_shortest_path(const simaps_config *cfg, int N, const simaps_agent *ag
  * 0 automatic: 3 while the whole launch is resident at once at mode 3's residency (N <= CUs x 2
  * small-room / x 1 large-room queries), else 2.  Modes 0-3 return the reference's waypoints
  * exactly.  (Round 6 measured an opt-in parent rule on the SSSP fixpoint instead of the SPFA:
- * 5-7x faster, but 88.7 % of fuzz paths within demo.py's atol=2 against a 99.9 % bar -- not kept,
+ * 3-13x faster, but 88.7 % of fuzz paths within demo.py's atol=2 against a 99.9 % bar -- not kept,
  * DESIGN.md section 9.) */
 int simaps_path_mode(int mode);
 
