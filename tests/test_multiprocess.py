@@ -262,3 +262,32 @@ def test_bench_main_world4_strong_split(config, total):
     agents = res['config']['agents_per_env']
     assert res['config']['stacks_per_step'] == total * agents
     assert [row['stacks_per_step'] for row in d['ranks']] == [n * agents for n in sizes]
+
+
+@pytest.mark.timeout(300)
+def test_bench_main_driver_launch_world8():
+    """The driver's scaling form at N = 8, verbatim but for the CPU stand-in: `python -m
+    torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port P
+    bench.py --gpus 8 --steps K --warmup W` (launcher 'external', gloo).  Exactly one JSON line
+    (rank 0's), n_gpus == world_size == 8, the default weak split of 64 envs per rank in rank order,
+    and value = all ranks' stacks x K / the job time."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT')}
+    env['OMP_NUM_THREADS'] = '1'
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '8', '--master-addr',
+           '127.0.0.1', '--master-port', str(_free_port()), os.path.join(ROOT, 'bench.py'), '--gpus', '8', '--steps',
+           '2', '--warmup', '1', '--envs', '2', '--standin']
+    p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, p.stdout
+    res = lines[0]
+    d = res['distributed']
+    assert res['n_gpus'] == 8 and d['world_size'] == 8 and d['launcher'] == 'external' and d['backend'] == 'gloo'
+    assert res['scaling'] == 'weak' and res['steps'] == 2 and res['warmup'] == 1
+    assert [row['rank'] for row in d['ranks']] == list(range(8))
+    assert [row['env_range'] for row in d['ranks']] == [[2 * r, 2 * r + 1] for r in range(8)]
+    assert res['config']['stacks_per_step'] == 8 * 2 * res['config']['agents_per_env']
+    slowest = max(row['seconds'] for row in d['ranks'])
+    assert res['value'] <= res['config']['stacks_per_step'] * res['steps'] / slowest * (1 + 1e-9)
