@@ -187,6 +187,300 @@ __global__ void __launch_bounds__(GL_NT) gl_sssp_kernel(int H, int W, const uint
     }
 }
 
+// ---- the tiled fixpoint (round 6) ----------------------------------------------------------------
+// gl_sssp_kernel's four waves sweep the WHOLE window every round (a 500 x 500 window: ~20 rounds of
+// 4 x 250 k cell-steps from global memory, 7 ms).  gl_tile_kernel does the same fixpoint with work
+// only where values still fall: the padded array stays in global memory (L2), cut into GT_TT x GT_TT
+// tiles; four groups of four waves take dirty tiles from an LDS queue.  A group loads its tile with a
+// one-cell halo into LDS, relaxes the tile's edge cells from the halo (which it only reads), sweeps
+// the interior down / up / right / left (sweep_t, one wave per direction) until a round changes
+// nothing, writes back the cells that fell and marks the neighbour tiles whose halo they are.  Every
+// value written is some path's left-fold float32 length (a stale halo value included), so the
+// unique fixpoint -- the reference SPFA's distances (pyx:69-114), bit for bit -- is reached when the
+// queue is empty and no group is busy: every edge inside a tile was relaxed by its last processing,
+// every edge into it from a halo cell after that cell's last change (which marked the tile).  A
+// tile is never processed by two groups at once (a mark that finds it busy asks its group to run it
+// again), so write-back is a plain store.  Host model, bitwise against the oracle with tile counts:
+// tools/tile_sssp_model.py (~2.3 processings per tile, ~2.2 sweep rounds per processing on 500^2).
+constexpr int GT_TT = 62;                       // tile interior side: one cell per lane (span <= 63)
+constexpr int GT_TP = 65;                       // LDS pitch of a tile buffer (odd: column sweeps spread over banks)
+constexpr int GT_PAD = 8;                       // rows of slack around a buffer: sweep_t's prefetch reads <= 6 lines
+constexpr int GT_BUF = (GT_TT + 2 + 2 * GT_PAD) * GT_TP;  // floats per group buffer  //  past either end
+constexpr int GT_GROUPS = 4;
+constexpr int GT_NT = 256 * GT_GROUPS;
+constexpr int GT_MAXT = 4096;                   // tiles per window (larger windows: gl_sssp_kernel)
+constexpr unsigned GT_Q = 1, GT_BUSY = 2, GT_AGAIN = 4;  // tile states (one byte per tile)
+constexpr unsigned GT_EMPTY = 0xffffffffu;      // a free ring slot
+struct GtShared {
+    unsigned bar[GT_GROUPS][4];                 // the groups' LDS barriers (Group)
+    unsigned st[GT_MAXT / 4];                   // tile state bytes
+    unsigned ring[GT_MAXT];                     // queue of dirty tiles (each at most once)
+    unsigned head, tail, outstanding, processed, abort;
+    int gtile[GT_GROUPS];                       // the tile a group works on next (-1: done)
+    unsigned chg[GT_GROUPS][3];                 // per group, per round: a sweep lowered a cell
+    unsigned emask[GT_GROUPS];                  // per group: which edges / corners of its tile fell
+};
+__host__ __device__ constexpr int gt_tiles(int wh, int ww) { return ((wh + GT_TT - 1) / GT_TT) * ((ww + GT_TT - 1) / GT_TT); }
+
+__device__ __forceinline__ unsigned gt_lds_ld(const unsigned *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+// a tile's state byte: CAS on its word; f(old byte) -> new byte, or -1 to leave it.  Returns the old byte.
+template <class F>
+__device__ __forceinline__ unsigned gt_state(GtShared &sh, int t, F f)
+{
+    unsigned *w = &sh.st[t >> 2];
+    const int s8 = (t & 3) * 8;
+    unsigned old = gt_lds_ld(w);
+    for (;;) {
+        const unsigned s = (old >> s8) & 0xffu;
+        const int ns = f(s);
+        if (ns < 0) return s;
+        const unsigned nw = (old & ~(0xffu << s8)) | ((unsigned)ns << s8);
+        const unsigned prev = atomicCAS(w, old, nw);
+        if (prev == old) return s;
+        old = prev;
+    }
+}
+
+// the tile's halo changed: queue it, or have its busy group run it again
+__device__ __forceinline__ void gt_mark(GtShared &sh, int t, int nt)
+{
+    const unsigned s = gt_state(sh, t, [](unsigned s) -> int {
+        if (s & GT_BUSY) return (s & GT_AGAIN) ? -1 : (int)(s | GT_AGAIN);
+        return (s & GT_Q) ? -1 : (int)(s | GT_Q);
+    });
+    if ((s & (GT_BUSY | GT_Q)) == 0) {  // this call queued it
+        atomicAdd(&sh.outstanding, 1u);
+        const unsigned k = atomicAdd(&sh.tail, 1u) % (unsigned)nt;
+        unsigned spins = 0;  // (the slot's previous entry may still be being taken: live entries <= nt)
+        while (atomicCAS(&sh.ring[k], GT_EMPTY, (unsigned)t) != GT_EMPTY)
+            if (++spins > (1u << 22)) { __hip_atomic_store(&sh.abort, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); break; }
+    }
+}
+
+// next dirty tile (busy from now on), or -1 when the queue is empty and no group is busy (or on abort)
+__device__ __forceinline__ int gt_pop(GtShared &sh, int nt)
+{
+    unsigned spins = 0;
+    for (;;) {
+        if (gt_lds_ld(&sh.abort)) return -1;
+        const unsigned h = gt_lds_ld(&sh.head);
+        if (h != gt_lds_ld(&sh.tail)) {
+            if (atomicCAS(&sh.head, h, h + 1) != h) continue;
+            unsigned v;
+            while ((v = atomicExch(&sh.ring[h % (unsigned)nt], GT_EMPTY)) == GT_EMPTY)  // (its push is landing)
+                if (++spins > (1u << 22)) { __hip_atomic_store(&sh.abort, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); return -1; }
+            gt_state(sh, (int)v, [](unsigned s) -> int { return (int)((s & ~GT_Q) | GT_BUSY); });
+            return (int)v;
+        }
+        if (gt_lds_ld(&sh.outstanding) == 0) return -1;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) { __hip_atomic_store(&sh.abort, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); return -1; }
+    }
+}
+
+// the group finished tile t: true if it must run it again (marked while busy)
+__device__ __forceinline__ bool gt_finish(GtShared &sh, int t)
+{
+    const unsigned s = gt_state(sh, t, [](unsigned s) -> int { return (s & GT_AGAIN) ? (int)(s & ~GT_AGAIN) : (int)(s & ~GT_BUSY); });
+    if (s & GT_AGAIN) return true;
+    atomicSub(&sh.outstanding, 1u);
+    return false;
+}
+
+// one whole directional sweep of the tile's interior (sweep_t: the halo is not read; the edge cells
+// took it beforehand).  (The get_state kernels' inline-asm loop, sweep_asm, measured the same here:
+// 1.08 vs 1.05 ms per 500^2 image, profiles/r6r_large_*.jsonl.)
+template <int DIR>
+__device__ __forceinline__ bool gt_sweep(lds_float *L, int th, int tw)
+{
+    return DIR < 2 ? sweep_t<DIR, 1, GT_TP>(L, th, tw, GT_TP) : sweep_t<DIR, 1, GT_TP>(L, tw, th, GT_TP);
+}
+
+// One group's processing of tile (ti, tj): load with halo -> edge relaxation -> sweep rounds -> write-back.
+// Returns the edge mask (bits: top, bottom, left, right rows / columns; corners (1,1), (1,tw), (th,1),
+// (th,tw)) of the cells that fell, in the group's leader; every thread of the group calls it.
+__device__ __forceinline__ unsigned gt_process(GtShared &sh, lds_float *L, float *D, const GlDims g, int ti, int tj,
+                                               const Group &grp, int gi, int sr, int sc)
+{
+    const int t = grp.t, dir = t >> 6;
+    const int r0 = ti * GT_TT, c0 = tj * GT_TT;
+    const int th = min(GT_TT, g.wh - r0), tw = min(GT_TT, g.ww - c0);
+    // Padded rows r0 .. r0 + th + 1, columns c0 .. c0 + tw + 1 (the halo: the neighbours' edge cells or
+    // the -inf border): wave w of the group takes rows w, w + 4, .., lane = column.  All 16 loads of a
+    // lane go out together (addresses clamped into the tile, so none is masked); the values stay in
+    // registers for the write-back's comparison.
+    const int lane = t & 63, a0 = t >> 6;
+    const int lb = min(lane, tw + 1);
+    const float *src = D + (long)r0 * g.pitch + c0 + lb;
+    float old[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) old[j] = gl_ld(src + (long)min(a0 + 4 * j, th + 1) * g.pitch);
+    // The source (padded cell (sr, sc)) starts at +inf in D and takes its 0 here, inside its tile, so
+    // that it counts as a cell that fell: on a tile edge or corner it marks the tiles it is the halo of.
+    // (Written by the lane that stores that cell: a separate store raced with it -- r6u / r6v, an image
+    // left at -1.)
+    const bool s_here = sr > r0 && sr <= r0 + th && sc > c0 && sc <= c0 + tw;
+    const int sa = s_here ? sr - r0 : -1, sb = sc - c0;
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+        if (a0 + 4 * j <= th + 1 && lane <= tw + 1)
+            L[(a0 + 4 * j) * GT_TP + lane] = (a0 + 4 * j == sa && lane == sb) ? 0.0f : old[j];
+    grp.sync();
+    // edge cells from the halo (read-only): top / bottom rows from rows 0 / th + 1, left / right columns
+    // from columns 0 / tw + 1; straight weight 1, diagonals sqrt(2) (pyx:30-32); |-inf| = +inf passes nothing
+    for (int k = t; k < 2 * tw + 2 * th; k += grp.n) {
+        int a, b, ha, hb, da, db;  // the edge cell, its straight halo neighbour, the diagonal step along the edge
+        if (k < 2 * tw) { b = 1 + k % tw; a = k < tw ? 1 : th; ha = k < tw ? 0 : th + 1; hb = b; da = 0; db = 1; }
+        else { const int q = k - 2 * tw; a = 1 + q % th; b = q < th ? 1 : tw; hb = q < th ? 0 : tw + 1; ha = a; da = 1; db = 0; }
+        const float s0 = fabsf(L[ha * GT_TP + hb]) + 1.0f;
+        const float s1 = fabsf(L[(ha - da) * GT_TP + hb - db]) + SQRT2F;
+        const float s2 = fabsf(L[(ha + da) * GT_TP + hb + db]) + SQRT2F;
+        lds_min(L + a * GT_TP + b, fminf(fminf(s0, s1), s2));  // (blocked cells keep -inf)
+    }
+    grp.sync();
+    for (int round = 0;; round++) {
+        const bool c = dir == 0 ? gt_sweep<0>(L, th, tw) : dir == 1 ? gt_sweep<1>(L, th, tw)
+                     : dir == 2 ? gt_sweep<2>(L, th, tw) : gt_sweep<3>(L, th, tw);
+        if (c && (t & 63) == 0) __hip_atomic_store(&sh.chg[gi][round % 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (t == 0) __hip_atomic_store(&sh.chg[gi][(round + 1) % 3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // (read 2 syncs ago)
+        grp.sync();
+        if (!gt_lds_ld(&sh.chg[gi][round % 3]) || gt_lds_ld(&sh.abort) || gt_lds_ld(&sh.bar[gi][2])) break;
+        if (round > 4 * (GT_TT + 2) * (GT_TT + 2)) {  // (a bug guard: every round lowers a value)
+            if (t == 0) __hip_atomic_store(&sh.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            break;
+        }
+    }
+    // write-back of the interior cells that fell (this group is the tile's only writer, so D still
+    // holds what it loaded)
+    unsigned em = 0;
+    const int b = lane;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int a = a0 + 4 * j;
+        if (a >= 1 && a <= th && b >= 1 && b <= tw) {
+            const float v = L[a * GT_TP + b];
+            if (v < old[j]) {
+                D[(long)(r0 + a) * g.pitch + c0 + b] = v;  // (plain: see gl_tile_kernel's store rule)
+                em |= (a == 1 ? 1u : 0u) | (a == th ? 2u : 0u) | (b == 1 ? 4u : 0u) | (b == tw ? 8u : 0u) |
+                      (a == 1 && b == 1 ? 16u : 0u) | (a == 1 && b == tw ? 32u : 0u) | (a == th && b == 1 ? 64u : 0u) |
+                      (a == th && b == tw ? 128u : 0u);
+            }
+        }
+    }
+    if (em) atomicOr(&sh.emask[gi], em);
+    gl_drain();  // the stores are in L2 before any mark can send another group to read them
+    grp.sync();
+    return t == 0 ? gt_lds_ld(&sh.emask[gi]) : 0u;
+}
+
+// Batched GridGraph(grid).shortest_path_image(source) for windows of up to GT_MAXT tiles, one
+// 1024-thread workgroup per query: same arguments, results and scratch layout as gl_sssp_kernel.
+// Store rule: every store to D is a PLAIN store and every load of D an agent-scope (sc1, L1-bypassing)
+// load.  The workgroup's waves share one CU, so one XCD's L2, where plain stores land: a store drained
+// (vmcnt 0) before the mark that sends another group to the cells is seen by that group's loads, and
+// the kernel's end writes the lines back for gl_path_kernel.
+__global__ void __launch_bounds__(GT_NT) gl_tile_kernel(int H, int W, const uint8_t *__restrict__ grids, long grid_stride,
+                                                       const int32_t *__restrict__ sources, int wi0, int wj0, int wh, int ww,
+                                                       float *scratch, long scratch_stride, float *__restrict__ out,
+                                                       unsigned *fault)
+{
+    __shared__ GtShared sh;
+    __shared__ float tiles[GT_GROUPS * GT_BUF];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const uint8_t *grid = grids + b * grid_stride;
+    const GlDims g = gl_dims(wh, ww);
+    float *D = scratch + b * scratch_stride;
+    const int si = sources[2 * b], sj = sources[2 * b + 1];
+    const bool s_in = si >= wi0 && si < wi0 + wh && sj >= wj0 && sj < wj0 + ww && grid[(long)si * W + sj] != 0;
+    const int ntj = (ww + GT_TT - 1) / GT_TT, nt = gt_tiles(wh, ww);
+    // (rows by wave, columns by lane: no 64-bit index division)
+    for (int r = tid >> 6; r < wh + 2; r += GT_NT / 64) {
+        const uint8_t *grow = grid + (long)(wi0 + r - 1) * W + wj0 - 1;
+        float *drow = D + (long)r * g.pitch;
+        const bool in_r = r >= 1 && r <= wh;
+        for (int c = tid & 63; c < g.pitch; c += 64) {
+            float v = -INFINITY;
+            if (in_r && c >= 1 && c <= ww && grow[c] != 0) v = INFINITY;  // (the source too: gt_process sets it)
+            drow[c] = v;
+        }
+    }
+    for (int k = tid; k < nt; k += GT_NT) sh.ring[k] = GT_EMPTY;
+    for (int k = tid; k < (nt + 3) / 4; k += GT_NT) sh.st[k] = 0u;
+    if (tid < GT_GROUPS * 4) (&sh.bar[0][0])[tid] = 0u;
+    if (tid == 0) {
+        sh.head = sh.tail = sh.outstanding = sh.processed = sh.abort = 0u;
+        for (int q = 0; q < GT_GROUPS; q++) sh.emask[q] = 0u;
+    }
+    gl_drain();
+    __syncthreads();
+    if (tid == 0 && s_in) gt_mark(sh, ((si - wi0) / GT_TT) * ntj + (sj - wj0) / GT_TT, nt);
+    __syncthreads();
+    const int gi = tid >> 8;
+    const Group grp{tid & 255, 256, sh.bar[gi], 4};
+    lds_float *L = (lds_float *)(tiles + gi * GT_BUF + GT_PAD * GT_TP);  // (ds_* addressing)
+    const unsigned cap = 64u * (unsigned)nt + 4096u;  // processings (a bug guard: ~2-3 per tile measured)
+    bool again = false;
+    int cur = -1;
+    for (;;) {
+        if (grp.t == 0) {
+            if (!again) cur = gt_pop(sh, nt);
+            if (cur >= 0 && atomicAdd(&sh.processed, 1u) >= cap) {
+                __hip_atomic_store(&sh.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                cur = -1;
+            }
+            sh.gtile[gi] = cur;
+            sh.chg[gi][0] = sh.chg[gi][1] = sh.chg[gi][2] = 0u;
+            sh.emask[gi] = 0u;
+        }
+        grp.sync();
+        const int tile = __builtin_amdgcn_readfirstlane(sh.gtile[gi]);  // (wave-uniform)
+        if (tile < 0) break;
+        if (gt_lds_ld(&sh.bar[gi][2])) {  // (a bug guard: a group barrier timed out -- stop the query)
+            if (grp.t == 0) __hip_atomic_store(&sh.abort, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            break;
+        }
+        const int ti = tile / ntj, tj = tile - ti * ntj;
+        const unsigned em = gt_process(sh, L, D, g, ti, tj, grp, gi, si - wi0 + 1, sj - wj0 + 1);
+        if (grp.t == 0) {
+            const int nti = (wh + GT_TT - 1) / GT_TT;
+            const bool up = ti > 0, dn = ti + 1 < nti, lf = tj > 0, rt = tj + 1 < ntj;
+            if ((em & 1u) && up) gt_mark(sh, tile - ntj, nt);
+            if ((em & 2u) && dn) gt_mark(sh, tile + ntj, nt);
+            if ((em & 4u) && lf) gt_mark(sh, tile - 1, nt);
+            if ((em & 8u) && rt) gt_mark(sh, tile + 1, nt);
+            if ((em & 16u) && up && lf) gt_mark(sh, tile - ntj - 1, nt);
+            if ((em & 32u) && up && rt) gt_mark(sh, tile - ntj + 1, nt);
+            if ((em & 64u) && dn && lf) gt_mark(sh, tile + ntj - 1, nt);
+            if ((em & 128u) && dn && rt) gt_mark(sh, tile + ntj + 1, nt);
+            again = gt_finish(sh, tile);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned ab = sh.abort;
+        unsigned f = ab == 1u ? SIMAPS_FAULT_ROUNDS : ab ? SIMAPS_FAULT_TIMEOUT : 0u;
+        for (int q = 0; q < GT_GROUPS; q++)
+            if (sh.bar[q][2]) f |= SIMAPS_FAULT_TIMEOUT;
+        post_faults(fault, f);
+    }
+    if (!out) return;
+    for (int i = tid >> 6; i < H; i += GT_NT / 64) {
+        float *orow = out + (long)b * H * W + (long)i * W;
+        const int r = i - wi0;
+        const float *drow = D + (long)(r + 1) * g.pitch + 1 - wj0;
+        for (int j = tid & 63; j < W; j += 64) {
+            float v = (i == si && j == sj) ? 0.0f : -1.0f;
+            const int c = j - wj0;
+            if (r >= 0 && r < wh && c >= 0 && c < ww) {
+                const float d = gl_ld(drow + j);
+                if (d >= 0.0f && d != INFINITY) v = d;
+            }
+            orow[j] = v;
+        }
+    }
+}
+
 // Per-query scratch of gl_path_kernel, in int32 / float32 units of `cells` (padded cells) and `n`
 // (window cells + 1): fix [cells] (gl_sssp_kernel's fixpoint), dist [cells], pin [cells], queue [n]
 // (ring: live entries <= free cells), dense [n], chain [n], stack [2 n].

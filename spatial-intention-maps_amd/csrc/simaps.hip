@@ -4314,6 +4314,13 @@ bool window_fits_lds(int wh, int ww)
     return ww <= SIMAPS_MAX_ROOM_W && wh <= MAX_ROWS && (wh + 2) * ((ww + 2) | 1) <= SIMAPS_MAX_ROOM_CELLS;
 }
 
+// the large-window fixpoint: the tiled kernel up to GT_MAXT tiles (windows up to ~3,968^2 cells), the
+// whole-window sweeps beyond (SIMAPS_GL_TILE=0: always the sweeps, an A/B build for timing only)
+#ifndef SIMAPS_GL_TILE
+#define SIMAPS_GL_TILE 1
+#endif
+bool gl_tiled(int wh, int ww) { return SIMAPS_GL_TILE && (long)gt_tiles(wh, ww) <= GT_MAXT; }
+
 // scratch of the large-window GridGraph kernels (stream-ordered, the library's pool); they have no
 // other path, so a launch being captured into a graph is refused instead
 int large_scratch(PathScratch &ps, hipStream_t st, size_t bytes, const char *what)
@@ -4678,8 +4685,12 @@ int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *s
         const long words = gl_path_words(wh, ww);
         PathScratch ps;
         if (const int rc = large_scratch(ps, st, (size_t)B * words * sizeof(int), "grid_path")) return rc;
-        hipLaunchKernelGGL(gl_sssp_kernel, dim3(B), dim3(GL_NT), 0, st, H, W, grids, (long)H * W, sources, wi0, wj0, wh,
-                           ww, ps.p, words, nullptr, g_fault_dev);
+        if (gl_tiled(wh, ww))
+            hipLaunchKernelGGL(gl_tile_kernel, dim3(B), dim3(GT_NT), 0, st, H, W, grids, (long)H * W, sources, wi0, wj0, wh,
+                               ww, ps.p, words, nullptr, g_fault_dev);
+        else
+            hipLaunchKernelGGL(gl_sssp_kernel, dim3(B), dim3(GL_NT), 0, st, H, W, grids, (long)H * W, sources, wi0, wj0, wh,
+                               ww, ps.p, words, nullptr, g_fault_dev);
         hipLaunchKernelGGL(gl_path_kernel, dim3(B), dim3(64), 0, st, H, W, grids, (long)H * W, sources, targets, wi0, wj0,
                            wh, ww, reinterpret_cast<int *>(ps.p), words, max_points, out_ij, out_count, g_fault_dev);
         const hipError_t e = hipGetLastError();
@@ -4726,8 +4737,12 @@ int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *s
         const long cells = (long)(wh + 2) * (ww + 2);
         PathScratch ps;
         if (const int rc = large_scratch(ps, st, (size_t)B * cells * sizeof(float), "sssp_grid")) return rc;
-        hipLaunchKernelGGL(gl_sssp_kernel, dim3(B), dim3(GL_NT), 0, st, H, W, grids, (long)H * W, sources, wi0, wj0, wh,
-                           ww, ps.p, cells, dists, g_fault_dev);
+        if (gl_tiled(wh, ww))
+            hipLaunchKernelGGL(gl_tile_kernel, dim3(B), dim3(GT_NT), 0, st, H, W, grids, (long)H * W, sources, wi0, wj0, wh,
+                               ww, ps.p, cells, dists, g_fault_dev);
+        else
+            hipLaunchKernelGGL(gl_sssp_kernel, dim3(B), dim3(GL_NT), 0, st, H, W, grids, (long)H * W, sources, wi0, wj0, wh,
+                               ww, ps.p, cells, dists, g_fault_dev);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(SIMAPS_EHIP, "sssp_grid (large window) launch: %s", hipGetErrorString(e));
         return 0;

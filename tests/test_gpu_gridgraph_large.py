@@ -164,3 +164,82 @@ def test_gridgraph_large_narrow_windows(M, w):
             assert _dp_tie(grid, src, t), (w, src, t)
             n_tie += 1
     assert n_tie <= 1
+
+
+def test_gridgraph_large_tile_seams(M):
+    """The tiled fixpoint (csrc/grid_large.h gl_tile_kernel, 62 x 62 tiles): windows of whole tiles
+    (124 x 186) and with one-cell partial tiles (125 x 187), sources on tile corners and seams, a
+    diagonal wall that every path crosses seams along: images and paths equal the oracle's."""
+    batch, vector_env = M
+    rs = np.random.RandomState(62)
+    for h, w in ((124, 186), (125, 187)):
+        grid = (rs.random_sample((h, w)) > 0.3).astype(np.uint8)
+        for k in range(min(h, w) - 20):                                          # a diagonal wall with one gap
+            if k != 40:
+                grid[k + 10, k + 15] = 0
+        gg = vector_env.GridGraph(grid)
+        assert gg.large
+        for src in ((61, 61), (62, 62), (61, 62), (0, w - 1), (h - 1, w - 1), (h - 1, 0)):
+            grid[src] = 1
+            gg = vector_env.GridGraph(grid)
+            assert _bitwise(gg.shortest_path_image(src), O.spfa_image(grid, src)), ((h, w), src)
+        free = np.argwhere(grid != 0)
+        src = (62, 62)
+        tgts = [tuple(int(x) for x in free[rs.randint(len(free))]) for _ in range(6)]
+        for t, p in zip(tgts, gg.shortest_paths([(src, t) for t in tgts])):
+            want = O.grid_shortest_path(grid, src, t)
+            if not np.array_equal(np.array(p, dtype=np.int64).reshape(-1, 2), np.array(want, dtype=np.int64).reshape(-1, 2)):
+                assert _dp_tie(grid, src, t), ((h, w), src, t)
+
+
+def test_whole_window_sweeps_fallback(M):
+    """Windows beyond GT_MAXT tiles (>= ~3,968^2 cells) keep the whole-window sweeps (gl_sssp_kernel).
+    No test-sized window gets there, so the diagnostic ring build (libsimaps_diagring.so, built with
+    SIMAPS_GL_TILE=0) runs every large window through them: images bitwise the oracle's, paths equal
+    the product library's (same replay on the same fixpoint)."""
+    batch, vector_env = M
+    import os
+    from simaps import _lib
+    L = _lib._load(os.path.join(os.path.dirname(_lib.__file__), 'libsimaps_diagring.so'))
+    rs = np.random.RandomState(505)
+    for name, grid in _big_grids(rs):
+        if name not in ('rand40', 'serpentine'):
+            continue
+        H, W = grid.shape
+        free = np.argwhere(grid != 0)
+        srcs = free[rs.randint(len(free), size=2)].astype(np.int32)
+        g = torch.from_numpy(grid).cuda().unsqueeze(0).expand(2, H, W).contiguous()
+        s = torch.from_numpy(srcs).cuda()
+        out = torch.empty((2, H, W), dtype=torch.float32, device='cuda')
+        _lib.check(L.simaps_sssp_grid(2, H, W, _lib.ptr(g), _lib.ptr(s), _lib.ptr(out), 0, 0, H, W,
+                                      _lib.stream_handle(None)), L)
+        got = out.cpu().numpy()
+        for k in range(2):
+            assert _bitwise(got[k], O.spfa_image(grid, tuple(srcs[k]))), (name, k)
+        tg = torch.from_numpy(free[rs.randint(len(free), size=2)].astype(np.int32)).cuda()
+        ij = torch.empty((2, 512, 2), dtype=torch.int32, device='cuda')
+        cnt = torch.empty((2,), dtype=torch.int32, device='cuda')
+        _lib.check(L.simaps_grid_path(2, H, W, _lib.ptr(g), _lib.ptr(s), _lib.ptr(tg), 0, 0, H, W, 512, _lib.ptr(ij),
+                                      _lib.ptr(cnt), _lib.stream_handle(None)), L)
+        ij2, cnt2 = batch.launch_grid_paths(g, s, tg, max_points=512)
+        torch.cuda.synchronize()
+        assert torch.equal(cnt, cnt2) and all(torch.equal(ij[k, :int(cnt[k])], ij2[k, :int(cnt2[k])]) for k in range(2))
+
+
+def test_gridgraph_large_walled_corner_source(M):
+    """A source on its tile's corner cell whose only way out is the diagonal into the next tile
+    (every other neighbour blocked): the source's own 0 must count as a change of that tile's corner,
+    or the diagonal tile is never queued (the tiled fixpoint's initial condition)."""
+    batch, vector_env = M
+    grid = np.ones((130, 130), np.uint8)
+    for s, exit_ in (((61, 61), (62, 62)), ((61, 62), (60, 61)), ((62, 61), (63, 60))):
+        g = grid.copy()
+        for di in (-1, 0, 1):
+            for dj in (-1, 0, 1):
+                if (di or dj) and (s[0] + di, s[1] + dj) != exit_:
+                    g[s[0] + di, s[1] + dj] = 0
+        gg = vector_env.GridGraph(g)
+        assert gg.large
+        img = gg.shortest_path_image(s)
+        assert _bitwise(img, O.spfa_image(g, s)), s
+        assert (img > 0).sum() > 10000, s

@@ -370,9 +370,10 @@ def bench_gridgraph_large(n=500, density=0.25, seed=505):
                       'gpu_path_ms': {str(B): v[1] * 1e3 for B, v in rows.items()},
                       'gpu_paths_per_s_at_64': 64 / rows[64][1],
                       'cpu_oracle_image_ms': cpu_img * 1e3, 'cpu_oracle_path_ms': cpu_path * 1e3, 'cpu_cores': 1,
-                      'note': 'image: gl_sssp_kernel (directional sweeps in L2); path: the sweeps + gl_path_kernel '
-                              '(one wave replays the SPFA, early exit at the target chain); the SPFA is serial, '
-                              'one L2 round trip per pop'}), flush=True)
+                      'note': 'image: gl_tile_kernel (62 x 62 tiles in LDS, a queue of dirty tiles, four groups '
+                              'of four waves; gl_sssp_kernel whole-window sweeps beyond 4,096 tiles); path: that '
+                              'fixpoint + gl_path_kernel (one wave replays the SPFA, early exit at the target chain); '
+                              'the SPFA is serial, one L2 round trip per pop'}), flush=True)
 
 
 if __name__ == '__main__':
