@@ -7,7 +7,7 @@
 #
 # Steps (extra arguments after '=' are appended to the step's command, e.g. fuzz_rows=--path-mode=4):
 #   pytest smoke bench bench20 prof configs extra env mixed large spawn2 rccl
-#   fuzz_states fuzz_states_plain fuzz_mixed fuzz_rows fuzz_ingest
+#   fuzz_states fuzz_states_plain fuzz_mixed fuzz_rows fuzz_ingest fuzz_large
 #   phase (needs the stamp build: make -C spatial-intention-maps_amd/csrc prof first)
 # Environment: SEED0 (fuzz seed base, default 50000).  pytest=a.py,b.py runs those test files instead of tests/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -36,6 +36,7 @@ for step in "$@"; do
     fuzz_mixed)        c="900|SIMAPS_FUZZ_SEED0=$seed0 python tools/fuzz_states.py 512 16 --perturb --mixed" ;;
     fuzz_rows)         c="600|python tools/fuzz_rows.py --seed0 $seed0 256 4 16" ;;
     fuzz_ingest)       c="600|SIMAPS_FUZZ_SEED0=$seed0 python tools/fuzz_ingest.py 128 16" ;;
+    fuzz_large)        c="600|python tools/fuzz_large.py 96 $seed0" ;;
     phase)   c="120|python tools/phase_profile.py --dump gpurun_out/${tag}_stamps.npy" ;;
     *) echo "unknown step $name" >&2; exit 2 ;;
   esac
