@@ -204,8 +204,9 @@ __global__ void __launch_bounds__(GL_NT) gl_sssp_kernel(int H, int W, const uint
 // tools/tile_sssp_model.py (~2.3 processings per tile, ~2.2 sweep rounds per processing on 500^2).
 constexpr int GT_TT = 62;                       // tile interior side: one cell per lane (span <= 63)
 constexpr int GT_TP = 65;                       // LDS pitch of a tile buffer (odd: column sweeps spread over banks)
-constexpr int GT_PAD = 8;                       // rows of slack around a buffer: sweep_t's prefetch reads <= 6 lines
-constexpr int GT_BUF = (GT_TT + 2 + 2 * GT_PAD) * GT_TP;  // floats per group buffer  //  past either end
+constexpr int GT_PAD = 8;                       // rows of slack around a buffer (sweep_t's prefetch reads up to
+                                                //  6 lines past either end of the tile)
+constexpr int GT_BUF = (GT_TT + 2 + 2 * GT_PAD) * GT_TP;  // floats per group buffer
 constexpr int GT_GROUPS = 4;
 constexpr int GT_NT = 256 * GT_GROUPS;
 constexpr int GT_MAXT = 4096;                   // tiles per window (larger windows: gl_sssp_kernel)
@@ -394,6 +395,10 @@ __global__ void __launch_bounds__(GT_NT) gl_tile_kernel(int H, int W, const uint
     const int si = sources[2 * b], sj = sources[2 * b + 1];
     const bool s_in = si >= wi0 && si < wi0 + wh && sj >= wj0 && sj < wj0 + ww && grid[(long)si * W + sj] != 0;
     const int ntj = (ww + GT_TT - 1) / GT_TT, nt = gt_tiles(wh, ww);
+    if (nt > GT_MAXT) {  // (the host dispatches such windows to gl_sssp_kernel: a guard for the LDS tables)
+        if (tid == 0) post_faults(fault, SIMAPS_FAULT_DESCRIPTOR);
+        return;
+    }
     // (rows by wave, columns by lane: no 64-bit index division)
     for (int r = tid >> 6; r < wh + 2; r += GT_NT / 64) {
         const uint8_t *grow = grid + (long)(wi0 + r - 1) * W + wj0 - 1;
