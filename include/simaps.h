@@ -334,8 +334,10 @@ int simaps_ingest(const simaps_config *cfg, const simaps_camera *cam, int N, con
  *   float32 (-1 unreachable, like pyx:110-112), all DEVICE.  All free cells of every grid must lie
  *   in the window rows [wi0, wi0+wh) x cols [wj0, wj0+ww) (cells outside it are treated as blocked).
  *   A window with (wh+2)*((ww+2)|1) <= SIMAPS_MAX_ROOM_CELLS and ww <= SIMAPS_MAX_ROOM_W runs the
- *   LDS-resident kernel; any larger one the global-memory sweeps (same results; scratch from the
- *   library's stream-ordered pool, so SIMAPS_EUNSUPPORTED while `stream` is being captured). */
+ *   LDS-resident kernel; any larger one the global-memory kernels: the tiled fixpoint (62 x 62-cell
+ *   tiles through LDS from a queue of dirty tiles) up to 4,096 tiles, the whole-window sweeps beyond
+ *   (same results; scratch from the library's stream-ordered pool, so SIMAPS_EUNSUPPORTED while
+ *   `stream` is being captured). */
 int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *sources, float *dists,
                      int wi0, int wj0, int wh, int ww, void *stream);
 
@@ -345,7 +347,7 @@ int simaps_sssp_grid(int B, int H, int W, const uint8_t *grids, const int32_t *s
  *   [B] = number of waypoints, or -needed if max_points is too small.  All DEVICE.  The SPFA replays
  *   pyx:69-114 (edge order, SLF swap), so parents -- and waypoints -- are the reference's; the
  *   line-of-sight pruning counts cells with grid != 1 as blocked (uint8 `1 - grid`, pyx:146).  The
- *   window rule of simaps_sssp_grid applies (larger windows: the global-memory sweeps, then one
+ *   window rule of simaps_sssp_grid applies (larger windows: the global-memory fixpoint, then one
  *   wave per query replays the SPFA).  An unreachable target gives [target] (pyx:136-137). */
 int simaps_grid_path(int B, int H, int W, const uint8_t *grids, const int32_t *sources, const int32_t *targets,
                      int wi0, int wj0, int wh, int ww, int max_points, int32_t *out_ij, int32_t *out_count,
