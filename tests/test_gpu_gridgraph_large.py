@@ -243,3 +243,27 @@ def test_gridgraph_large_walled_corner_source(M):
         img = gg.shortest_path_image(s)
         assert _bitwise(img, O.spfa_image(g, s)), s
         assert (img > 0).sum() > 10000, s
+
+
+def test_gridgraph_large_window_offset(M):
+    """Free cells that start away from the grid's origin (a blocked margin of 7 rows / 11 columns, and
+    a blocked grid corner beyond the window): the window (i0, j0, h, w) the drop-in derives is offset,
+    and the tiled fixpoint's tiles, halo and source cell follow it -- images and paths equal the oracle's."""
+    batch, vector_env = M
+    rs = np.random.RandomState(711)
+    grid = np.zeros((300, 400), np.uint8)
+    grid[7:280, 11:390] = (rs.random_sample((273, 379)) > 0.3).astype(np.uint8)
+    gg = vector_env.GridGraph(grid)
+    assert gg.large and gg.window[:2] != (0, 0), gg.window
+    free = np.argwhere(grid != 0)
+    srcs = [tuple(int(x) for x in free[0]), tuple(int(x) for x in free[-1]), (7 + 61, 11 + 62)]
+    grid[srcs[2]] = 1
+    gg = vector_env.GridGraph(grid)
+    imgs = gg.shortest_path_images(srcs).cpu().numpy()
+    for s, img in zip(srcs, imgs):
+        assert _bitwise(img, O.spfa_image(grid, s)), s
+    tgts = [tuple(int(x) for x in free[rs.randint(len(free))]) for _ in range(4)]
+    for t, p in zip(tgts, gg.shortest_paths([(srcs[2], t) for t in tgts])):
+        want = O.grid_shortest_path(grid, srcs[2], t)
+        if not np.array_equal(np.array(p, dtype=np.int64).reshape(-1, 2), np.array(want, dtype=np.int64).reshape(-1, 2)):
+            assert _dp_tie(grid, srcs[2], t), t
