@@ -424,7 +424,9 @@ __global__ void __launch_bounds__(GT_NT) gl_tile_kernel(int H, int W, const uint
     const int gi = tid >> 8;
     const Group grp{tid & 255, 256, sh.bar[gi], 4};
     lds_float *L = (lds_float *)(tiles + gi * GT_BUF + GT_PAD * GT_TP);  // (ds_* addressing)
-    const unsigned cap = 64u * (unsigned)nt + 4096u;  // processings (a bug guard: ~2-3 per tile measured)
+    // processings: a bug guard.  Random grids take 2-3 per tile; a spiral corridor with 1-cell walls
+    // crosses every tile ~31 times each way and takes ~60 (tools/tile_sssp_model.py), so 4x that.
+    const unsigned cap = 256u * (unsigned)nt + 4096u;
     bool again = false;
     int cur = -1;
     for (;;) {

@@ -267,3 +267,33 @@ def test_gridgraph_large_window_offset(M):
         want = O.grid_shortest_path(grid, srcs[2], t)
         if not np.array_equal(np.array(p, dtype=np.int64).reshape(-1, 2), np.array(want, dtype=np.int64).reshape(-1, 2)):
             assert _dp_tie(grid, srcs[2], t), t
+
+
+def _spiral(n, gap):
+    """A rectangular spiral corridor (1 cell wide, walls gap - 1 thick) from the corner (0, 0)."""
+    g = np.zeros((n, n), np.uint8)
+    top, left, bot, right = 0, 0, n - 1, n - 1
+    g[0, :] = 1
+    while bot - top >= gap and right - left >= gap:
+        g[top:bot + 1, right] = 1
+        g[bot, left:right + 1] = 1
+        g[top + gap:bot + 1, left] = 1
+        top += gap
+        g[top, left:right - gap + 1] = 1
+        left += gap
+        right -= gap
+        bot -= gap
+    return g
+
+
+def test_gridgraph_large_spiral(M):
+    """The tiled fixpoint's worst case: a 300 x 300 spiral corridor with 1-cell walls passes through
+    every tile ~31 times each way (~58 processings per tile in the host model; random grids take
+    2-3): the image equals the oracle's, with no fault (the processing cap is a bug guard only)."""
+    batch, vector_env = M
+    g = _spiral(300, 2)
+    gg = vector_env.GridGraph(g)
+    assert gg.large
+    for src in ((0, 0), (150, 150)):
+        if g[src]:
+            assert _bitwise(gg.shortest_path_image(src), O.spfa_image(g, src)), src

@@ -22,6 +22,17 @@ def test_tiled_fixpoint_equals_the_oracle(tt):
     m[::8, 1:] = 0
     m[4::16, :-1] = 1
     grids.append(m)
+    sp = np.zeros((60, 60), np.uint8)                                  # spiral corridor, 1-cell walls
+    top, left, bot, right = 0, 0, 59, 59
+    sp[0, :] = 1
+    while bot - top >= 2 and right - left >= 2:
+        sp[top:bot + 1, right] = 1
+        sp[bot, left:right + 1] = 1
+        sp[top + 2:bot + 1, left] = 1
+        top += 2
+        sp[top, left:right - 1] = 1
+        left, right, bot = left + 2, right - 2, bot - 2
+    grids.append(sp)
     for grid in grids:
         free = np.argwhere(grid != 0)
         for src in (tuple(free[0]), tuple(free[rs.randint(len(free))]), tuple(free[-1])):
