@@ -220,7 +220,8 @@ struct GtShared {
     int gtile[GT_GROUPS];                       // the tile a group works on next (-1: done)
     unsigned chg[GT_GROUPS][3];                 // per group, per round: a sweep lowered a cell
     unsigned emask[GT_GROUPS];                  // per group: which edges / corners of its tile fell
-};
+    uint64_t gdm[GT_GROUPS][4];                 // per group and sweep direction: lines to relax out of
+};                                              //  again (bit L - 1 = line L; a tile has <= 62 lines)
 __host__ __device__ constexpr int gt_tiles(int wh, int ww) { return ((wh + GT_TT - 1) / GT_TT) * ((ww + GT_TT - 1) / GT_TT); }
 
 __device__ __forceinline__ unsigned gt_lds_ld(const unsigned *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -289,13 +290,47 @@ __device__ __forceinline__ bool gt_finish(GtShared &sh, int t)
     return false;
 }
 
-// one whole directional sweep of the tile's interior (sweep_t: the halo is not read; the edge cells
-// took it beforehand).  (The get_state kernels' inline-asm loop, sweep_asm, measured the same here:
-// 1.08 vs 1.05 ms per 500^2 image, profiles/r6r_large_*.jsonl.)
+// One directional sweep of the tile's interior over its dirty lines only: the get_state kernels'
+// dirty-line rule (simaps.hip sweep()) with the inline-asm step loop at the tile pitch.  The wave
+// snapshot-clears its direction's mask, sweeps from the first dirty line and stops at the first
+// non-improving group of 4 lines past the last one; it marks the lines it lowered for the opposite
+// direction and the lines of its improving lanes for the two perpendicular ones.  Marks follow the
+// sweep's own writes (the asm drains them) and the snapshot precedes its reads, so a decrease is
+// either seen or left marked; a round without improvement leaves every mask empty = the tile's local
+// fixpoint.  A tile's first lines to sweep are those of the edge cells its halo lowered (and the
+// source's), so a small halo change costs a small sweep.  (Whole sweeps with sweep_t: 1.05 ms per
+// 500^2 image, r6x.)
 template <int DIR>
-__device__ __forceinline__ bool gt_sweep(lds_float *L, int th, int tw)
+__device__ __forceinline__ bool gt_sweep(lds_float *L, int th, int tw, uint64_t *dm)
 {
-    return DIR < 2 ? sweep_t<DIR, 1, GT_TP>(L, th, tw, GT_TP) : sweep_t<DIR, 1, GT_TP>(L, tw, th, GT_TP);
+    constexpr bool VERT = DIR < 2, FWD = (DIR & 1) == 0;
+    const int len = VERT ? th : tw, span = VERT ? tw : th;
+    uint64_t m = 0;
+    if ((threadIdx.x & 63) == 0) m = __hip_atomic_exchange(&dm[DIR], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
+    if (!m) return false;
+    const int blo = __builtin_ctzll(m), bhi = 63 - __builtin_clzll(m);
+    const int t0 = FWD ? blo : len - 1 - bhi, tmax = FWD ? bhi : len - 1 - blo;  // step t: line FWD ? t + 1 : len - t
+    const SweepOut o = sweep_asm<DIR, 1, GT_TP>(L, len, span, t0, tmax, len);
+    if (!o.lanes) return false;
+    if ((threadIdx.x & 63) == 0) {
+        const int a = FWD ? o.imin : len - 1 - o.imax, b = FWD ? o.imax : len - 1 - o.imin;
+        __hip_atomic_fetch_or(&dm[DIR ^ 1], bits64(max(a, 0), min(b, 63)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        constexpr int P = VERT ? 2 : 0;  // lane i owns line i + 1 of the perpendicular directions
+        __hip_atomic_fetch_or(&dm[P], o.lanes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_or(&dm[P + 1], o.lanes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return true;
+}
+
+// a changed cell (row a, column b of the tile, 1-based) dirties its row for the vertical sweeps and its
+// column for the horizontal ones
+__device__ __forceinline__ void gt_mark_lines(uint64_t *dm, int a, int b)
+{
+    __hip_atomic_fetch_or(&dm[0], 1ull << (a - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(&dm[1], 1ull << (a - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(&dm[2], 1ull << (b - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(&dm[3], 1ull << (b - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // One group's processing of tile (ti, tj): load with halo -> edge relaxation -> sweep rounds -> write-back.
@@ -337,12 +372,18 @@ __device__ __forceinline__ unsigned gt_process(GtShared &sh, lds_float *L, float
         const float s0 = fabsf(L[ha * GT_TP + hb]) + 1.0f;
         const float s1 = fabsf(L[(ha - da) * GT_TP + hb - db]) + SQRT2F;
         const float s2 = fabsf(L[(ha + da) * GT_TP + hb + db]) + SQRT2F;
-        lds_min(L + a * GT_TP + b, fminf(fminf(s0, s1), s2));  // (blocked cells keep -inf)
+        const float m = fminf(fminf(s0, s1), s2);
+        if (m < L[a * GT_TP + b]) {  // (blocked cells hold -inf: never) its row and column are dirty
+            lds_min(L + a * GT_TP + b, m);
+            gt_mark_lines(sh.gdm[gi], a, b);
+        }
     }
+    if (t == 0 && sa > 0) gt_mark_lines(sh.gdm[gi], sa, sb);  // (the source's 0, set above)
     grp.sync();
     for (int round = 0;; round++) {
-        const bool c = dir == 0 ? gt_sweep<0>(L, th, tw) : dir == 1 ? gt_sweep<1>(L, th, tw)
-                     : dir == 2 ? gt_sweep<2>(L, th, tw) : gt_sweep<3>(L, th, tw);
+        uint64_t *dm = sh.gdm[gi];
+        const bool c = dir == 0 ? gt_sweep<0>(L, th, tw, dm) : dir == 1 ? gt_sweep<1>(L, th, tw, dm)
+                     : dir == 2 ? gt_sweep<2>(L, th, tw, dm) : gt_sweep<3>(L, th, tw, dm);
         if (c && (t & 63) == 0) __hip_atomic_store(&sh.chg[gi][round % 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (t == 0) __hip_atomic_store(&sh.chg[gi][(round + 1) % 3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // (read 2 syncs ago)
         grp.sync();
@@ -439,6 +480,7 @@ __global__ void __launch_bounds__(GT_NT) gl_tile_kernel(int H, int W, const uint
             sh.gtile[gi] = cur;
             sh.chg[gi][0] = sh.chg[gi][1] = sh.chg[gi][2] = 0u;
             sh.emask[gi] = 0u;
+            sh.gdm[gi][0] = sh.gdm[gi][1] = sh.gdm[gi][2] = sh.gdm[gi][3] = 0ull;
         }
         grp.sync();
         const int tile = __builtin_amdgcn_readfirstlane(sh.gtile[gi]);  // (wave-uniform)
