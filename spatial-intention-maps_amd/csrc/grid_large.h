@@ -47,6 +47,10 @@ __device__ __forceinline__ void gl_sti(int *p, int v) { __hip_atomic_store(p, v,
 // every store / atomic of this wave has reached L2 before the next load issues
 __device__ __forceinline__ void gl_drain() { __builtin_amdgcn_s_waitcnt(0); }
 
+// lane k's value (k wave-uniform) in every lane
+__device__ __forceinline__ int gl_lane(int x, int k) { return __builtin_amdgcn_readlane(x, k); }
+__device__ __forceinline__ float gl_lane(float x, int k) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), k)); }
+
 // lane i <- lane i - 1 (lane 0 <- edge) / lane i <- lane i + 1 (lane 63 <- edge): DPP wave_shr:1 /
 // wave_shl:1 with bound_ctrl off, so the lane without a source keeps the `old` operand
 __device__ __forceinline__ float gl_from_prev_lane(float v, float edge)
@@ -628,11 +632,13 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
         const int third_l = (lane == 9 && cnt >= 3) ? queue[q3] : -1;
         const float dfr_l = (lane == 10 && cnt >= 2) ? dist[s2] : 0.0f;
         const long fr = cnt >= 2 ? s2 : -1;  // the front after this pop (queue[head + 1])
-        const long third = __shfl(third_l, 9);
-        const float dfr = __shfl(dfr_l, 10);  // its distance before this pop
+        // (lane values to the wave by v_readlane, uniform lane index: a ds_bpermute (__shfl) is an LDS
+        // round trip on the pop's serial chain, several per pop)
+        const long third = gl_lane(third_l, 9);
+        const float dfr = gl_lane(dfr_l, 10);  // its distance before this pop
         qh = q2;
         cnt--;
-        const float du = __shfl(dv, 8);
+        const float du = gl_lane(dv, 8);
         const float nd = du + wl;
         const bool imp = lane < 8 && nd < dv;
         if (imp) {
@@ -650,9 +656,9 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
         while (todo) {
             const int k = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const long vk = __shfl(v, k);
-            const float ndk = __shfl(nd, k);
-            if (__shfl(pv, k) & GL_INQ) {  // the front itself improved (queued: no push)
+            const long vk = gl_lane((int)v, k);  // (a cell index < 2^31: H, W <= 32767)
+            const float ndk = gl_lane(nd, k);
+            if (gl_lane(pv, k) & GL_INQ) {  // the front itself improved (queued: no push)
                 if (vk == f) df = ndk;
                 continue;
             }
