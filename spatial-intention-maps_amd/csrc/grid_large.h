@@ -602,20 +602,23 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
     // reference's linear queue holds 8 V entries (pyx:78), so its SPFA never pops more than that.
     const long pop_cap = SIMAPS_POP_CAP > 8L * wh * ww + 1 ? (long)SIMAPS_POP_CAP : 8L * wh * ww + 1;
     const int k8 = lane < 8 ? lane : 8;
-    const long off = lane < 8 ? gl_dir_off(lane, P) : 0;  // lane 8: the popped vertex itself
+    const int off = lane < 8 ? (int)gl_dir_off(lane, P) : 0;  // lane 8: the popped vertex itself
     const float wl = (lane >= 2 && lane < 8 && lane != 3 && lane != 6) ? SQRT2F : 1.0f;
     // the queue: live slots qh .. qt (mod QR), cnt entries; its front u and (cnt >= 2) second s2 are
     // kept in registers, so a pop's reads -- u's edge heads, the entry after s2, s2's distance -- go
     // out together in one round
-    const long QR = n1;
-    long qh = 0, qt = 0, cnt = 1, u = su, s2 = -1;
+    // (cell and slot indices in 32 bits: a window has < 2^31 padded cells, H, W <= 32767; 64-bit index
+    // arithmetic was a good part of each pop's serial instruction stream)
+    const int QR = (int)n1;
+    int qh = 0, qt = 0, cnt = 1, u = (int)su, s2 = -1;
     long pops = 0, lim = GL_CHECK;
     // Early exit, incremental (round 6): the chain from the target up to (not including) wchk holds its
     // fixpoint distances, so its parents can no longer change (pyx:97-99 sets a parent only on a strict
     // improvement) and each check resumes at wchk instead of walking the chain again.  (Round 5
     // re-walked it at doubling intervals, 64, 128, ... pops, and so stopped up to twice as late:
     // modelled on 500^2 grids, the chain was final after 54-91 % of the pops the old schedule ran.)
-    long wchk = tv, chk_steps = 0;
+    int wchk = (int)tv;
+    long chk_steps = 0;
     bool early = false;
     // an unreachable (+inf) or blocked (-inf) target never gets a parent (pin[tv] stays 0 unless it is
     // the source): the path is [target] whatever the SPFA does, so it is not run
@@ -625,16 +628,16 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
 #endif
     while (cnt > 0) {
         // (2) pop u; its edges in pyx order on lanes 0-7 (pyx:89-101), lane 8 u itself
-        const long q2 = qh + 1 == QR ? 0 : qh + 1, q3 = q2 + 1 == QR ? 0 : q2 + 1;
-        const long v = u + off;
+        const int q2 = qh + 1 == QR ? 0 : qh + 1, q3 = q2 + 1 == QR ? 0 : q2 + 1;
+        const int v = u + off;
         const float dv = lane <= 8 ? dist[v] : 0.0f;
         const int pv = lane <= 8 ? pin[v] : 0;
         const int third_l = (lane == 9 && cnt >= 3) ? queue[q3] : -1;
         const float dfr_l = (lane == 10 && cnt >= 2) ? dist[s2] : 0.0f;
-        const long fr = cnt >= 2 ? s2 : -1;  // the front after this pop (queue[head + 1])
+        const int fr = cnt >= 2 ? s2 : -1;  // the front after this pop (queue[head + 1])
         // (lane values to the wave by v_readlane, uniform lane index: a ds_bpermute (__shfl) is an LDS
         // round trip on the pop's serial chain, several per pop)
-        const long third = gl_lane(third_l, 9);
+        const int third = gl_lane(third_l, 9);
         const float dfr = gl_lane(dfr_l, 10);  // its distance before this pop
         qh = q2;
         cnt--;
@@ -650,13 +653,13 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
         // distance as of each edge: lowered by this pop's own edge to it, if any.  Queued heads are
         // never pushed (the original front too, also after a swap moved it to the tail).
         uint64_t todo = __ballot(imp && ((pv & GL_INQ) == 0 || v == fr));
-        long f = fr, nsec = cnt >= 2 ? third : -1;
-        const long q2n = qh + 1 == QR ? 0 : qh + 1;  // the slot after the front
+        int f = fr, nsec = cnt >= 2 ? third : -1;
+        const int q2n = qh + 1 == QR ? 0 : qh + 1;  // the slot after the front
         float df = dfr;
         while (todo) {
             const int k = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const long vk = gl_lane((int)v, k);  // (a cell index < 2^31: H, W <= 32767)
+            const int vk = gl_lane(v, k);
             const float ndk = gl_lane(nd, k);
             if (gl_lane(pv, k) & GL_INQ) {  // the front itself improved (queued: no push)
                 if (vk == f) df = ndk;
@@ -664,7 +667,7 @@ __global__ void __launch_bounds__(64) gl_path_kernel(int H, int W, const uint8_t
             }
             qt = qt + 1 == QR ? 0 : qt + 1;
             cnt++;
-            long content = vk;
+            int content = vk;
             if (cnt == 1) {  // (the queue was empty: tail == head + 1 == this slot)
                 f = vk;
                 df = ndk;
