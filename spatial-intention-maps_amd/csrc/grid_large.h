@@ -445,15 +445,22 @@ __global__ void __launch_bounds__(GT_NT) gl_tile_kernel(int H, int W, const uint
         if (tid == 0) post_faults(fault, SIMAPS_FAULT_DESCRIPTOR);
         return;
     }
-    // (rows by wave, columns by lane: no 64-bit index division)
+    // (rows by wave, columns by lane: no 64-bit index division; four independent loads in flight per
+    // lane before their stores)
     for (int r = tid >> 6; r < wh + 2; r += GT_NT / 64) {
         const uint8_t *grow = grid + (long)(wi0 + r - 1) * W + wj0 - 1;
         float *drow = D + (long)r * g.pitch;
         const bool in_r = r >= 1 && r <= wh;
-        for (int c = tid & 63; c < g.pitch; c += 64) {
-            float v = -INFINITY;
-            if (in_r && c >= 1 && c <= ww && grow[c] != 0) v = INFINITY;  // (the source too: gt_process sets it)
-            drow[c] = v;
+        for (int c0 = tid & 63; c0 < g.pitch; c0 += 256) {
+            unsigned gb[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int c = c0 + 64 * q;
+                gb[q] = (in_r && c >= 1 && c <= ww) ? grow[c] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)  // (the source too is +inf here: gt_process sets it)
+                if (c0 + 64 * q < g.pitch) drow[c0 + 64 * q] = gb[q] ? INFINITY : -INFINITY;
         }
     }
     for (int k = tid; k < nt; k += GT_NT) sh.ring[k] = GT_EMPTY;
@@ -522,15 +529,24 @@ __global__ void __launch_bounds__(GT_NT) gl_tile_kernel(int H, int W, const uint
     for (int i = tid >> 6; i < H; i += GT_NT / 64) {
         float *orow = out + (long)b * H * W + (long)i * W;
         const int r = i - wi0;
+        const bool rin = r >= 0 && r < wh;
         const float *drow = D + (long)(r + 1) * g.pitch + 1 - wj0;
-        for (int j = tid & 63; j < W; j += 64) {
-            float v = (i == si && j == sj) ? 0.0f : -1.0f;
-            const int c = j - wj0;
-            if (r >= 0 && r < wh && c >= 0 && c < ww) {
-                const float d = gl_ld(drow + j);
-                if (d >= 0.0f && d != INFINITY) v = d;
+        for (int j0 = tid & 63; j0 < W; j0 += 256) {
+            float d[4];  // (four independent loads in flight per lane before their stores)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int j = j0 + 64 * q, c = j - wj0;
+                d[q] = (rin && j < W && c >= 0 && c < ww) ? gl_ld(drow + j) : -INFINITY;
             }
-            orow[j] = v;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int j = j0 + 64 * q;
+                if (j < W) {
+                    float v = (i == si && j == sj) ? 0.0f : -1.0f;
+                    if (d[q] >= 0.0f && d[q] != INFINITY) v = d[q];
+                    orow[j] = v;
+                }
+            }
         }
     }
 }
