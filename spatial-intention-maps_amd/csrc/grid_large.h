@@ -5,7 +5,9 @@
 //
 // Same algorithm as the LDS kernels, with the arrays in global memory (L2-resident for grids up to a
 // few Mcells) and one workgroup per query:
-//   gl_sssp_kernel  the float32 fixpoint by directional sweeps (down / up / right / left, GL_WPD waves
+//   gl_tile_kernel  (round 6, windows of up to GT_MAXT tiles) the same fixpoint through 62 x 62-cell LDS
+//                   tiles taken from a queue of dirty tiles by four 4-wave groups (below)
+//   gl_sssp_kernel  (larger windows) the float32 fixpoint by directional sweeps (down / up / right / left, GL_WPD waves
 //                   each over 64-cell strips of their lines, lines prefetched ahead); every write is
 //                   an atomic min(cell, fl(d_u + w)) of a real edge, so the unique fixpoint -- the
 //                   reference SPFA's distances (pyx:69-114), bit for bit -- is reached whatever the
@@ -13,7 +15,8 @@
 //                   read proves it (values only fall; in a round without writes every read is exact).
 //   gl_path_kernel  one wave per query: the exact SPFA replay (edge order, SLF swap, pyx:89-107) with
 //                   the early exit of the LDS kernels (it stops once every vertex of the target's
-//                   parent chain holds its fixpoint distance: no parent on it can change any more),
+//                   parent chain holds its fixpoint distance: no parent on it can change any more;
+//                   checked every 64 pops, resuming the chain walk where it stopped),
 //                   the parent walk, approximate_polygon(tolerance=1) and the line-of-sight pruning
 //                   (pyx:121-154).  The SPFA is serial by definition: one round of loads per pop.
 // Padded layout per query: (wh + 2) rows x pitch = ww + 2 columns, border and blocked cells -inf,
