@@ -341,7 +341,7 @@ def bench_mixed(envs=64, steps=50):
 
 def bench_gridgraph_large(n=500, density=0.25, seed=505):
     """GridGraph(grid).shortest_path_image / shortest_path on an n x n random grid (obstacle density
-    `density`), B = 1 and 64 queries per launch, against the oracle's C SPFA (the reference's
+    `density`), B = 1, 64 and 256 queries per launch (256: one query per CU), against the oracle's C SPFA (the reference's
     algorithm, 1 core; the reference's Cython SPFA runs at about the same speed, profiles/r2_cpu_calibration.json)."""
     import oracle
     rs = np.random.RandomState(seed)
@@ -350,7 +350,7 @@ def bench_gridgraph_large(n=500, density=0.25, seed=505):
     pick = lambda k: free[rs.randint(len(free), size=k)].astype(np.int32)  # noqa: E731
     g1 = torch.from_numpy(grid).cuda()
     rows = {}
-    for B in (1, 64):
+    for B in (1, 64, 256):
         grids = g1.unsqueeze(0).expand(B, n, n).contiguous()
         srcs = torch.from_numpy(pick(B)).cuda()
         tg = pick(B)
@@ -366,9 +366,9 @@ def bench_gridgraph_large(n=500, density=0.25, seed=505):
     cpu_path = time.perf_counter() - c0
     print(json.dumps({'row': 'gridgraph_large', 'grid': '%dx%d' % (n, n), 'obstacle_density': density,
                       'gpu_image_ms': {str(B): v[0] * 1e3 for B, v in rows.items()},
-                      'gpu_images_per_s_at_64': 64 / rows[64][0],
+                      'gpu_images_per_s_at_64': 64 / rows[64][0], 'gpu_images_per_s_at_256': 256 / rows[256][0],
                       'gpu_path_ms': {str(B): v[1] * 1e3 for B, v in rows.items()},
-                      'gpu_paths_per_s_at_64': 64 / rows[64][1],
+                      'gpu_paths_per_s_at_64': 64 / rows[64][1], 'gpu_paths_per_s_at_256': 256 / rows[256][1],
                       'cpu_oracle_image_ms': cpu_img * 1e3, 'cpu_oracle_path_ms': cpu_path * 1e3, 'cpu_cores': 1,
                       'note': 'image: gl_tile_kernel (62 x 62 tiles in LDS, a queue of dirty tiles, four groups '
                               'of four waves; gl_sssp_kernel whole-window sweeps beyond 4,096 tiles); path: that '
